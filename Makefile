@@ -1,0 +1,68 @@
+# Build of the MI355X-native Nori path_mis hot path.
+#   make            product library (HIP kernels for gfx950 + host C++) and the oracle
+#   make ref        reference-side checker binaries (pcg32 demo) from /root/reference sources
+#   make clean
+# Floating point: no contraction anywhere (the reference is built without FMA;
+# SURVEY.md Appendix D shows contraction alone breaks 1e-4 parity), correctly
+# rounded fp32 div/sqrt, denormals preserved.
+
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      ?= g++
+ARCH     ?= gfx950
+PKG      := optix-renderer_amd
+LIBDIR   := $(PKG)/lib
+OBJDIR   := build/obj
+JOBS     ?= 8
+
+FP_FLAGS   := -ffp-contract=off -fno-fast-math
+HOST_FLAGS := -std=c++17 -O2 -fPIC -Wall -Wextra -Wno-unused-parameter $(FP_FLAGS) -Iinclude -I$(PKG)/host -pthread
+HIP_FLAGS  := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) $(FP_FLAGS) \
+              -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero \
+              -Iinclude -I$(PKG)/csrc -Wno-unused-result
+
+HOST_SRC := $(PKG)/host/xml_lite.cpp $(PKG)/host/scene_loader.cpp $(PKG)/host/bvh_build.cpp $(PKG)/host/image_io.cpp
+HIP_SRC  := $(PKG)/csrc/nh_kernels.hip $(PKG)/csrc/nh_api.hip
+HOST_OBJ := $(patsubst $(PKG)/host/%.cpp,$(OBJDIR)/host_%.o,$(HOST_SRC))
+HIP_OBJ  := $(patsubst $(PKG)/csrc/%.hip,$(OBJDIR)/hip_%.o,$(HIP_SRC))
+HIP_DEPS := $(wildcard $(PKG)/csrc/*.h) include/nori_hip.h
+
+LIB      := $(LIBDIR)/libnori_hip.so
+HOSTLIB  := $(LIBDIR)/libnori_host.so
+ORACLE   := oracle/_build/libnori_oracle.so
+CLI      := $(LIBDIR)/nori_hip
+
+all: $(LIB) $(HOSTLIB) $(ORACLE) $(CLI)
+
+$(OBJDIR)/host_%.o: $(PKG)/host/%.cpp $(wildcard $(PKG)/host/*.h) include/nori_hip.h
+	@mkdir -p $(OBJDIR)
+	$(CXX) $(HOST_FLAGS) -c $< -o $@
+
+$(OBJDIR)/hip_%.o: $(PKG)/csrc/%.hip $(HIP_DEPS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIP_FLAGS) -c $< -o $@
+
+# product library: host ingestion + HIP kernels + C ABI
+$(LIB): $(HOST_OBJ) $(HIP_OBJ)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+# host-only subset (scene loader, BVH builder, image I/O): usable without a GPU runtime
+$(HOSTLIB): $(HOST_OBJ)
+	@mkdir -p $(LIBDIR)
+	$(CXX) -shared -fPIC -pthread -o $@ $^
+
+$(CLI): $(PKG)/host/nori_hip_main.cpp $(LIB)
+	$(CXX) $(HOST_FLAGS) -o $@ $< -L$(LIBDIR) -lnori_hip -Wl,-rpath,'$$ORIGIN'
+
+# test infrastructure: CPU restatement of the reference path (never linked into the product)
+$(ORACLE): oracle/nori_oracle.cpp oracle/nori_oracle.h include/nori_hip.h
+	@mkdir -p oracle/_build
+	$(CXX) -std=c++17 -O2 -fPIC -pthread $(FP_FLAGS) -Iinclude -Ioracle -shared -o $@ $<
+
+ref:
+	./oracle/build_ref.sh
+
+clean:
+	rm -rf build $(LIBDIR) oracle/_build oracle/_ref
+
+.PHONY: all clean ref

@@ -1,0 +1,255 @@
+/*
+ * nori_hip.h -- C-ABI boundary of the MI355X-native Nori `path_mis` hot path.
+ *
+ * Everything crossing this boundary is plain C: PODs, pointers and sizes. No
+ * C++ types, no exceptions, no torch types. Every call returns an int status
+ * (NH_OK == 0); the message of the last failure on a context is available via
+ * nh_last_error(), and for the context-free host calls via nh_host_last_error().
+ *
+ * What each entry point replaces in the reference (rogerbarton/optix-renderer,
+ * paths relative to the reference root):
+ *
+ *   nh_scene_load_xml     loadFromXML + Scene::cloneAndInit/update
+ *                         (src/utils/parser.cpp:28-378, src/utils/scene.cpp:59-202)
+ *   nh_bvh_build          BVH::build (src/utils/bvh.cpp:54-380)
+ *   nh_create/nh_destroy  OptixState context creation (include/nori/optix/OptixState.cpp:39-74)
+ *   nh_upload_scene       OptixState::preRender scene/SBT upload
+ *                         (include/nori/optix/OptixState.render.cpp:19-85, OptixState.cpp:344-411)
+ *   nh_upload_bvh         OptixState GAS/IAS build (include/nori/optix/OptixState.as.cpp:47-248)
+ *   nh_trace_rays         BVH::rayIntersect / Scene::rayIntersect
+ *                         (src/utils/bvh.cpp:402-460, include/nori/scene.h:114-137)
+ *   nh_render             RenderThread::renderThreadMain sample loop + renderBlock + PathMISIntegrator::Li
+ *                         (src/utils/render.cpp:281-347, :421-459; src/integrators/path_mis.cpp:16-150)
+ *                         and the OptiX subframe launch (include/nori/optix/OptixState.cpp:485-510)
+ *   nh_get_framebuffer    ImageBlock master (src/utils/block.cpp:38-134); toBitmap is nh_framebuffer_to_rgb
+ *   nh_reduce_framebuffers  (new) RCCL sum of per-GPU RGBW framebuffers over xGMI
+ *
+ * Conventions (mirroring the reference's threading contract):
+ *   - input pointers are host-owned and only read during the call;
+ *   - calls on one nh_ctx are serialised by the caller; distinct contexts may be
+ *     driven from distinct host threads (one per GPU).
+ */
+#ifndef NORI_HIP_H
+#define NORI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NH_OK 0
+#define NH_ERR_INVALID 1
+#define NH_ERR_IO 2
+#define NH_ERR_DEVICE 3
+#define NH_ERR_UNSUPPORTED 4
+#define NH_ERR_STATE 5
+
+/* ---- scene description (flattened Nori scene graph) --------------------- */
+
+enum { NH_SHAPE_MESH = 0, NH_SHAPE_SPHERE = 1 };
+enum { NH_BSDF_DIFFUSE = 0, NH_BSDF_MIRROR = 1, NH_BSDF_DIELECTRIC = 2, NH_BSDF_MICROFACET = 3 };
+enum { NH_EMITTER_AREA = 0, NH_EMITTER_POINT = 1, NH_EMITTER_ENVMAP = 2 };
+enum { NH_INTEGRATOR_PATH_MIS = 0, NH_INTEGRATOR_PATH_MATS = 1 };
+
+/* One Nori Shape (src/shapes/mesh.cpp, src/shapes/sphere.cpp). Mesh data lives in
+ * the scene-wide concatenated arrays at the given offsets. */
+typedef struct nh_shape {
+    int32_t type;            /* NH_SHAPE_* */
+    int32_t bsdf;            /* index into nh_scene_desc.bsdfs (every shape has one; default diffuse 0.5) */
+    int32_t emitter;         /* index into nh_scene_desc.emitters, or -1 */
+    uint32_t v_offset;       /* first vertex in V/N/UV/T/BT */
+    uint32_t n_vertices;
+    uint32_t f_offset;       /* first face in F (face indices are local to the shape) */
+    uint32_t n_faces;
+    int32_t has_normals;     /* N present (per vertex) */
+    int32_t has_uvs;         /* UV present (per vertex); tangents T/BT present iff both */
+    float center[3];         /* sphere */
+    float radius;            /* sphere */
+    float bbox_min[3];       /* Shape::getBoundingBox() */
+    float bbox_max[3];
+    uint32_t pdf_offset;     /* mesh area DiscretePDF: n_faces+1 CDF entries in area_cdf */
+    float pdf_normalization; /* DiscretePDF::getNormalization() = 1/sum(area) */
+} nh_shape;
+
+/* One Nori BSDF (src/bsdf/{diffuse,mirror,dielectric,microfacet}.cpp). */
+typedef struct nh_bsdf {
+    int32_t type;            /* NH_BSDF_* */
+    float albedo[3];         /* diffuse: constant albedo texture */
+    float alpha;             /* microfacet: Beckmann roughness */
+    float int_ior, ext_ior;  /* dielectric / microfacet */
+    float kd[3];             /* microfacet diffuse base */
+    float ks;                /* microfacet: 1 - max(kd) */
+} nh_bsdf;
+
+/* One Nori Emitter (src/emitters/{arealight,pointlight}.cpp). */
+typedef struct nh_emitter {
+    int32_t type;            /* NH_EMITTER_* */
+    int32_t shape;           /* area light: owning shape */
+    float radiance[3];       /* area: radiance; point: power */
+    float light_prob;        /* lightWeight (emitter DiscretePDF weight) */
+    float position[3];       /* point light */
+    float pad;
+} nh_emitter;
+
+/* PerspectiveCamera after update() (src/cameras/perspective.cpp:48-96). Row-major 4x4. */
+typedef struct nh_camera {
+    int32_t width, height;
+    float sample_to_camera[16];
+    float camera_to_world[16];
+    float inv_output_size[2];
+    float near_clip, far_clip;
+    float lens_radius, focal_distance;
+} nh_camera;
+
+/* Tabulated reconstruction filter as ImageBlock::init builds it (src/utils/block.cpp:54-70). */
+typedef struct nh_filter {
+    float radius;
+    int32_t border;          /* ceil(radius - 0.5) */
+    float lookup_factor;     /* NORI_FILTER_RESOLUTION / radius */
+    float table[33];         /* NORI_FILTER_RESOLUTION + 1 entries, last = 0 */
+} nh_filter;
+
+typedef struct nh_scene_desc {
+    nh_camera camera;
+    nh_filter filter;
+    int32_t integrator;      /* NH_INTEGRATOR_* */
+    int32_t sample_count;    /* sampler sampleCount */
+    uint32_t n_shapes;
+    const nh_shape *shapes;
+    uint32_t n_bsdfs;
+    const nh_bsdf *bsdfs;
+    uint32_t n_emitters;
+    const nh_emitter *emitters;
+    const float *emitter_cdf;     /* Scene::emitterDpdf CDF, n_emitters+1 entries */
+    int32_t envmap;               /* emitter index of the environment map, or -1 */
+    uint32_t n_vertices;          /* total over all meshes */
+    const float *V;               /* 3 floats per vertex */
+    const float *N;               /* 3 per vertex (zeros for meshes without normals) */
+    const float *UV;              /* 2 per vertex */
+    const float *T;               /* 3 per vertex: accumulated tangents (mesh.cpp:165-190 uses normalised) */
+    const float *BT;              /* 3 per vertex */
+    uint32_t n_faces;
+    const uint32_t *F;            /* 3 per face, local to the owning shape */
+    uint32_t n_area_cdf;
+    const float *area_cdf;        /* concatenated per-mesh area CDFs */
+} nh_scene_desc;
+
+/* ---- BVH in the reference's own layout (include/nori/bvh.h:127-165) ---- */
+
+/* 32-byte node: word0 = flag | (size_or_axis << 1), word1 = leaf start / right child. */
+typedef struct nh_bvh_node {
+    uint32_t word0;
+    uint32_t word1;
+    float bbox_min[3];
+    float bbox_max[3];
+} nh_bvh_node;
+
+typedef struct nh_bvh_desc {
+    uint32_t n_nodes;
+    const nh_bvh_node *nodes;
+    uint32_t n_indices;           /* == primitive count */
+    const uint32_t *indices;      /* global primitive ids in leaf order */
+    uint32_t n_shapes;
+    const uint32_t *shape_offset; /* n_shapes+1 prefix sums of primitive counts (BVH::m_shapeOffset) */
+    float bbox_min[3], bbox_max[3];
+    uint32_t max_depth;           /* deepest node level (root = 0): bounds the traversal stack */
+} nh_bvh_desc;
+
+/* ---- ray batches for the traversal entry point -------------------------- */
+
+typedef struct nh_ray_soa {
+    const float *ox, *oy, *oz;
+    const float *dx, *dy, *dz;
+    const float *mint, *maxt;     /* Ray3f semantics: mint == 1e-4f triggers the adaptive epsilon */
+} nh_ray_soa;
+
+typedef struct nh_hit_soa {
+    uint8_t *hit;                 /* 0/1 */
+    float *t, *u, *v;             /* closest-hit only */
+    uint32_t *prim;               /* global primitive id, closest-hit only */
+    uint32_t *shape;              /* shape index, closest-hit only */
+} nh_hit_soa;
+
+/* ---- rendering ------------------------------------------------------------ */
+
+enum { NH_MODE_MEGAKERNEL = 0, NH_MODE_WAVEFRONT = 1 };
+enum { NH_TRAVERSAL_REFERENCE = 0, NH_TRAVERSAL_ORDERED = 1 };
+
+typedef struct nh_render_req {
+    int32_t sample_begin;         /* sample rounds [sample_begin, sample_end) */
+    int32_t sample_end;
+    uint64_t seed;                /* base of the per-(pixel, sample) pcg32 seeding contract */
+    int32_t n_blocks;             /* number of 32x32 image blocks this context renders; 0 = all */
+    const int32_t *blocks;        /* block ids (by*nbx+bx) when n_blocks > 0 */
+    int32_t mode;                 /* NH_MODE_* */
+    int32_t traversal;            /* NH_TRAVERSAL_* */
+    int32_t clear;                /* zero the framebuffer first */
+    int32_t collect_stats;        /* 1: count BVH nodes/prims visited (calibration, slower) */
+} nh_render_req;
+
+typedef struct nh_render_stats {
+    double kernel_ms_path;        /* summed device time of the path-tracing kernel(s) */
+    double kernel_ms_splat;       /* summed device time of the ImageBlock splat kernel */
+    double kernel_ms_extend;      /* wavefront: closest-hit kernel */
+    double kernel_ms_shadow;      /* wavefront: any-hit kernel */
+    double kernel_ms_shade;       /* wavefront: shading kernels */
+    uint64_t launches_path, launches_splat, launches_extend, launches_shadow, launches_shade;
+    uint64_t samples;             /* camera samples traced */
+    uint64_t ray_queries;         /* closest + any-hit queries (collect_stats) */
+    uint64_t nodes_visited;       /* BVH inner-node pops (collect_stats) */
+    uint64_t boxes_tested;        /* child boxes tested (collect_stats) */
+    uint64_t prims_tested;        /* primitive intersection tests (collect_stats) */
+    uint64_t invalid_samples;     /* ImageBlock::put drops (NaN/Inf/negative) */
+} nh_render_stats;
+
+typedef struct nh_scene nh_scene;
+typedef struct nh_bvh nh_bvh;
+typedef struct nh_ctx nh_ctx;
+
+/* host-side scene ingestion */
+int nh_scene_load_xml(const char *path, nh_scene **out);
+/* <test> roots (src/utils/ttest.cpp) hold several <scene>s: load the index-th one */
+int nh_scene_load_xml_index(const char *path, int32_t index, nh_scene **out);
+int nh_scene_get_desc(const nh_scene *scene, nh_scene_desc *out);
+/* overrides used by benchmarks and tests (camera resize recomputes the projection) */
+int nh_scene_set_resolution(nh_scene *scene, int32_t width, int32_t height);
+int nh_scene_set_sample_count(nh_scene *scene, int32_t spp);
+int nh_scene_set_bsdf(nh_scene *scene, uint32_t shape, const nh_bsdf *bsdf);
+int nh_scene_set_integrator(nh_scene *scene, int32_t integrator);
+void nh_scene_free(nh_scene *scene);
+const char *nh_host_last_error(void);
+
+int nh_bvh_build(const nh_scene_desc *scene, int32_t n_threads, nh_bvh **out);
+int nh_bvh_get_desc(const nh_bvh *bvh, nh_bvh_desc *out);
+void nh_bvh_free(nh_bvh *bvh);
+
+/* ImageBlock::toBitmap (src/utils/block.cpp:76-82): rgbw with border -> W*H*3 rgb */
+int nh_framebuffer_to_rgb(const float *rgbw, int32_t width, int32_t height, int32_t border, float *rgb);
+/* Bitmap::save equivalents: PFM (always available) and uncompressed OpenEXR */
+int nh_write_pfm(const char *path, const float *rgb, int32_t width, int32_t height);
+int nh_write_exr(const char *path, const float *rgb, int32_t width, int32_t height);
+
+/* device side */
+int nh_get_device_count(int *n);
+int nh_create(int device, nh_ctx **out);
+void nh_destroy(nh_ctx *ctx);
+int nh_upload_scene(nh_ctx *ctx, const nh_scene_desc *scene);
+int nh_upload_bvh(nh_ctx *ctx, const nh_bvh_desc *bvh);
+int nh_trace_rays(nh_ctx *ctx, const nh_ray_soa *rays, int32_t n, int32_t any_hit, int32_t traversal, nh_hit_soa *out);
+int nh_render(nh_ctx *ctx, const nh_render_req *req);
+int nh_synchronize(nh_ctx *ctx);
+int nh_get_framebuffer(nh_ctx *ctx, float *rgbw, size_t n_floats);
+/* device pointer of the (W+2b)(H+2b)x4 fp32 framebuffer, for collectives issued by the caller */
+int nh_framebuffer_device_ptr(nh_ctx *ctx, void **dptr, size_t *n_floats);
+int nh_get_stats(nh_ctx *ctx, nh_render_stats *out);
+int nh_reset_stats(nh_ctx *ctx);
+/* single-process multi-GPU: RCCL sum of the framebuffers of n contexts into ctxs[root] */
+int nh_reduce_framebuffers(nh_ctx **ctxs, int32_t n, int32_t root);
+const char *nh_last_error(const nh_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NORI_HIP_H */

@@ -1,0 +1,622 @@
+// C-ABI device side of the MI355X path_mis hot path (declared in include/nori_hip.h).
+//
+// One nh_ctx per GPU owns every device allocation: scene records, the GPU BVH, the
+// (W+2b)x(H+2b) RGBW master framebuffer and the per-chunk sample records. Rendering
+// a sample range launches, per chunk of sample rounds, the path megakernel (one
+// thread per (pixel, round)) and the ImageBlock splat gather on one HIP stream.
+// This replaces the reference's OptiX state (include/nori/optix/OptixState*.cpp) and the
+// CPU render loop (src/utils/render.cpp:232-459) behind the same plugin boundary.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "nh_internal.h"
+#include "nori_hip.h"
+
+using nhd::DBsdf;
+using nhd::DEmitter;
+using nhd::DShape;
+
+struct nh_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // host copies needed to build primitive records
+    std::vector<nh_shape> shapes;
+    std::vector<float> V;
+    std::vector<uint32_t> F;
+    int width = 0, height = 0, border = 0, n_emitters = 0, integrator = 0;
+    nh_filter filter{};
+    nhd::DScene S{};
+    nhd::Traversal tv{};
+    std::vector<void *> scene_bufs, bvh_bufs;
+    bool has_scene = false, has_bvh = false;
+    int depth = 0;
+    std::vector<uint32_t> bvh_indices, shape_offset;
+    float *fb = nullptr;
+    size_t fb_floats = 0;
+    float4 *rec = nullptr;
+    float *rec_jy = nullptr;
+    size_t rec_cap = 0;  // entries
+    int *pixel_list = nullptr, *pixel_map = nullptr, *block_rank = nullptr;
+    int n_list = 0, nbx = 0, nby = 0;
+    std::vector<int32_t> list_key;
+    bool have_list = false;
+    unsigned long long *counters = nullptr;  // queries, nodes, boxes, prims, invalid
+    nh_render_stats stats{};
+};
+
+namespace {
+
+bool fail(nh_ctx *c, const std::string &m) {
+    if (c) c->err = m;
+    return false;
+}
+
+#define HIP_TRY(ctx, expr)                                                                               \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess) {                                                                          \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                              \
+            return NH_ERR_DEVICE;                                                                        \
+        }                                                                                                \
+    } while (0)
+
+template <typename T>
+int upload(nh_ctx *c, std::vector<void *> &owner, const T *src, size_t n, const T **dst) {
+    void *p = nullptr;
+    size_t bytes = std::max<size_t>(n * sizeof(T), 16);
+    HIP_TRY(c, hipMalloc(&p, bytes));
+    owner.push_back(p);
+    if (n) HIP_TRY(c, hipMemcpyAsync(p, src, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    *dst = reinterpret_cast<const T *>(p);
+    return NH_OK;
+}
+
+void free_all(std::vector<void *> &v) {
+    for (void *p : v) hipFree(p);
+    v.clear();
+}
+
+// BlockGenerator spiral order (src/utils/block.cpp:151-199) -> rank per block id
+std::vector<int> spiral_rank(int w, int h, int bs, int &nbx, int &nby) {
+    nbx = (int)std::ceil(w / (float)bs);
+    nby = (int)std::ceil(h / (float)bs);
+    std::vector<int> rank((size_t)nbx * nby, 0);
+    int left = nbx * nby, dir = 0, bx = nbx / 2, by = nby / 2, steps_left = 1, num_steps = 1, r = 0;
+    while (left > 0) {
+        rank[(size_t)by * nbx + bx] = r++;
+        if (--left == 0) break;
+        do {
+            switch (dir) {
+                case 0: ++bx; break;
+                case 1: ++by; break;
+                case 2: --bx; break;
+                case 3: --by; break;
+            }
+            if (--steps_left == 0) {
+                dir = (dir + 1) % 4;
+                if (dir == 0 || dir == 2) ++num_steps;
+                steps_left = num_steps;
+            }
+        } while (bx < 0 || by < 0 || bx >= nbx || by >= nby);
+    }
+    return rank;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *nh_last_error(const nh_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int nh_get_device_count(int *n) {
+    if (!n) return NH_ERR_INVALID;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return NH_OK;
+}
+
+int nh_create(int device, nh_ctx **out) {
+    if (!out) return NH_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return NH_ERR_DEVICE;
+    auto *c = new nh_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->counters, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        delete c;
+        return NH_ERR_DEVICE;
+    }
+    hipMemset(c->counters, 0, 8 * sizeof(unsigned long long));
+    *out = c;
+    return NH_OK;
+}
+
+void nh_destroy(nh_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    free_all(c->scene_bufs);
+    free_all(c->bvh_bufs);
+    hipFree(c->fb);
+    hipFree(c->rec);
+    hipFree(c->rec_jy);
+    hipFree(c->pixel_list);
+    hipFree(c->pixel_map);
+    hipFree(c->block_rank);
+    hipFree(c->counters);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
+    if (!c || !d) return NH_ERR_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (d->camera.width <= 0 || d->camera.height <= 0) return fail(c, "invalid camera resolution"), NH_ERR_INVALID;
+    if (d->camera.lens_radius > 1e-4f)
+        return fail(c, "depth of field is not supported (reference uses a shared static sampler)"), NH_ERR_UNSUPPORTED;
+    if (d->envmap >= 0) return fail(c, "environment maps are not supported yet"), NH_ERR_UNSUPPORTED;
+    free_all(c->scene_bufs);
+    free_all(c->bvh_bufs);
+    c->has_scene = c->has_bvh = false;
+    c->have_list = false;
+
+    std::vector<DShape> ds(d->n_shapes);
+    for (uint32_t i = 0; i < d->n_shapes; ++i) {
+        const nh_shape &s = d->shapes[i];
+        if (s.bsdf < 0 || (uint32_t)s.bsdf >= d->n_bsdfs) return fail(c, "shape without a valid BSDF"), NH_ERR_INVALID;
+        DShape &o = ds[i];
+        std::memset(&o, 0, sizeof(o));
+        o.type = s.type;
+        o.bsdf = s.bsdf;
+        o.emitter = s.emitter;
+        o.v_off = (int)s.v_offset;
+        o.f_off = (int)s.f_offset;
+        o.n_faces = (int)s.n_faces;
+        o.has_n = s.has_normals;
+        o.has_uv = s.has_uvs;
+        o.cx = s.center[0]; o.cy = s.center[1]; o.cz = s.center[2];
+        o.radius = s.radius;
+        o.pdf_off = (int)s.pdf_offset;
+        o.pdf_norm = s.pdf_normalization;
+    }
+    std::vector<DBsdf> db(d->n_bsdfs);
+    for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
+        const nh_bsdf &b = d->bsdfs[i];
+        DBsdf &o = db[i];
+        std::memset(&o, 0, sizeof(o));
+        o.type = b.type;
+        o.ar = b.albedo[0]; o.ag = b.albedo[1]; o.ab = b.albedo[2];
+        o.alpha = b.alpha; o.int_ior = b.int_ior; o.ext_ior = b.ext_ior; o.ks = b.ks;
+        o.kr = b.kd[0]; o.kg = b.kd[1]; o.kb = b.kd[2];
+    }
+    std::vector<DEmitter> de(d->n_emitters);
+    for (uint32_t i = 0; i < d->n_emitters; ++i) {
+        const nh_emitter &e = d->emitters[i];
+        if (e.type == NH_EMITTER_ENVMAP) return fail(c, "environment maps are not supported yet"), NH_ERR_UNSUPPORTED;
+        DEmitter &o = de[i];
+        std::memset(&o, 0, sizeof(o));
+        o.type = e.type;
+        o.shape = e.shape;
+        o.lr = e.radiance[0]; o.lg = e.radiance[1]; o.lb = e.radiance[2];
+        o.px = e.position[0]; o.py = e.position[1]; o.pz = e.position[2];
+    }
+    nhd::DScene &S = c->S;
+    std::memset(&S, 0, sizeof(S));
+    int rc;
+    const size_t nv = d->n_vertices;
+    if ((rc = upload(c, c->scene_bufs, ds.data(), ds.size(), &S.shapes))) return rc;
+    if ((rc = upload(c, c->scene_bufs, db.data(), db.size(), &S.bsdfs))) return rc;
+    if ((rc = upload(c, c->scene_bufs, de.data(), de.size(), &S.emitters))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->emitter_cdf, (size_t)d->n_emitters + 1, &S.emitter_cdf))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->V, 3 * nv, &S.V))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->N, 3 * nv, &S.N))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->UV, 2 * nv, &S.UV))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->T, 3 * nv, &S.T))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->BT, 3 * nv, &S.BT))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->F, 3 * (size_t)d->n_faces, &S.F))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->area_cdf, (size_t)d->n_area_cdf, &S.area_cdf))) return rc;
+    S.n_emitters = (int)d->n_emitters;
+    S.integrator = d->integrator == NH_INTEGRATOR_PATH_MATS ? 1 : 0;
+    std::memcpy(S.s2c, d->camera.sample_to_camera, sizeof(S.s2c));
+    std::memcpy(S.c2w, d->camera.camera_to_world, sizeof(S.c2w));
+    S.inv_w = d->camera.inv_output_size[0];
+    S.inv_h = d->camera.inv_output_size[1];
+    S.near_clip = d->camera.near_clip;
+    S.far_clip = d->camera.far_clip;
+    S.width = d->camera.width;
+    S.height = d->camera.height;
+    S.filter_radius = d->filter.radius;
+    S.lookup = d->filter.lookup_factor;
+    S.border = d->filter.border;
+    std::memcpy(S.table, d->filter.table, sizeof(S.table));
+
+    c->shapes.assign(d->shapes, d->shapes + d->n_shapes);
+    c->V.assign(d->V, d->V + 3 * nv);
+    c->F.assign(d->F, d->F + 3 * (size_t)d->n_faces);
+    c->width = d->camera.width;
+    c->height = d->camera.height;
+    c->border = d->filter.border;
+    c->filter = d->filter;
+    c->n_emitters = (int)d->n_emitters;
+    c->integrator = S.integrator;
+
+    // master ImageBlock
+    hipFree(c->fb);
+    c->fb = nullptr;
+    c->fb_floats = 4 * (size_t)(c->width + 2 * c->border) * (size_t)(c->height + 2 * c->border);
+    HIP_TRY(c, hipMalloc(&c->fb, c->fb_floats * sizeof(float)));
+    HIP_TRY(c, hipMemsetAsync(c->fb, 0, c->fb_floats * sizeof(float), c->stream));
+    // block spiral ranks
+    auto rank = spiral_rank(c->width, c->height, 32, c->nbx, c->nby);
+    hipFree(c->block_rank);
+    HIP_TRY(c, hipMalloc(&c->block_rank, rank.size() * sizeof(int)));
+    HIP_TRY(c, hipMemcpyAsync(c->block_rank, rank.data(), rank.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->has_scene = true;
+    return NH_OK;
+}
+
+int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
+    if (!c || !b) return NH_ERR_INVALID;
+    if (!c->has_scene) return fail(c, "nh_upload_bvh: upload the scene first"), NH_ERR_STATE;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    free_all(c->bvh_bufs);
+    c->has_bvh = false;
+    // primitive id -> (shape, local)
+    std::vector<uint32_t> off(1, 0u);
+    for (auto &s : c->shapes) off.push_back(off.back() + (s.type == NH_SHAPE_MESH ? s.n_faces : 1u));
+    if (b->n_indices != off.back()) return fail(c, "BVH primitive count does not match the scene"), NH_ERR_INVALID;
+    if (b->n_indices > 0 && b->n_nodes == 0) return fail(c, "empty BVH for a non-empty scene"), NH_ERR_INVALID;
+
+    std::vector<float4> nodes;
+    std::vector<int2> leaves;
+    nhd::DScene &S = c->S;
+    if (b->n_nodes == 0) {
+        S.root_kind = 0;
+    } else {
+        const nh_bvh_node *N = b->nodes;
+        for (int i = 0; i < 3; ++i) { S.root_min[i] = N[0].bbox_min[i]; S.root_max[i] = N[0].bbox_max[i]; }
+        if (N[0].word0 & 1u) {
+            S.root_kind = 2;
+            leaves.push_back(make_int2((int)N[0].word1, (int)(N[0].word0 >> 1)));
+        } else {
+            S.root_kind = 1;
+            // DFS (left first) over inner nodes assigning GPU ids in visit order
+            std::vector<int> gid(b->n_nodes, -1);
+            std::vector<uint32_t> order, st{0u};
+            while (!st.empty()) {
+                uint32_t i = st.back();
+                st.pop_back();
+                if (N[i].word0 & 1u) continue;
+                gid[i] = (int)order.size();
+                order.push_back(i);
+                if (N[i].word1 >= b->n_nodes || i + 1 >= b->n_nodes)
+                    return fail(c, "corrupt BVH child index"), NH_ERR_INVALID;
+                st.push_back(N[i].word1);
+                st.push_back(i + 1);
+            }
+            nodes.resize(4 * order.size());
+            auto child_ref = [&](uint32_t ch) -> int {
+                if (N[ch].word0 & 1u) {
+                    leaves.push_back(make_int2((int)N[ch].word1, (int)(N[ch].word0 >> 1)));
+                    return ~(int)(leaves.size() - 1);
+                }
+                return gid[ch];
+            };
+            for (size_t g = 0; g < order.size(); ++g) {
+                uint32_t i = order[g];
+                const nh_bvh_node &L = N[i + 1], &R = N[N[i].word1];
+                int lr = child_ref(i + 1), rr = child_ref(N[i].word1);
+                nodes[4 * g] = make_float4(L.bbox_min[0], L.bbox_min[1], L.bbox_min[2], L.bbox_max[0]);
+                nodes[4 * g + 1] = make_float4(L.bbox_max[1], L.bbox_max[2], R.bbox_min[0], R.bbox_min[1]);
+                nodes[4 * g + 2] = make_float4(R.bbox_min[2], R.bbox_max[0], R.bbox_max[1], R.bbox_max[2]);
+                int4 r4 = make_int4(lr, rr, 0, 0);
+                std::memcpy(&nodes[4 * g + 3], &r4, sizeof(int4));
+            }
+        }
+    }
+    // primitives in leaf order
+    std::vector<float4> prims(3 * (size_t)b->n_indices);
+    for (uint32_t k = 0; k < b->n_indices; ++k) {
+        uint32_t g = b->indices[k];
+        if (g >= off.back()) return fail(c, "BVH index out of range"), NH_ERR_INVALID;
+        uint32_t s = (uint32_t)(std::upper_bound(off.begin(), off.end(), g) - off.begin()) - 1;
+        uint32_t local = g - off[s];
+        const nh_shape &sh = c->shapes[s];
+        float4 *p = &prims[3 * (size_t)k];
+        int si = (int)s, one = 1, zero = 0;
+        float fs, f1, f0;
+        std::memcpy(&fs, &si, 4);
+        std::memcpy(&f1, &one, 4);
+        std::memcpy(&f0, &zero, 4);
+        if (sh.type == NH_SHAPE_SPHERE) {
+            p[0] = make_float4(sh.center[0], sh.center[1], sh.center[2], sh.radius);
+            p[1] = make_float4(0, 0, 0, fs);
+            p[2] = make_float4(0, 0, 0, f1);
+        } else {
+            const uint32_t *f = &c->F[3 * ((size_t)sh.f_offset + local)];
+            const float *p0 = &c->V[3 * ((size_t)sh.v_offset + f[0])], *p1 = &c->V[3 * ((size_t)sh.v_offset + f[1])],
+                        *p2 = &c->V[3 * ((size_t)sh.v_offset + f[2])];
+            int li = (int)local;
+            float fl;
+            std::memcpy(&fl, &li, 4);
+            p[0] = make_float4(p0[0], p0[1], p0[2], fl);
+            p[1] = make_float4(p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2], fs);
+            p[2] = make_float4(p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2], f0);
+        }
+    }
+    int rc;
+    if ((rc = upload(c, c->bvh_bufs, nodes.data(), nodes.size(), &c->tv.nodes))) return rc;
+    if ((rc = upload(c, c->bvh_bufs, leaves.data(), leaves.size(), &c->tv.leaves))) return rc;
+    if ((rc = upload(c, c->bvh_bufs, prims.data(), prims.size(), &c->tv.prims))) return rc;
+    S.nodes = c->tv.nodes;
+    S.prims = c->tv.prims;
+    c->bvh_indices.assign(b->indices, b->indices + b->n_indices);
+    c->shape_offset = off;
+    c->depth = (int)b->max_depth + 2;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->has_bvh = true;
+    return NH_OK;
+}
+
+int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, int32_t traversal, nh_hit_soa *out) {
+    if (!c || !r || !out || n < 0) return NH_ERR_INVALID;
+    if (!c->has_bvh) return fail(c, "nh_trace_rays: no BVH uploaded"), NH_ERR_STATE;
+    if (n == 0) return NH_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    std::vector<void *> tmp;
+    const float *in[8];
+    const float *src[8] = {r->ox, r->oy, r->oz, r->dx, r->dy, r->dz, r->mint, r->maxt};
+    int rc;
+    for (int i = 0; i < 8; ++i)
+        if ((rc = upload(c, tmp, src[i], (size_t)n, &in[i]))) { free_all(tmp); return rc; }
+    RayBatch rb{in[0], in[1], in[2], in[3], in[4], in[5], in[6], in[7]};
+    HitBatch hb{};
+    void *p;
+    size_t nn = (size_t)n;
+    HIP_TRY(c, hipMalloc(&p, nn)); tmp.push_back(p); hb.hit = (uint8_t *)p;
+    HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.t = (float *)p;
+    HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.u = (float *)p;
+    HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.v = (float *)p;
+    HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.k = (int *)p;
+    nh::launch_trace(c->S, c->tv, rb, hb, n, any_hit != 0, traversal == NH_TRAVERSAL_ORDERED, false, c->depth,
+                     c->counters, c->stream);
+    HIP_TRY(c, hipGetLastError());
+    std::vector<int> k(nn);
+    HIP_TRY(c, hipMemcpyAsync(out->hit, hb.hit, nn, hipMemcpyDeviceToHost, c->stream));
+    if (!any_hit) {
+        if (out->t) HIP_TRY(c, hipMemcpyAsync(out->t, hb.t, nn * 4, hipMemcpyDeviceToHost, c->stream));
+        if (out->u) HIP_TRY(c, hipMemcpyAsync(out->u, hb.u, nn * 4, hipMemcpyDeviceToHost, c->stream));
+        if (out->v) HIP_TRY(c, hipMemcpyAsync(out->v, hb.v, nn * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(k.data(), hb.k, nn * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    free_all(tmp);
+    if (!any_hit)
+        for (size_t i = 0; i < nn; ++i) {
+            uint32_t prim = 0xffffffffu, shape = 0xffffffffu;
+            if (k[i] >= 0) {
+                prim = c->bvh_indices[(size_t)k[i]];
+                shape = (uint32_t)(std::upper_bound(c->shape_offset.begin(), c->shape_offset.end(), prim) -
+                                   c->shape_offset.begin()) - 1;
+            }
+            if (out->prim) out->prim[i] = prim;
+            if (out->shape) out->shape[i] = shape;
+        }
+    return NH_OK;
+}
+
+static int ensure_pixel_list(nh_ctx *c, const nh_render_req *q) {
+    std::vector<int32_t> key;
+    if (q->n_blocks > 0 && q->blocks) key.assign(q->blocks, q->blocks + q->n_blocks);
+    if (c->have_list && key == c->list_key) return NH_OK;
+    std::vector<int32_t> blocks = key;
+    if (blocks.empty())
+        for (int i = 0; i < c->nbx * c->nby; ++i) blocks.push_back(i);
+    std::vector<int> list, map((size_t)c->width * c->height, -1);
+    for (int32_t bid : blocks) {
+        if (bid < 0 || bid >= c->nbx * c->nby) return fail(c, "block id out of range"), NH_ERR_INVALID;
+        int bx = bid % c->nbx, by = bid / c->nbx;
+        for (int y = by * 32; y < std::min(c->height, by * 32 + 32); ++y)
+            for (int x = bx * 32; x < std::min(c->width, bx * 32 + 32); ++x) {
+                int pix = y * c->width + x;
+                if (map[pix] >= 0) return fail(c, "duplicate block id"), NH_ERR_INVALID;
+                map[pix] = (int)list.size();
+                list.push_back(pix);
+            }
+    }
+    hipFree(c->pixel_list);
+    hipFree(c->pixel_map);
+    c->pixel_list = c->pixel_map = nullptr;
+    HIP_TRY(c, hipMalloc(&c->pixel_list, std::max<size_t>(list.size(), 1) * sizeof(int)));
+    HIP_TRY(c, hipMalloc(&c->pixel_map, map.size() * sizeof(int)));
+    if (!list.empty())
+        HIP_TRY(c, hipMemcpyAsync(c->pixel_list, list.data(), list.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->pixel_map, map.data(), map.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->n_list = (int)list.size();
+    c->list_key = key;
+    c->have_list = true;
+    return NH_OK;
+}
+
+int nh_render(nh_ctx *c, const nh_render_req *q) {
+    if (!c || !q) return NH_ERR_INVALID;
+    if (!c->has_scene || !c->has_bvh) return fail(c, "nh_render: scene and BVH must be uploaded"), NH_ERR_STATE;
+    if (q->sample_end < q->sample_begin || q->sample_begin < 0) return fail(c, "invalid sample range"), NH_ERR_INVALID;
+    if (c->integrator == 0 && c->n_emitters == 0) return fail(c, "No Emitter in scene!"), NH_ERR_INVALID;
+    if (q->mode != NH_MODE_MEGAKERNEL) return fail(c, "wavefront mode is not built yet"), NH_ERR_UNSUPPORTED;
+    HIP_TRY(c, hipSetDevice(c->device));
+    int rc = ensure_pixel_list(c, q);
+    if (rc) return rc;
+    if (q->clear) HIP_TRY(c, hipMemsetAsync(c->fb, 0, c->fb_floats * sizeof(float), c->stream));
+    const int rounds = q->sample_end - q->sample_begin;
+    if (rounds == 0 || c->n_list == 0) return NH_OK;
+    // sample records per chunk of rounds (20 B per sample)
+    size_t budget = (size_t)1 << 30;
+    if (const char *e = std::getenv("NH_RECORD_BUDGET_MB")) budget = (size_t)std::max(1L, std::atol(e)) << 20;
+    size_t per_round = (size_t)c->n_list;
+    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / (per_round * 20)));
+    while ((size_t)chunk * per_round > (size_t)0x7fffffff) chunk = std::max(1, chunk / 2);
+    if (c->rec_cap < (size_t)chunk * per_round) {
+        hipFree(c->rec);
+        hipFree(c->rec_jy);
+        c->rec = nullptr;
+        c->rec_jy = nullptr;
+        c->rec_cap = (size_t)chunk * per_round;
+        HIP_TRY(c, hipMalloc(&c->rec, c->rec_cap * sizeof(float4)));
+        HIP_TRY(c, hipMalloc(&c->rec_jy, c->rec_cap * sizeof(float)));
+    }
+    if (q->collect_stats) HIP_TRY(c, hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), c->stream));
+    struct Ev {
+        hipEvent_t a, b, d;
+    };
+    std::vector<Ev> evs;
+    for (int s = q->sample_begin; s < q->sample_end; s += chunk) {
+        const int k = std::min(chunk, q->sample_end - s);
+        PathLaunch L{};
+        L.n_paths = k * c->n_list;
+        L.n_list = c->n_list;
+        L.s0 = s;
+        L.seed = q->seed;
+        L.pixel_list = c->pixel_list;
+        L.rec_rgbx = c->rec;
+        L.rec_jy = c->rec_jy;
+        L.counters = c->counters;
+        SplatLaunch P{};
+        P.fb = c->fb;
+        P.width = c->width;
+        P.height = c->height;
+        P.border = c->border;
+        P.reach = (int)std::floor(c->filter.radius + 0.5f);
+        P.nbx = c->nbx;
+        P.n_rounds = k;
+        P.n_list = c->n_list;
+        P.pixel_map = c->pixel_map;
+        P.block_rank = c->block_rank;
+        P.rec_rgbx = c->rec;
+        P.rec_jy = c->rec_jy;
+        P.radius = c->filter.radius;
+        P.lookup = c->filter.lookup_factor;
+        std::memcpy(P.table, c->filter.table, sizeof(P.table));
+        Ev ev;
+        HIP_TRY(c, hipEventCreate(&ev.a));
+        HIP_TRY(c, hipEventCreate(&ev.b));
+        HIP_TRY(c, hipEventCreate(&ev.d));
+        HIP_TRY(c, hipEventRecord(ev.a, c->stream));
+        nh::launch_path(c->S, c->tv, L, q->traversal == NH_TRAVERSAL_ORDERED, q->collect_stats != 0, c->depth, c->stream);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipEventRecord(ev.b, c->stream));
+        if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters + 4, c->stream);
+        nh::launch_splat(P, c->stream);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipEventRecord(ev.d, c->stream));
+        evs.push_back(ev);
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (auto &ev : evs) {
+        float a = 0, b = 0;
+        hipEventElapsedTime(&a, ev.a, ev.b);
+        hipEventElapsedTime(&b, ev.b, ev.d);
+        c->stats.kernel_ms_path += a;
+        c->stats.kernel_ms_splat += b;
+        c->stats.launches_path++;
+        c->stats.launches_splat++;
+        hipEventDestroy(ev.a);
+        hipEventDestroy(ev.b);
+        hipEventDestroy(ev.d);
+    }
+    c->stats.samples += (uint64_t)rounds * (uint64_t)c->n_list;
+    if (q->collect_stats) {
+        unsigned long long h[8];
+        HIP_TRY(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost));
+        c->stats.ray_queries += h[0];
+        c->stats.nodes_visited += h[1];
+        c->stats.boxes_tested += h[2];
+        c->stats.prims_tested += h[3];
+        c->stats.invalid_samples += h[4];
+    }
+    return NH_OK;
+}
+
+int nh_synchronize(nh_ctx *c) {
+    if (!c) return NH_ERR_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return NH_OK;
+}
+
+int nh_get_framebuffer(nh_ctx *c, float *rgbw, size_t n) {
+    if (!c || !rgbw) return NH_ERR_INVALID;
+    if (!c->has_scene) return fail(c, "no scene"), NH_ERR_STATE;
+    if (n < c->fb_floats) return fail(c, "framebuffer destination too small"), NH_ERR_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemcpy(rgbw, c->fb, c->fb_floats * sizeof(float), hipMemcpyDeviceToHost));
+    return NH_OK;
+}
+
+int nh_framebuffer_device_ptr(nh_ctx *c, void **dptr, size_t *n) {
+    if (!c || !dptr || !n) return NH_ERR_INVALID;
+    if (!c->has_scene) return fail(c, "no scene"), NH_ERR_STATE;
+    *dptr = c->fb;
+    *n = c->fb_floats;
+    return NH_OK;
+}
+
+int nh_get_stats(nh_ctx *c, nh_render_stats *out) {
+    if (!c || !out) return NH_ERR_INVALID;
+    *out = c->stats;
+    return NH_OK;
+}
+
+int nh_reset_stats(nh_ctx *c) {
+    if (!c) return NH_ERR_INVALID;
+    std::memset(&c->stats, 0, sizeof(c->stats));
+    return NH_OK;
+}
+
+int nh_reduce_framebuffers(nh_ctx **ctxs, int32_t n, int32_t root) {
+    if (!ctxs || n <= 0 || root < 0 || root >= n) return NH_ERR_INVALID;
+    for (int i = 0; i < n; ++i)
+        if (!ctxs[i] || !ctxs[i]->has_scene || ctxs[i]->fb_floats != ctxs[0]->fb_floats) return NH_ERR_INVALID;
+    if (n == 1) return NH_OK;
+    std::vector<ncclComm_t> comms(n);
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) devs[i] = ctxs[i]->device;
+    if (ncclCommInitAll(comms.data(), n, devs.data()) != ncclSuccess) {
+        ctxs[root]->err = "ncclCommInitAll failed";
+        return NH_ERR_DEVICE;
+    }
+    ncclGroupStart();
+    for (int i = 0; i < n; ++i) {
+        hipSetDevice(ctxs[i]->device);
+        ncclReduce(ctxs[i]->fb, ctxs[i]->fb, ctxs[i]->fb_floats, ncclFloat, ncclSum, root, comms[i], ctxs[i]->stream);
+    }
+    ncclResult_t r = ncclGroupEnd();
+    for (int i = 0; i < n; ++i) {
+        hipSetDevice(ctxs[i]->device);
+        hipStreamSynchronize(ctxs[i]->stream);
+        ncclCommDestroy(comms[i]);
+    }
+    if (r != ncclSuccess) {
+        ctxs[root]->err = "ncclReduce failed";
+        return NH_ERR_DEVICE;
+    }
+    return NH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,212 @@
+// BVH traversal for gfx950: BVH::rayIntersect (src/utils/bvh.cpp:402-460) semantics on
+// a GPU node layout.
+//
+// Layout (HBM, built by nh_api.hip from the reference's node array):
+//   inner node (64 B) = 4 x float4:
+//     n0 = (L.min.xyz, L.max.x)  n1 = (L.max.yz, R.min.xy)  n2 = (R.min.z, R.max.xyz)
+//     n3 = (int L.ref, int R.ref, 0, 0)   ref >= 0: inner node, ref < 0: leaf ~ref
+//   leaf table: int2 (start, count) into the primitive array
+//   primitive (48 B, in the reference's m_indices order) = 3 x float4:
+//     triangle: (p0, local face) (p1-p0, shape) (p2-p0, 0)
+//     sphere:   (center, radius) (0, shape) (0, 1)
+// Child boxes live in the parent, so one 64-B fetch tests both children; the
+// reference tests a node's own box when it is visited, which is the same set of
+// tests. Deferred children carry their slab entry distance and are re-checked against
+// the current maxt when popped -- exactly the reference's visit-time test, whose
+// other terms do not depend on maxt.
+//
+// Two visit orders:
+//   REFERENCE: left child first (the reference's order);
+//   ORDERED:   nearer child first.
+// Both return the reference's answer: the smallest t; among equal t the primitive
+// latest in left-first DFS order, which is the largest leaf-order position k (the
+// reference accepts t <= maxt, so a later equal-t primitive overwrites).
+#pragma once
+#include "nh_device.h"
+
+namespace nhd {
+
+struct Hit {
+    float t, u, v;
+    int k;  // leaf-order primitive position
+};
+
+struct TravStats {
+    uint32_t nodes, boxes, prims;
+};
+
+// BoundingBox::rayIntersect (bbox.h:336-363); returns the entry distance in near_out
+NHD bool box_test(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, F3 o, F3 d, F3 r, float mint,
+                  float maxt, float &near_out) {
+    float near_t = -INFINITY, far_t = INFINITY;
+    if (d.x == 0) {
+        if (o.x < mnx || o.x > mxx) return false;
+    } else {
+        float t1 = (mnx - o.x) * r.x, t2 = (mxx - o.x) * r.x;
+        if (t1 > t2) { float tmp = t1; t1 = t2; t2 = tmp; }
+        near_t = e_max(t1, near_t);
+        far_t = e_min(t2, far_t);
+        if (!(near_t <= far_t)) return false;
+    }
+    if (d.y == 0) {
+        if (o.y < mny || o.y > mxy) return false;
+    } else {
+        float t1 = (mny - o.y) * r.y, t2 = (mxy - o.y) * r.y;
+        if (t1 > t2) { float tmp = t1; t1 = t2; t2 = tmp; }
+        near_t = e_max(t1, near_t);
+        far_t = e_min(t2, far_t);
+        if (!(near_t <= far_t)) return false;
+    }
+    if (d.z == 0) {
+        if (o.z < mnz || o.z > mxz) return false;
+    } else {
+        float t1 = (mnz - o.z) * r.z, t2 = (mxz - o.z) * r.z;
+        if (t1 > t2) { float tmp = t1; t1 = t2; t2 = tmp; }
+        near_t = e_max(t1, near_t);
+        far_t = e_min(t2, far_t);
+        if (!(near_t <= far_t)) return false;
+    }
+    near_out = near_t;
+    return mint <= far_t && near_t <= maxt;
+}
+
+// Mesh::rayIntersect (mesh.cpp:101-139) on precomputed edges
+NHD bool tri_test(float4 a, float4 b, float4 c, F3 o, F3 d, float mint, float maxt, float &t, float &u, float &v) {
+    F3 p0 = f3(a.x, a.y, a.z), e1 = f3(b.x, b.y, b.z), e2 = f3(c.x, c.y, c.z);
+    F3 pvec = cross(d, e2);
+    float det = dot(e1, pvec);
+    if (det > -1e-8f && det < 1e-8f) return false;
+    float inv_det = 1.0f / det;
+    F3 tvec = sub(o, p0);
+    u = dot(tvec, pvec) * inv_det;
+    if (u < 0.0f || u > 1.0f) return false;
+    F3 qvec = cross(tvec, e1);
+    v = dot(d, qvec) * inv_det;
+    if (v < 0.0f || u + v > 1.0f) return false;
+    t = dot(e2, qvec) * inv_det;
+    return t >= mint && t <= maxt;
+}
+
+// Sphere::rayIntersect (sphere.cpp:67-94)
+NHD bool sphere_test(float4 a, F3 o, F3 d, float mint, float maxt, float &t) {
+    F3 L = sub(o, f3(a.x, a.y, a.z));
+    float qa = dot(d, d);
+    float qb = 2.f * dot(d, L);
+    float qc = dot(L, L) - a.w * a.w;
+    float discr = qb * qb - 4.f * qa * qc;
+    if (discr < 0.f) return false;
+    const float tmin = (-qb - f_sqrt(discr)) / 2 / qa;
+    const float tmax = (-qb + f_sqrt(discr)) / 2 / qa;
+    if (mint <= tmin && maxt >= tmin) { t = tmin; return true; }
+    if (mint <= tmax && maxt >= tmax) { t = tmax; return true; }
+    return false;
+}
+
+struct Traversal {
+    const float4 *nodes;
+    const int2 *leaves;
+    const float4 *prims;
+};
+
+// Test the primitives of one leaf. Returns true when an any-hit query is answered.
+template <bool ANY, bool STATS>
+NHD bool leaf_test(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float &maxt, Hit &best, bool &found,
+                   TravStats &st) {
+    const int2 lf = tv.leaves[leaf];
+    for (int k = lf.x, e = lf.x + lf.y; k < e; ++k) {
+        const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
+        if (STATS) st.prims++;
+        float t, u = 0.f, v = 0.f;
+        bool hit = (__float_as_int(c.w) == 0) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
+                                              : sphere_test(a, o, d, mint, maxt, t);
+        if (!hit) continue;
+        if (ANY) return true;
+        if (t < maxt || k > best.k) {
+            found = true;
+            maxt = t;
+            best.t = t;
+            best.u = u;
+            best.v = v;
+            best.k = k;
+        }
+    }
+    return false;
+}
+
+// Closest / any hit. stk points at this thread's first LDS stack slot; consecutive
+// entries are `stride` uint2 apart (lane-interleaved, bank-conflict free).
+template <int DEPTH, bool ORDERED, bool ANY, bool STATS>
+NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, float maxt, Hit &best, uint2 *stk,
+               int stride, TravStats &st) {
+    // adaptive ray epsilon (bvh.cpp:407-410)
+    if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));
+    if (S.root_kind == 0 || maxt < mint) return false;
+    const F3 r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    bool found = false;
+    best.k = -1;
+    best.t = INFINITY;
+    float near_t;
+    if (STATS) st.boxes++;
+    if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d, r,
+                  mint, maxt, near_t))
+        return false;
+    if (S.root_kind == 2) {
+        bool any = leaf_test<ANY, STATS>(tv, 0, o, d, mint, maxt, best, found, st);
+        return ANY ? any : found;
+    }
+    int sp = 0;
+    int cur = 0;
+    for (;;) {
+        while (cur >= 0) {
+            const float4 n0 = tv.nodes[4 * cur], n1 = tv.nodes[4 * cur + 1], n2 = tv.nodes[4 * cur + 2];
+            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * cur + 3]);
+            if (STATS) { st.nodes++; st.boxes += 2; }
+            float nl, nr;
+            const bool hl = box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, nl);
+            const bool hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
+            int next;
+            if (hl && hr) {
+                int first = n3.x, second = n3.y;
+                float second_near = nr;
+                if (ORDERED && nr < nl) {
+                    first = n3.y;
+                    second = n3.x;
+                    second_near = nl;
+                }
+                stk[sp * stride] = make_uint2((uint32_t)second, __float_as_uint(second_near));
+                ++sp;
+                next = first;
+            } else if (hl) {
+                next = n3.x;
+            } else if (hr) {
+                next = n3.y;
+            } else {
+                break;
+            }
+            if (next >= 0) {
+                cur = next;
+                continue;
+            }
+            if (leaf_test<ANY, STATS>(tv, ~next, o, d, mint, maxt, best, found, st)) return true;
+            break;
+        }
+        // pop, re-checking the deferred entry distance against the current maxt
+        cur = -1;
+        while (sp > 0) {
+            --sp;
+            const uint2 e = stk[sp * stride];
+            if (!(__uint_as_float(e.y) <= maxt)) continue;
+            const int ref = (int)e.x;
+            if (ref >= 0) {
+                cur = ref;
+                break;
+            }
+            if (leaf_test<ANY, STATS>(tv, ~ref, o, d, mint, maxt, best, found, st)) return true;
+        }
+        if (cur < 0) break;
+    }
+    (void)DEPTH;
+    return ANY ? false : found;
+}
+
+}  // namespace nhd

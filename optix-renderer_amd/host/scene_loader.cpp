@@ -1,0 +1,943 @@
+// Host-side Nori scene ingestion: XML subset -> flattened nh_scene_desc.
+//
+// Follows the reference's object model (include/nori/object.h:38-291) and parser
+// (src/utils/parser.cpp:28-378): children are parsed first, the object is then
+// created from its PropertyList and receives its children in document order;
+// transform operations pre-multiply (parser.cpp:312-366). Shape/emitter wiring
+// mirrors Scene::addChild (src/utils/scene.cpp:203-266) and Shape::addChild
+// (src/shapes/shape.cpp:118-153); the OBJ loader mirrors WavefrontOBJ::loadFromFile
+// (src/shapes/obj.cpp:77-238: vertex dedup on the (p, uv, n) triple, quad split
+// into (0,1,2),(3,0,2), toWorld baked in). Derived quantities follow
+// PerspectiveCamera::update (src/cameras/perspective.cpp:48-96), ImageBlock::init's
+// filter table (src/utils/block.cpp:54-70), Mesh::update's area DiscretePDF
+// (src/shapes/mesh.cpp:35-48) and Scene::update's emitter DiscretePDF
+// (src/utils/scene.cpp:178-184).
+//
+// Floating-point conventions: per-element arithmetic is fp32 with no contraction;
+// 3-element dot products / squared norms are evaluated x0*y0 + (x1*y1 + x2*y2),
+// which is what the reference's vendored Eigen 3.3.8 emits for Vector3f (measured,
+// DESIGN.md). Matrix inverses are computed in fp64 and rounded (the reference uses
+// Eigen's SSE 4x4 inverse; host-side setup only, identical for GPU and oracle).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <map>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "nori_hip.h"
+#include "nh_host.h"
+#include "xml_lite.h"
+
+namespace nh {
+
+thread_local std::string g_host_error;
+
+void set_host_error(const std::string &msg) { g_host_error = msg; }
+
+struct SceneError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+// ---------------------------------------------------------------------------
+// small fp32 math helpers in the reference's evaluation order
+// ---------------------------------------------------------------------------
+namespace {
+
+struct V3 {
+    float x = 0, y = 0, z = 0;
+};
+inline V3 v3(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+inline V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline float dot3(V3 a, V3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
+inline V3 cross3(V3 a, V3 b) {
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+inline V3 normalized(V3 a) {
+    float n = dot3(a, a);
+    if (n > 0.0f) {
+        float s = std::sqrt(n);
+        return v3(a.x / s, a.y / s, a.z / s);
+    }
+    return a;
+}
+
+struct M4 {
+    float m[4][4];
+    static M4 identity() {
+        M4 r;
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) r.m[i][j] = (i == j) ? 1.0f : 0.0f;
+        return r;
+    }
+};
+
+// 4x4 product, left-to-right accumulation (Eigen's lazy 4x4 product on SSE).
+M4 mul(const M4 &a, const M4 &b) {
+    M4 r;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            float s = a.m[i][0] * b.m[0][j];
+            s = s + a.m[i][1] * b.m[1][j];
+            s = s + a.m[i][2] * b.m[2][j];
+            s = s + a.m[i][3] * b.m[3][j];
+            r.m[i][j] = s;
+        }
+    return r;
+}
+
+M4 inverse(const M4 &a) {
+    double m[4][8];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 8; ++j) m[i][j] = (j < 4) ? (double)a.m[i][j] : (j - 4 == i ? 1.0 : 0.0);
+    for (int c = 0; c < 4; ++c) {
+        int p = c;
+        for (int r = c + 1; r < 4; ++r)
+            if (std::fabs(m[r][c]) > std::fabs(m[p][c])) p = r;
+        if (m[p][c] == 0.0) throw SceneError("singular transform matrix");
+        if (p != c)
+            for (int j = 0; j < 8; ++j) std::swap(m[p][j], m[c][j]);
+        double inv = 1.0 / m[c][c];
+        for (int j = 0; j < 8; ++j) m[c][j] *= inv;
+        for (int r = 0; r < 4; ++r) {
+            if (r == c) continue;
+            double f = m[r][c];
+            if (f == 0.0) continue;
+            for (int j = 0; j < 8; ++j) m[r][j] -= f * m[c][j];
+        }
+    }
+    M4 r;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) r.m[i][j] = (float)m[i][j + 4];
+    return r;
+}
+
+// Transform::operator*(Point3f): homogeneous, left-to-right 4x4 product, divide by w.
+V3 xform_point(const M4 &t, V3 p) {
+    float r[4];
+    for (int i = 0; i < 4; ++i) {
+        float s = t.m[i][0] * p.x;
+        s = s + t.m[i][1] * p.y;
+        s = s + t.m[i][2] * p.z;
+        s = s + t.m[i][3] * 1.0f;
+        r[i] = s;
+    }
+    return v3(r[0] / r[3], r[1] / r[3], r[2] / r[3]);
+}
+// Transform::operator*(Vector3f): top-left 3x3 product (Eigen redux order per row).
+V3 xform_vector(const M4 &t, V3 v) {
+    return v3(t.m[0][0] * v.x + (t.m[0][1] * v.y + t.m[0][2] * v.z),
+              t.m[1][0] * v.x + (t.m[1][1] * v.y + t.m[1][2] * v.z),
+              t.m[2][0] * v.x + (t.m[2][1] * v.y + t.m[2][2] * v.z));
+}
+// Transform::operator*(Normal3f): inverse-transpose 3x3.
+V3 xform_normal(const M4 &inv, V3 n) {
+    return v3(inv.m[0][0] * n.x + (inv.m[1][0] * n.y + inv.m[2][0] * n.z),
+              inv.m[0][1] * n.x + (inv.m[1][1] * n.y + inv.m[2][1] * n.z),
+              inv.m[0][2] * n.x + (inv.m[1][2] * n.y + inv.m[2][2] * n.z));
+}
+
+float to_float(const std::string &str) {
+    const char *c = str.c_str();
+    char *end = nullptr;
+    float r = std::strtof(c, &end);
+    while (end && *end && std::isspace((unsigned char)*end)) ++end;
+    if (end == c || *end != '\0') throw SceneError("could not parse floating point value \"" + str + "\"");
+    return r;
+}
+int to_int(const std::string &str) {
+    const char *c = str.c_str();
+    char *end = nullptr;
+    long r = std::strtol(c, &end, 10);
+    if (end == c || *end != '\0') throw SceneError("could not parse integer value \"" + str + "\"");
+    return (int)r;
+}
+bool to_bool(const std::string &str) {
+    std::string v = str;
+    std::transform(v.begin(), v.end(), v.begin(), ::tolower);
+    if (v == "true") return true;
+    if (v == "false") return false;
+    throw SceneError("could not parse boolean value \"" + str + "\"");
+}
+// common.cpp tokenize(): delimiters ", ", empty tokens dropped
+std::vector<std::string> tokenize(const std::string &s, const std::string &delim = ", ", bool include_empty = false) {
+    std::vector<std::string> out;
+    std::string::size_type last = 0, pos = s.find_first_of(delim, last);
+    while (last != std::string::npos) {
+        if (pos != last || include_empty) out.push_back(s.substr(last, pos - last));
+        last = pos;
+        if (last != std::string::npos) {
+            last += 1;
+            pos = s.find_first_of(delim, last);
+        }
+    }
+    return out;
+}
+V3 to_v3(const std::string &s) {
+    auto t = tokenize(s);
+    if (t.size() != 3) throw SceneError("expected 3 values in \"" + s + "\"");
+    return v3(to_float(t[0]), to_float(t[1]), to_float(t[2]));
+}
+
+// ---------------------------------------------------------------------------
+// PropertyList (src/utils/proplist.cpp)
+// ---------------------------------------------------------------------------
+struct Prop {
+    enum Kind { Bool, Int, Float, String, Point, Vector, Color, Transform } kind;
+    bool b = false;
+    int i = 0;
+    float f = 0;
+    std::string s;
+    V3 v;
+    M4 t;
+};
+
+struct PropList {
+    std::map<std::string, Prop> props;
+    void set(const std::string &name, const Prop &p) {
+        if (props.count(name)) throw SceneError("property \"" + name + "\" was specified multiple times");
+        props[name] = p;
+    }
+    bool has(const std::string &n) const { return props.count(n) != 0; }
+    const Prop *get(const std::string &n, Prop::Kind k) const {
+        auto it = props.find(n);
+        if (it == props.end()) return nullptr;
+        if (it->second.kind != k) throw SceneError("property \"" + n + "\" has the wrong type");
+        return &it->second;
+    }
+    float get_float(const std::string &n, float def) const { auto p = get(n, Prop::Float); return p ? p->f : def; }
+    float get_float(const std::string &n) const {
+        auto p = get(n, Prop::Float);
+        if (!p) throw SceneError("property \"" + n + "\" is missing");
+        return p->f;
+    }
+    int get_int(const std::string &n, int def) const { auto p = get(n, Prop::Int); return p ? p->i : def; }
+    std::string get_string(const std::string &n, const std::string &def) const { auto p = get(n, Prop::String); return p ? p->s : def; }
+    std::string get_string(const std::string &n) const {
+        auto p = get(n, Prop::String);
+        if (!p) throw SceneError("property \"" + n + "\" is missing");
+        return p->s;
+    }
+    V3 get_point(const std::string &n, V3 def) const { auto p = get(n, Prop::Point); return p ? p->v : def; }
+    V3 get_color(const std::string &n, V3 def) const { auto p = get(n, Prop::Color); return p ? p->v : def; }
+    V3 get_color(const std::string &n) const {
+        auto p = get(n, Prop::Color);
+        if (!p) throw SceneError("property \"" + n + "\" is missing");
+        return p->v;
+    }
+    M4 get_transform(const std::string &n, const M4 &def) const { auto p = get(n, Prop::Transform); return p ? p->t : def; }
+};
+
+// ---------------------------------------------------------------------------
+// object tree produced by the parser
+// ---------------------------------------------------------------------------
+struct Obj {
+    std::string tag;   // scene, shape, bsdf, emitter, camera, integrator, sampler, rfilter, ...
+    std::string type;  // plugin name
+    PropList props;
+    std::vector<std::unique_ptr<Obj>> children;
+    size_t offset = 0;
+};
+
+}  // namespace
+
+// Owning scene (the C handle).
+struct SceneData {
+    nh_camera camera{};
+    nh_filter filter{};
+    int32_t integrator = NH_INTEGRATOR_PATH_MIS;
+    int32_t sample_count = 1;
+    std::vector<nh_shape> shapes;
+    std::vector<nh_bsdf> bsdfs;
+    std::vector<nh_emitter> emitters;
+    std::vector<float> emitter_cdf;
+    int32_t envmap = -1;
+    std::vector<float> V, N, UV, T, BT;
+    std::vector<uint32_t> F;
+    std::vector<float> area_cdf;
+    // camera parameters kept for re-projection on resize
+    float fov = 30.f, near_clip = 1e-4f, far_clip = 1e4f, focal = 10.f, fstop = 0.f, lens = 0.f;
+    M4 to_world = M4::identity();
+};
+
+namespace {
+
+const char *kObjectTags[] = {"scene", "shape", "texture", "volume", "bsdf", "phase", "emitter", "medium", "camera",
+                             "integrator", "sampler", "pxsampler", "denoiser", "test", "rfilter", "renderer"};
+const char *kPropTags[] = {"boolean", "integer", "float", "string", "point", "vector", "color", "transform"};
+const char *kXformTags[] = {"translate", "matrix", "rotate", "scale", "lookat"};
+
+bool in_list(const std::string &s, const char *const *list, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        if (s == list[i]) return true;
+    return false;
+}
+
+struct ParseCtx {
+    const std::string &text;
+    const std::string &filename;
+    std::string pos(size_t off) const { return xml_position(text, off); }
+};
+
+void check_attrs(const XmlNode &n, std::initializer_list<const char *> allowed, const ParseCtx &c) {
+    std::vector<std::string> need(allowed.begin(), allowed.end());
+    for (auto &kv : n.attrs) {
+        auto it = std::find(need.begin(), need.end(), kv.first);
+        if (it == need.end())
+            throw SceneError("unexpected attribute \"" + kv.first + "\" in \"" + n.name + "\" at " + c.pos(n.offset));
+        need.erase(it);
+    }
+    if (!need.empty()) throw SceneError("missing attribute \"" + need[0] + "\" in \"" + n.name + "\" at " + c.pos(n.offset));
+}
+
+M4 xform_op(const XmlNode &n, const ParseCtx &c) {
+    M4 r = M4::identity();
+    if (n.name == "translate") {
+        check_attrs(n, {"value"}, c);
+        V3 v = to_v3(*n.attr("value"));
+        r.m[0][3] = v.x; r.m[1][3] = v.y; r.m[2][3] = v.z;
+    } else if (n.name == "scale") {
+        check_attrs(n, {"value"}, c);
+        V3 v = to_v3(*n.attr("value"));
+        r.m[0][0] = v.x; r.m[1][1] = v.y; r.m[2][2] = v.z;
+    } else if (n.name == "matrix") {
+        check_attrs(n, {"value"}, c);
+        auto t = tokenize(*n.attr("value"));
+        if (t.size() != 16) throw SceneError("expected 16 values");
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) r.m[i][j] = to_float(t[i * 4 + j]);
+    } else if (n.name == "rotate") {
+        check_attrs(n, {"angle", "axis"}, c);
+        float angle = to_float(*n.attr("angle")) * (3.14159265358979323846f / 180.0f);
+        V3 a = to_v3(*n.attr("axis"));
+        // Eigen::AngleAxis::toRotationMatrix
+        float s = (float)std::sin((double)angle), co = (float)std::cos((double)angle);
+        V3 sa = v3(s * a.x, s * a.y, s * a.z);
+        V3 c1 = v3((1.0f - co) * a.x, (1.0f - co) * a.y, (1.0f - co) * a.z);
+        float tmp = c1.x * a.y;
+        r.m[0][1] = tmp - sa.z; r.m[1][0] = tmp + sa.z;
+        tmp = c1.x * a.z;
+        r.m[0][2] = tmp + sa.y; r.m[2][0] = tmp - sa.y;
+        tmp = c1.y * a.z;
+        r.m[1][2] = tmp - sa.x; r.m[2][1] = tmp + sa.x;
+        r.m[0][0] = c1.x * a.x + co; r.m[1][1] = c1.y * a.y + co; r.m[2][2] = c1.z * a.z + co;
+    } else if (n.name == "lookat") {
+        check_attrs(n, {"origin", "target", "up"}, c);
+        V3 origin = to_v3(*n.attr("origin")), target = to_v3(*n.attr("target")), up = to_v3(*n.attr("up"));
+        V3 dir = normalized(sub(target, origin));
+        V3 left = normalized(cross3(normalized(up), dir));
+        V3 new_up = normalized(cross3(dir, left));
+        r.m[0][0] = left.x; r.m[1][0] = left.y; r.m[2][0] = left.z;
+        r.m[0][1] = new_up.x; r.m[1][1] = new_up.y; r.m[2][1] = new_up.z;
+        r.m[0][2] = dir.x; r.m[1][2] = dir.y; r.m[2][2] = dir.z;
+        r.m[0][3] = origin.x; r.m[1][3] = origin.y; r.m[2][3] = origin.z;
+    } else {
+        throw SceneError("unhandled transform element \"" + n.name + "\"");
+    }
+    return r;
+}
+
+std::unique_ptr<Obj> parse_node(const XmlNode &n, PropList *parent_props, const std::string &parent_tag,
+                                const ParseCtx &c) {
+    const bool is_obj = in_list(n.name, kObjectTags, sizeof(kObjectTags) / sizeof(*kObjectTags));
+    const bool is_prop = in_list(n.name, kPropTags, sizeof(kPropTags) / sizeof(*kPropTags));
+    const bool is_xop = in_list(n.name, kXformTags, sizeof(kXformTags) / sizeof(*kXformTags));
+    if (!is_obj && !is_prop && !is_xop)
+        throw SceneError("unexpected tag \"" + n.name + "\" at " + c.pos(n.offset));
+    const bool has_parent = !parent_tag.empty();
+    if (!has_parent && !is_obj)
+        throw SceneError("root element \"" + n.name + "\" must be a Nori object (at " + c.pos(n.offset) + ")");
+    if ((parent_tag == "transform") != is_xop)
+        throw SceneError("transform nodes can only contain transform operations (at " + c.pos(n.offset) + ")");
+    if (is_obj) {
+        auto o = std::make_unique<Obj>();
+        o->tag = n.name;
+        o->offset = n.offset;
+        const std::string *t = n.attr("type");
+        o->type = (n.name == "scene") ? "scene" : (t ? *t : "");
+        for (auto &ch : n.children) {
+            auto child = parse_node(*ch, &o->props, n.name, c);
+            if (child) o->children.push_back(std::move(child));
+        }
+        const std::string *nm = n.attr("name");
+        Prop p; p.kind = Prop::String; p.s = nm ? *nm : "";
+        if (!o->props.has("name")) o->props.props["name"] = p;
+        return o;
+    }
+    if (!parent_props) throw SceneError("property outside of an object at " + c.pos(n.offset));
+    if (n.name == "transform") {
+        check_attrs(n, {"name"}, c);
+        M4 acc = M4::identity();
+        for (auto &ch : n.children) {
+            if (!in_list(ch->name, kXformTags, sizeof(kXformTags) / sizeof(*kXformTags)))
+                throw SceneError("transform nodes can only contain transform operations (at " + c.pos(ch->offset) + ")");
+            acc = mul(xform_op(*ch, c), acc);  // pre-multiply: later operations apply last
+        }
+        Prop p; p.kind = Prop::Transform; p.t = acc;
+        parent_props->set(*n.attr("name"), p);
+        return nullptr;
+    }
+    check_attrs(n, {"name", "value"}, c);
+    const std::string &name = *n.attr("name"), &val = *n.attr("value");
+    Prop p;
+    if (n.name == "boolean") { p.kind = Prop::Bool; p.b = to_bool(val); }
+    else if (n.name == "integer") { p.kind = Prop::Int; p.i = to_int(val); }
+    else if (n.name == "float") { p.kind = Prop::Float; p.f = to_float(val); }
+    else if (n.name == "string") { p.kind = Prop::String; p.s = val; }
+    else if (n.name == "point" || n.name == "vector") {
+        auto tk = tokenize(val);
+        if (tk.size() != 3) throw SceneError(n.name + " \"" + name + "\" must have 3 components");
+        p.kind = n.name == "point" ? Prop::Point : Prop::Vector;
+        p.v = to_v3(val);
+    } else if (n.name == "color") { p.kind = Prop::Color; p.v = to_v3(val); }
+    parent_props->set(name, p);
+    return nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// scene assembly
+// ---------------------------------------------------------------------------
+
+std::string join_path(const std::string &base_dir, const std::string &rel) {
+    if (!rel.empty() && rel[0] == '/') return rel;
+    if (base_dir.empty()) return rel;
+    return base_dir + "/" + rel;
+}
+
+// WavefrontOBJ::loadFromFile
+void load_obj(const std::string &path, const M4 &trafo, SceneData &sd, nh_shape &sh) {
+    std::ifstream is(path);
+    if (is.fail()) throw SceneError("unable to open OBJ file \"" + path + "\"");
+    M4 inv = inverse(trafo);
+    struct Key {
+        uint32_t p, uv, n;
+        bool operator==(const Key &o) const { return p == o.p && uv == o.uv && n == o.n; }
+    };
+    struct KeyHash {
+        size_t operator()(const Key &k) const {
+            size_t h = std::hash<uint32_t>()(k.p);
+            h = h * 37 + std::hash<uint32_t>()(k.uv);
+            h = h * 37 + std::hash<uint32_t>()(k.n);
+            return h;
+        }
+    };
+    std::vector<V3> positions, normals;
+    std::vector<std::pair<float, float>> texcoords;
+    std::vector<uint32_t> indices;
+    std::vector<Key> vertices;
+    std::unordered_map<Key, uint32_t, KeyHash> vmap;
+    V3 bmin = v3(INFINITY, INFINITY, INFINITY), bmax = v3(-INFINITY, -INFINITY, -INFINITY);
+
+    auto parse_vertex = [&](const std::string &s) {
+        auto tk = tokenize(s, "/", true);
+        if (tk.size() < 1 || tk.size() > 3) throw SceneError("invalid vertex data \"" + s + "\"");
+        Key k{(uint32_t)-1, (uint32_t)-1, (uint32_t)-1};
+        k.p = (uint32_t)std::stoul(tk[0]);
+        if (tk.size() >= 2 && !tk[1].empty()) k.uv = (uint32_t)std::stoul(tk[1]);
+        if (tk.size() >= 3 && !tk[2].empty()) k.n = (uint32_t)std::stoul(tk[2]);
+        return k;
+    };
+    std::string line_str;
+    while (std::getline(is, line_str)) {
+        std::istringstream line(line_str);
+        std::string prefix;
+        line >> prefix;
+        if (prefix == "v") {
+            V3 p;
+            line >> p.x >> p.y >> p.z;
+            p = xform_point(trafo, p);
+            bmin = v3(std::min(bmin.x, p.x), std::min(bmin.y, p.y), std::min(bmin.z, p.z));
+            bmax = v3(std::max(bmax.x, p.x), std::max(bmax.y, p.y), std::max(bmax.z, p.z));
+            positions.push_back(p);
+        } else if (prefix == "vt") {
+            float u = 0, v = 0;
+            line >> u >> v;
+            texcoords.emplace_back(u, v);
+        } else if (prefix == "vn") {
+            V3 n;
+            line >> n.x >> n.y >> n.z;
+            normals.push_back(normalized(xform_normal(inv, n)));
+        } else if (prefix == "f") {
+            std::string s1, s2, s3, s4;
+            line >> s1 >> s2 >> s3 >> s4;
+            Key verts[6];
+            int nv = 3;
+            verts[0] = parse_vertex(s1);
+            verts[1] = parse_vertex(s2);
+            verts[2] = parse_vertex(s3);
+            if (!s4.empty()) {
+                verts[3] = parse_vertex(s4);
+                verts[4] = verts[0];
+                verts[5] = verts[2];
+                nv = 6;
+            }
+            for (int i = 0; i < nv; ++i) {
+                auto it = vmap.find(verts[i]);
+                if (it == vmap.end()) {
+                    vmap[verts[i]] = (uint32_t)vertices.size();
+                    indices.push_back((uint32_t)vertices.size());
+                    vertices.push_back(verts[i]);
+                } else {
+                    indices.push_back(it->second);
+                }
+            }
+        }
+    }
+    const uint32_t nvert = (uint32_t)vertices.size(), nface = (uint32_t)(indices.size() / 3);
+    sh.type = NH_SHAPE_MESH;
+    sh.v_offset = (uint32_t)(sd.V.size() / 3);
+    sh.n_vertices = nvert;
+    sh.f_offset = (uint32_t)(sd.F.size() / 3);
+    sh.n_faces = nface;
+    sh.has_normals = normals.empty() ? 0 : 1;
+    sh.has_uvs = texcoords.empty() ? 0 : 1;
+    sh.bbox_min[0] = bmin.x; sh.bbox_min[1] = bmin.y; sh.bbox_min[2] = bmin.z;
+    sh.bbox_max[0] = bmax.x; sh.bbox_max[1] = bmax.y; sh.bbox_max[2] = bmax.z;
+
+    std::vector<V3> P(nvert), Nn(nvert), Tt(nvert), Bt(nvert);
+    std::vector<std::pair<float, float>> Uv(nvert, {0.f, 0.f});
+    for (uint32_t i = 0; i < nvert; ++i) {
+        if (vertices[i].p - 1 >= positions.size()) throw SceneError("OBJ position index out of range in " + path);
+        P[i] = positions[vertices[i].p - 1];
+        if (sh.has_normals) {
+            if (vertices[i].n - 1 >= normals.size()) throw SceneError("OBJ normal index out of range in " + path);
+            Nn[i] = normals[vertices[i].n - 1];
+        }
+        if (sh.has_uvs) {
+            if (vertices[i].uv - 1 >= texcoords.size()) throw SceneError("OBJ texcoord index out of range in " + path);
+            Uv[i] = texcoords[vertices[i].uv - 1];
+        }
+    }
+    if (sh.has_normals && sh.has_uvs) {  // obj.cpp:180-224 tangent accumulation
+        for (uint32_t t = 0; t < nface; ++t) {
+            uint32_t i1 = indices[3 * t], i2 = indices[3 * t + 1], i3 = indices[3 * t + 2];
+            V3 e1 = sub(P[i2], P[i1]), e2 = sub(P[i3], P[i1]);
+            float du1 = Uv[i2].first - Uv[i1].first, dv1 = Uv[i2].second - Uv[i1].second;
+            float du2 = Uv[i3].first - Uv[i1].first, dv2 = Uv[i3].second - Uv[i1].second;
+            float frac = du1 * dv2 - du2 * dv1;
+            float f = 1.f / (frac == 0.f ? 1e-4f : frac);
+            V3 tan = v3(f * (dv2 * e1.x - dv1 * e2.x), f * (dv2 * e1.y - dv1 * e2.y), f * (dv2 * e1.z - dv1 * e2.z));
+            V3 tw = xform_vector(trafo, tan);
+            for (uint32_t k : {i1, i2, i3}) {
+                Tt[k] = v3(Tt[k].x + tw.x, Tt[k].y + tw.y, Tt[k].z + tw.z);
+                V3 bw = xform_vector(trafo, cross3(Nn[k], tan));
+                Bt[k] = v3(Bt[k].x + bw.x, Bt[k].y + bw.y, Bt[k].z + bw.z);
+            }
+        }
+    }
+    for (uint32_t i = 0; i < nvert; ++i) {
+        sd.V.insert(sd.V.end(), {P[i].x, P[i].y, P[i].z});
+        sd.N.insert(sd.N.end(), {Nn[i].x, Nn[i].y, Nn[i].z});
+        sd.UV.insert(sd.UV.end(), {Uv[i].first, Uv[i].second});
+        sd.T.insert(sd.T.end(), {Tt[i].x, Tt[i].y, Tt[i].z});
+        sd.BT.insert(sd.BT.end(), {Bt[i].x, Bt[i].y, Bt[i].z});
+    }
+    sd.F.insert(sd.F.end(), indices.begin(), indices.end());
+}
+
+// Mesh::update: DiscretePDF over triangle areas (mesh.cpp:35-48, 92-99; dpdf.h)
+void build_area_pdf(SceneData &sd, nh_shape &sh) {
+    sh.pdf_offset = (uint32_t)sd.area_cdf.size();
+    std::vector<float> cdf;
+    cdf.reserve(sh.n_faces + 1);
+    cdf.push_back(0.0f);
+    const float *V = sd.V.data() + 3 * (size_t)sh.v_offset;
+    const uint32_t *F = sd.F.data() + 3 * (size_t)sh.f_offset;
+    for (uint32_t i = 0; i < sh.n_faces; ++i) {
+        const float *p0 = V + 3 * F[3 * i], *p1 = V + 3 * F[3 * i + 1], *p2 = V + 3 * F[3 * i + 2];
+        V3 a = v3(p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]);
+        V3 b = v3(p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2]);
+        V3 cr = cross3(a, b);
+        float area = 0.5f * std::sqrt(dot3(cr, cr));
+        cdf.push_back(cdf.back() + area);
+    }
+    float sum = cdf.back();
+    if (sum > 0) {
+        float norm = 1.0f / sum;
+        for (size_t i = 1; i < cdf.size(); ++i) cdf[i] *= norm;
+        cdf.back() = 1.0f;
+        sh.pdf_normalization = norm;
+    } else {
+        sh.pdf_normalization = 0.0f;
+    }
+    sd.area_cdf.insert(sd.area_cdf.end(), cdf.begin(), cdf.end());
+}
+
+float filter_eval(int type, float radius, float stddev, float B, float C, float x) {
+    switch (type) {
+        case 0: {  // gaussian (rfilter.cpp:41-47)
+            float alpha = -1.0f / (2.0f * stddev * stddev);
+            float a = (float)std::exp((double)(alpha * x * x));
+            float b = (float)std::exp((double)(alpha * radius * radius));
+            return std::max(0.0f, a - b);
+        }
+        case 1: {  // mitchell (rfilter.cpp:95-111)
+            x = std::fabs(2.0f * x / radius);
+            float x2 = x * x, x3 = x2 * x;
+            if (x < 1)
+                return 1.0f / 6.0f * ((12 - 9 * B - 6 * C) * x3 + (-18 + 12 * B + 6 * C) * x2 + (6 - 2 * B));
+            else if (x < 2)
+                return 1.0f / 6.0f * ((-B - 6 * C) * x3 + (6 * B + 30 * C) * x2 + (-12 * B - 48 * C) * x + (8 * B + 24 * C));
+            return 0.0f;
+        }
+        case 2: return std::max(0.0f, 1.0f - std::fabs(x));  // tent
+        default: return 1.0f;                                 // box
+    }
+}
+
+void set_filter(nh_filter &f, int type, float radius, float stddev, float B, float C) {
+    f.radius = radius;
+    f.border = (int)std::ceil(radius - 0.5f);
+    for (int i = 0; i < 32; ++i) {
+        float pos = (radius * (float)i) / 32.0f;
+        f.table[i] = filter_eval(type, radius, stddev, B, C, pos);
+    }
+    f.table[32] = 0.0f;
+    f.lookup_factor = 32.0f / radius;
+}
+
+}  // namespace
+
+// PerspectiveCamera::update (perspective.cpp:67-95)
+void camera_update(SceneData &sd) {
+    nh_camera &c = sd.camera;
+    c.inv_output_size[0] = 1.0f / (float)c.width;
+    c.inv_output_size[1] = 1.0f / (float)c.height;
+    float aspect = (float)c.width / (float)c.height;
+    float recip = 1.0f / (sd.far_clip - sd.near_clip);
+    float cot = 1.0f / (float)std::tan((double)((sd.fov / 2.0f) * (3.14159265358979323846f / 180.0f)));
+    M4 persp = M4::identity();
+    persp.m[0][0] = cot; persp.m[1][1] = cot;
+    persp.m[2][2] = sd.far_clip * recip;
+    persp.m[2][3] = -sd.near_clip * sd.far_clip * recip;
+    persp.m[3][2] = 1.0f; persp.m[3][3] = 0.0f;
+    M4 st = M4::identity();  // DiagonalMatrix(0.5, -0.5*aspect, 1) * Translation(1, -1/aspect, 0)
+    st.m[0][0] = 0.5f; st.m[1][1] = -0.5f * aspect; st.m[2][2] = 1.0f;
+    st.m[0][3] = 0.5f * 1.0f; st.m[1][3] = (-0.5f * aspect) * (-1.0f / aspect); st.m[2][3] = 1.0f * 0.0f;
+    M4 s2c = inverse(mul(st, persp));
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            c.sample_to_camera[i * 4 + j] = s2c.m[i][j];
+            c.camera_to_world[i * 4 + j] = sd.to_world.m[i][j];
+        }
+    c.near_clip = sd.near_clip;
+    c.far_clip = sd.far_clip;
+    c.focal_distance = sd.focal;
+    // cloneAndInit: fstop/lensRadius coupling (perspective.cpp:39-42)
+    c.lens_radius = sd.lens;
+}
+
+namespace {
+
+nh_bsdf make_bsdf(const Obj &o) {
+    nh_bsdf b{};
+    const PropList &p = o.props;
+    if (o.type == "diffuse") {
+        b.type = NH_BSDF_DIFFUSE;
+        for (auto &ch : o.children)
+            if (ch->tag == "texture") throw SceneError("textured diffuse albedo is not supported yet");
+        V3 a = p.get_color("albedo", v3(0.5f, 0.5f, 0.5f));
+        b.albedo[0] = a.x; b.albedo[1] = a.y; b.albedo[2] = a.z;
+    } else if (o.type == "mirror") {
+        b.type = NH_BSDF_MIRROR;
+    } else if (o.type == "dielectric") {
+        b.type = NH_BSDF_DIELECTRIC;
+        b.int_ior = p.get_float("intIOR", 1.5046f);
+        b.ext_ior = p.get_float("extIOR", 1.000277f);
+    } else if (o.type == "microfacet") {
+        b.type = NH_BSDF_MICROFACET;
+        b.alpha = p.get_float("alpha", 0.1f);
+        b.int_ior = p.get_float("intIOR", 1.5046f);
+        b.ext_ior = p.get_float("extIOR", 1.000277f);
+        V3 kd = p.get_color("kd", v3(0.5f, 0.5f, 0.5f));
+        b.kd[0] = kd.x; b.kd[1] = kd.y; b.kd[2] = kd.z;
+        // m_ks = 1 - m_kd.maxCoeff()  (Eigen max redux: f(c0, f(c1, c2)), f(a,b) = a < b ? b : a)
+        float m12 = kd.y < kd.z ? kd.z : kd.y;
+        float mx = kd.x < m12 ? m12 : kd.x;
+        b.ks = 1 - mx;
+    } else {
+        throw SceneError("BSDF type \"" + o.type + "\" is not supported by the HIP path");
+    }
+    return b;
+}
+
+nh_bsdf default_diffuse() {
+    nh_bsdf b{};
+    b.type = NH_BSDF_DIFFUSE;
+    b.albedo[0] = b.albedo[1] = b.albedo[2] = 0.5f;
+    return b;
+}
+
+void build_scene(const Obj &scene, const std::string &base_dir, SceneData &sd) {
+    bool have_camera = false, have_integrator = false, have_sampler = false;
+    set_filter(sd.filter, 0, 2.0f, 0.5f, 1.0f / 3.0f, 1.0f / 3.0f);
+    for (auto &chp : scene.children) {
+        const Obj &ch = *chp;
+        if (ch.tag == "integrator") {
+            if (have_integrator) throw SceneError("there can only be one integrator per scene");
+            have_integrator = true;
+            if (ch.type == "path_mis") sd.integrator = NH_INTEGRATOR_PATH_MIS;
+            else if (ch.type == "path_mats") sd.integrator = NH_INTEGRATOR_PATH_MATS;
+            else throw SceneError("integrator \"" + ch.type + "\" is not supported by the HIP path");
+        } else if (ch.tag == "camera") {
+            if (have_camera) throw SceneError("there can only be one camera per scene");
+            have_camera = true;
+            if (ch.type != "perspective") throw SceneError("camera \"" + ch.type + "\" is not supported");
+            sd.camera.width = ch.props.get_int("width", 1280);
+            sd.camera.height = ch.props.get_int("height", 720);
+            sd.to_world = ch.props.get_transform("toWorld", M4::identity());
+            sd.fov = ch.props.get_float("fov", 30.0f);
+            sd.near_clip = ch.props.get_float("nearClip", 1e-4f);
+            sd.far_clip = ch.props.get_float("farClip", 1e4f);
+            sd.focal = ch.props.get_float("focalDistance", 10.f);
+            sd.fstop = ch.props.get_float("fstop", 0.f);
+            sd.lens = ch.props.get_float("lensRadius", 0.f);
+            if (sd.fstop == 0.f) sd.fstop = sd.focal / sd.lens;
+            else sd.lens = sd.focal / sd.fstop;
+            for (auto &rf : ch.children) {
+                if (rf->tag != "rfilter") throw SceneError("camera child <" + rf->tag + "> is not supported");
+                const PropList &p = rf->props;
+                if (rf->type == "gaussian")
+                    set_filter(sd.filter, 0, p.get_float("radius", 2.0f), p.get_float("stddev", 0.5f), 0, 0);
+                else if (rf->type == "mitchell")
+                    set_filter(sd.filter, 1, p.get_float("radius", 2.0f), 0, p.get_float("B", 1.0f / 3.0f),
+                               p.get_float("C", 1.0f / 3.0f));
+                else if (rf->type == "tent") set_filter(sd.filter, 2, 1.0f, 0, 0, 0);
+                else if (rf->type == "box") set_filter(sd.filter, 3, 0.5f, 0, 0, 0);
+                else throw SceneError("rfilter \"" + rf->type + "\" is not supported");
+            }
+        } else if (ch.tag == "sampler") {
+            if (have_sampler) throw SceneError("there can only be one sampler per scene");
+            have_sampler = true;
+            if (ch.type != "independent")
+                throw SceneError("sampler \"" + ch.type + "\" is not supported (the HIP path uses per-path pcg32)");
+            sd.sample_count = ch.props.get_int("sampleCount", 1);
+        } else if (ch.tag == "shape") {
+            nh_shape sh{};
+            sh.emitter = -1;
+            int bsdf = -1, emitter = -1;
+            nh_emitter em{};
+            for (auto &sc : ch.children) {
+                if (sc->tag == "bsdf") {
+                    if (bsdf >= 0) throw SceneError("Shape: tried to register multiple BSDF instances");
+                    sd.bsdfs.push_back(make_bsdf(*sc));
+                    bsdf = (int)sd.bsdfs.size() - 1;
+                } else if (sc->tag == "emitter") {
+                    if (emitter >= 0) throw SceneError("Shape: tried to register multiple Emitter instances");
+                    if (sc->type != "area") throw SceneError("shape emitter \"" + sc->type + "\" is not supported");
+                    em.type = NH_EMITTER_AREA;
+                    V3 r = sc->props.get_color("radiance");
+                    em.radiance[0] = r.x; em.radiance[1] = r.y; em.radiance[2] = r.z;
+                    em.light_prob = sc->props.get_float("lightWeight", 1.f);
+                    emitter = 1;
+                } else if (sc->tag == "medium") {
+                    throw SceneError("participating media are out of scope for path_mis");
+                } else {
+                    throw SceneError("shape child <" + sc->tag + "> is not supported");
+                }
+            }
+            if (bsdf < 0) {  // Shape::cloneAndInit default diffuse
+                sd.bsdfs.push_back(default_diffuse());
+                bsdf = (int)sd.bsdfs.size() - 1;
+            }
+            sh.bsdf = bsdf;
+            if (ch.type == "obj") {
+                std::string fn = join_path(base_dir, ch.props.get_string("filename"));
+                load_obj(fn, ch.props.get_transform("toWorld", M4::identity()), sd, sh);
+            } else if (ch.type == "sphere") {
+                sh.type = NH_SHAPE_SPHERE;
+                V3 c = ch.props.get_point("center", v3(0, 0, 0));
+                float r = ch.props.get_float("radius", 1.f);
+                sh.center[0] = c.x; sh.center[1] = c.y; sh.center[2] = c.z;
+                sh.radius = r;
+                sh.v_offset = (uint32_t)(sd.V.size() / 3);
+                sh.f_offset = (uint32_t)(sd.F.size() / 3);
+                sh.bbox_min[0] = c.x - r; sh.bbox_min[1] = c.y - r; sh.bbox_min[2] = c.z - r;
+                sh.bbox_max[0] = c.x + r; sh.bbox_max[1] = c.y + r; sh.bbox_max[2] = c.z + r;
+            } else {
+                throw SceneError("shape \"" + ch.type + "\" is not supported");
+            }
+            if (sh.type == NH_SHAPE_MESH) build_area_pdf(sd, sh);
+            if (emitter >= 0) {
+                em.shape = (int32_t)sd.shapes.size();
+                sd.emitters.push_back(em);
+                sh.emitter = (int32_t)sd.emitters.size() - 1;
+            }
+            sd.shapes.push_back(sh);
+        } else if (ch.tag == "emitter") {
+            nh_emitter em{};
+            em.shape = -1;
+            em.light_prob = ch.props.get_float("lightWeight", 1.f);
+            if (ch.type == "point") {
+                em.type = NH_EMITTER_POINT;
+                V3 p = ch.props.get_point("position", v3(0, 0, 0));
+                V3 pw = ch.props.get_color("power", v3(1, 1, 1));
+                em.position[0] = p.x; em.position[1] = p.y; em.position[2] = p.z;
+                // PointLight::update: m_radiance = m_power / (4 * M_PI)
+                float d = 4 * 3.14159265358979323846f;
+                em.radiance[0] = pw.x / d; em.radiance[1] = pw.y / d; em.radiance[2] = pw.z / d;
+            } else {
+                throw SceneError("emitter \"" + ch.type + "\" is not supported yet");
+            }
+            sd.emitters.push_back(em);
+        } else if (ch.tag == "denoiser" || ch.tag == "renderer") {
+            // GUI/OptiX-only objects: no effect on the path_mis hot path
+        } else if (ch.tag == "medium") {
+            if (ch.type != "vacuum") throw SceneError("participating media are out of scope for path_mis");
+        } else {
+            throw SceneError("Scene::addChild(<" + ch.tag + ">) is not supported");
+        }
+    }
+    if (!have_integrator) throw SceneError("No integrator was specified!");
+    if (!have_camera) throw SceneError("No camera was specified!");
+    // Scene::update: emitter DiscretePDF
+    sd.emitter_cdf.assign(1, 0.0f);
+    for (auto &e : sd.emitters) sd.emitter_cdf.push_back(sd.emitter_cdf.back() + e.light_prob);
+    float sum = sd.emitter_cdf.back();
+    if (sum > 0) {
+        float norm = 1.0f / sum;
+        for (size_t i = 1; i < sd.emitter_cdf.size(); ++i) sd.emitter_cdf[i] *= norm;
+        sd.emitter_cdf.back() = 1.0f;
+    }
+    camera_update(sd);
+}
+
+}  // namespace
+
+SceneData *load_scene(const std::string &path, int scene_index) {
+    std::ifstream is(path, std::ios::binary);
+    if (is.fail()) throw SceneError("unable to open scene file \"" + path + "\"");
+    std::stringstream ss;
+    ss << is.rdbuf();
+    std::string text = ss.str();
+    std::unique_ptr<XmlNode> root;
+    try {
+        root = xml_parse(text);
+    } catch (const XmlError &e) {
+        throw SceneError("Error while parsing \"" + path + "\": " + e.what());
+    }
+    ParseCtx c{text, path};
+    auto obj = parse_node(*root, nullptr, "", c);
+    const Obj *scene = nullptr;
+    if (obj->tag == "scene") {
+        if (scene_index > 0) throw SceneError("scene index out of range");
+        scene = obj.get();
+    } else if (obj->tag == "test") {
+        int k = 0;
+        for (auto &ch : obj->children)
+            if (ch->tag == "scene" && k++ == scene_index) { scene = ch.get(); break; }
+        if (!scene) throw SceneError("scene index out of range in test file");
+    } else {
+        throw SceneError("root element <" + obj->tag + "> is not a scene");
+    }
+    std::string base_dir;
+    auto slash = path.find_last_of('/');
+    if (slash != std::string::npos) base_dir = path.substr(0, slash);
+    auto sd = std::make_unique<SceneData>();
+    build_scene(*scene, base_dir, *sd);
+    return sd.release();
+}
+
+void fill_desc(const SceneData &sd, nh_scene_desc *d) {
+    std::memset(d, 0, sizeof(*d));
+    d->camera = sd.camera;
+    d->filter = sd.filter;
+    d->integrator = sd.integrator;
+    d->sample_count = sd.sample_count;
+    d->n_shapes = (uint32_t)sd.shapes.size();
+    d->shapes = sd.shapes.data();
+    d->n_bsdfs = (uint32_t)sd.bsdfs.size();
+    d->bsdfs = sd.bsdfs.data();
+    d->n_emitters = (uint32_t)sd.emitters.size();
+    d->emitters = sd.emitters.data();
+    d->emitter_cdf = sd.emitter_cdf.data();
+    d->envmap = sd.envmap;
+    d->n_vertices = (uint32_t)(sd.V.size() / 3);
+    d->V = sd.V.data();
+    d->N = sd.N.data();
+    d->UV = sd.UV.data();
+    d->T = sd.T.data();
+    d->BT = sd.BT.data();
+    d->n_faces = (uint32_t)(sd.F.size() / 3);
+    d->F = sd.F.data();
+    d->n_area_cdf = (uint32_t)sd.area_cdf.size();
+    d->area_cdf = sd.area_cdf.data();
+}
+
+}  // namespace nh
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+struct nh_scene {
+    nh::SceneData *data;
+};
+
+extern "C" {
+
+const char *nh_host_last_error(void) { return nh::g_host_error.c_str(); }
+
+static int load_impl(const char *path, int index, nh_scene **out) {
+    if (!path || !out) { nh::set_host_error("null argument"); return NH_ERR_INVALID; }
+    try {
+        auto *s = new nh_scene{nh::load_scene(path, index)};
+        *out = s;
+        return NH_OK;
+    } catch (const std::exception &e) {
+        nh::set_host_error(e.what());
+        return NH_ERR_IO;
+    }
+}
+
+int nh_scene_load_xml(const char *path, nh_scene **out) { return load_impl(path, 0, out); }
+int nh_scene_load_xml_index(const char *path, int32_t index, nh_scene **out) { return load_impl(path, index, out); }
+
+int nh_scene_get_desc(const nh_scene *scene, nh_scene_desc *out) {
+    if (!scene || !out) { nh::set_host_error("null argument"); return NH_ERR_INVALID; }
+    nh::fill_desc(*scene->data, out);
+    return NH_OK;
+}
+
+int nh_scene_set_resolution(nh_scene *scene, int32_t width, int32_t height) {
+    if (!scene || width <= 0 || height <= 0) { nh::set_host_error("invalid resolution"); return NH_ERR_INVALID; }
+    scene->data->camera.width = width;
+    scene->data->camera.height = height;
+    nh::camera_update(*scene->data);
+    return NH_OK;
+}
+
+int nh_scene_set_sample_count(nh_scene *scene, int32_t spp) {
+    if (!scene || spp <= 0) { nh::set_host_error("invalid sample count"); return NH_ERR_INVALID; }
+    scene->data->sample_count = spp;
+    return NH_OK;
+}
+
+int nh_scene_set_bsdf(nh_scene *scene, uint32_t shape, const nh_bsdf *bsdf) {
+    if (!scene || !bsdf || shape >= scene->data->shapes.size()) { nh::set_host_error("invalid shape index"); return NH_ERR_INVALID; }
+    scene->data->bsdfs.push_back(*bsdf);
+    scene->data->shapes[shape].bsdf = (int32_t)scene->data->bsdfs.size() - 1;
+    return NH_OK;
+}
+
+int nh_scene_set_integrator(nh_scene *scene, int32_t integrator) {
+    if (!scene || (integrator != NH_INTEGRATOR_PATH_MIS && integrator != NH_INTEGRATOR_PATH_MATS)) {
+        nh::set_host_error("invalid integrator");
+        return NH_ERR_INVALID;
+    }
+    scene->data->integrator = integrator;
+    return NH_OK;
+}
+
+void nh_scene_free(nh_scene *scene) {
+    if (!scene) return;
+    delete scene->data;
+    delete scene;
+}
+
+}  // extern "C"

@@ -1,0 +1,161 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of the CPU restatement (oracle/nori_oracle.cpp).
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the
+checker / reported CPU baseline. See nori_oracle.h for what pins this oracle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "optix-renderer_amd"))
+import nori_hip as nh  # noqa: E402  (struct layouts of the shared scene description)
+
+LIB_PATH = os.path.join(_HERE, "_build", "libnori_oracle.so")
+_lib = C.CDLL(LIB_PATH)
+
+PER_PATH, NORI_BLOCK = 0, 1
+PCG32_DEFAULT_STATE = 0x853C49E6748FEA9B
+PCG32_DEFAULT_STREAM = 0xDA3E39CB94B95BDB
+
+_vp, _i32, _u32, _u64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_uint64
+_fp = C.POINTER(C.c_float)
+_u64p = C.POINTER(C.c_uint64)
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+
+
+_sig("no_scene_create", _i32, C.POINTER(nh.nh_scene_desc), C.POINTER(_vp))
+_sig("no_scene_free", None, _vp)
+_sig("no_bvh_info", _i32, _vp, C.POINTER(_u32), C.POINTER(_u32))
+_sig("no_bvh_export", _i32, _vp, C.POINTER(nh.nh_bvh_node), C.POINTER(_u32))
+_sig("no_trace_rays", _i32, _vp, C.POINTER(nh.nh_ray_soa), _i32, _i32, C.POINTER(nh.nh_hit_soa))
+_sig("no_pcg32_seed", None, _u64p, _u64p, _u64, _u64)
+_sig("no_pcg32_next", _u32, _u64p, _u64p)
+_sig("no_path_seed", None, _u64, _u64, _u64, _u64p, _u64p)
+_sig("no_render", _i32, _vp, _i32, _u64, _i32, _i32, C.POINTER(_i32), _i32, _i32, _fp, _u64p)
+_sig("no_path_radiance", _i32, _vp, _u64, _i32, _i32, _i32, _fp, _fp)
+_sig("no_ttest_scene", _i32, _vp, _u64p, _u64p, _i32, C.POINTER(C.c_double), C.POINTER(C.c_double))
+_sig("no_ttest_bsdf", _i32, C.POINTER(nh.nh_bsdf), C.c_float, _u64p, _u64p, _i32, C.POINTER(C.c_double),
+     C.POINTER(C.c_double))
+_sig("no_bsdf_sample", _i32, C.POINTER(nh.nh_bsdf), _fp, _fp, _fp, _fp, _fp, C.POINTER(_i32))
+_sig("no_bsdf_pdf", C.c_float, C.POINTER(nh.nh_bsdf), _fp, _fp)
+
+
+class Pcg32:
+    """pcg32 restatement handle (state/inc live on the Python side)."""
+
+    def __init__(self, state=PCG32_DEFAULT_STATE, inc=PCG32_DEFAULT_STREAM):
+        self.state, self.inc = _u64(state), _u64(inc)
+
+    @classmethod
+    def seeded(cls, initstate, initseq=1):
+        r = cls()
+        _lib.no_pcg32_seed(C.byref(r.state), C.byref(r.inc), initstate, initseq)
+        return r
+
+    @classmethod
+    def per_path(cls, seed, pixel, sample):
+        r = cls()
+        _lib.no_path_seed(seed, pixel, sample, C.byref(r.state), C.byref(r.inc))
+        return r
+
+    def next_uint(self):
+        return _lib.no_pcg32_next(C.byref(self.state), C.byref(self.inc))
+
+    def next_float(self):
+        u = (self.next_uint() >> 9) | 0x3F800000
+        return float(np.array([u], np.uint32).view(np.float32)[0] - np.float32(1.0))
+
+
+class OracleScene:
+    def __init__(self, scene: "nh.Scene"):
+        self._keep = scene
+        d = scene.desc
+        h = _vp()
+        if _lib.no_scene_create(C.byref(d), C.byref(h)) != 0:
+            raise RuntimeError("oracle scene creation failed")
+        self._h = h
+        self.width, self.height, self.border = d.camera.width, d.camera.height, d.filter.border
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.no_scene_free(self._h)
+            self._h = None
+
+    def bvh(self):
+        nn, ni = _u32(), _u32()
+        _lib.no_bvh_info(self._h, C.byref(nn), C.byref(ni))
+        nodes = (nh.nh_bvh_node * max(nn.value, 1))()
+        idx = np.zeros(ni.value, np.uint32)
+        _lib.no_bvh_export(self._h, nodes, idx.ctypes.data_as(C.POINTER(_u32)))
+        raw = np.ctypeslib.as_array(C.cast(nodes, C.POINTER(C.c_uint32)), shape=(max(nn.value, 1) * 8,))
+        return raw.reshape(-1, 8)[: nn.value].copy(), idx
+
+    def trace(self, o, d, mint, maxt, any_hit=False):
+        n = len(o)
+        cols = [np.ascontiguousarray(x, dtype=np.float32) for x in (o[:, 0], o[:, 1], o[:, 2], d[:, 0], d[:, 1],
+                                                                     d[:, 2], mint, maxt)]
+        r = nh.nh_ray_soa(*[c.ctypes.data_as(_fp) for c in cols])
+        res = {"hit": np.zeros(n, np.uint8), "t": np.zeros(n, np.float32), "u": np.zeros(n, np.float32),
+               "v": np.zeros(n, np.float32), "prim": np.zeros(n, np.uint32), "shape": np.zeros(n, np.uint32)}
+        h = nh.nh_hit_soa(res["hit"].ctypes.data_as(C.POINTER(C.c_uint8)), res["t"].ctypes.data_as(_fp),
+                          res["u"].ctypes.data_as(_fp), res["v"].ctypes.data_as(_fp),
+                          res["prim"].ctypes.data_as(C.POINTER(_u32)), res["shape"].ctypes.data_as(C.POINTER(_u32)))
+        _lib.no_trace_rays(self._h, C.byref(r), n, int(any_hit), C.byref(h))
+        return res
+
+    def render(self, s0, s1, seed=0, mode=PER_PATH, blocks=None, threads=None, rgbw=None):
+        if rgbw is None:
+            rgbw = np.zeros((self.height + 2 * self.border, self.width + 2 * self.border, 4), np.float32)
+        threads = threads or os.cpu_count() or 1
+        nb, bp = 0, None
+        keep = None
+        if blocks is not None:
+            keep = np.ascontiguousarray(blocks, np.int32)
+            nb, bp = len(keep), keep.ctypes.data_as(C.POINTER(_i32))
+        inv = _u64()
+        rc = _lib.no_render(self._h, mode, seed, s0, s1, bp, nb, threads, rgbw.ctypes.data_as(_fp), C.byref(inv))
+        if rc != 0:
+            raise RuntimeError(f"oracle render failed ({rc})")
+        self.last_invalid = inv.value
+        return rgbw
+
+    def path(self, seed, px, py, sample):
+        rgb, jit = np.zeros(3, np.float32), np.zeros(2, np.float32)
+        _lib.no_path_radiance(self._h, seed, px, py, sample, rgb.ctypes.data_as(_fp), jit.ctypes.data_as(_fp))
+        return rgb, jit
+
+    def ttest(self, rng: Pcg32, n: int):
+        m, v = C.c_double(), C.c_double()
+        _lib.no_ttest_scene(self._h, C.byref(rng.state), C.byref(rng.inc), n, C.byref(m), C.byref(v))
+        return m.value, v.value
+
+
+def ttest_bsdf(bsdf: "nh.nh_bsdf", angle_deg: float, rng: Pcg32, n: int):
+    m, v = C.c_double(), C.c_double()
+    _lib.no_ttest_bsdf(C.byref(bsdf), angle_deg, C.byref(rng.state), C.byref(rng.inc), n, C.byref(m), C.byref(v))
+    return m.value, v.value
+
+
+def bsdf_sample(bsdf, wi, sample):
+    wi = np.asarray(wi, np.float32)
+    s = np.asarray(sample, np.float32)
+    wo, w, pdf, meas = np.zeros(3, np.float32), np.zeros(3, np.float32), C.c_float(), _i32()
+    _lib.no_bsdf_sample(C.byref(bsdf), wi.ctypes.data_as(_fp), s.ctypes.data_as(_fp), wo.ctypes.data_as(_fp),
+                        w.ctypes.data_as(_fp), C.byref(pdf), C.byref(meas))
+    return wo, w, pdf.value, meas.value
+
+
+def bsdf_pdf(bsdf, wi, wo):
+    wi = np.asarray(wi, np.float32)
+    wo = np.asarray(wo, np.float32)
+    return _lib.no_bsdf_pdf(C.byref(bsdf), wi.ctypes.data_as(_fp), wo.ctypes.data_as(_fp))
