@@ -1,0 +1,18 @@
+#!/usr/bin/env bash
+# Builds reference-side checker binaries from /root/reference sources in place, outputs only
+# into oracle/_ref/ (git-ignored, travels to the GPU box). Only the pcg32 demo compiles
+# from the reference's own files without stand-in headers: every Nori translation unit
+# includes include/nori/common.h -> <ImathPlatform.h> (IlmBase, absent) and the BVH /
+# ImageBlock units need TBB headers (absent), so the renderer itself is unbuildable here.
+set -euo pipefail
+REF=${REFERENCE_ROOT:-/root/reference}
+OUT="$(cd "$(dirname "$0")" && pwd)/_ref"
+if [ ! -d "$REF/ext/pcg32" ]; then
+  echo "build_ref: $REF not present, skipping" >&2
+  exit 0
+fi
+mkdir -p "$OUT"
+# pcg32.h uses std::iter_swap without including <algorithm> (Nori includes it first);
+# -include supplies that standard header, no reference file is altered or stubbed.
+g++ -O2 -std=c++11 -include algorithm -I"$REF/ext/pcg32" "$REF/ext/pcg32/pcg32-demo.cpp" -o "$OUT/pcg32-demo"
+echo "built $OUT/pcg32-demo"

@@ -509,7 +509,8 @@ bool box_intersect(const float *mn, const float *mx, const Ray &ray) {
 }
 
 // BVH::rayIntersect (bvh.cpp:402-460)
-bool bvh_intersect(const no_scene &s, const Ray &_ray, Its &its, bool shadow, uint32_t *out_prim = nullptr) {
+bool bvh_intersect(const no_scene &s, const Ray &_ray, Its &its, bool shadow, uint32_t *out_prim = nullptr,
+                   float *out_bary = nullptr) {
     uint32_t node_idx = 0, stack_idx = 0, stack[64];
     its.t = std::numeric_limits<float>::infinity();
     Ray ray(_ray);
@@ -556,6 +557,7 @@ bool bvh_intersect(const no_scene &s, const Ray &_ray, Its &its, bool shadow, ui
         its.u = hu;
         its.v = hv;
         if (out_prim) *out_prim = s.shape_offset[fshape] + f;
+        if (out_bary) { out_bary[0] = hu; out_bary[1] = hv; }
         set_hit_information(s, fshape, f, ray, its);
     }
     return found;
@@ -1064,12 +1066,13 @@ int no_trace_rays(const no_scene *s, const nh_ray_soa *r, int32_t n, int32_t any
         Ray ray = make_ray(mk(r->ox[i], r->oy[i], r->oz[i]), mk(r->dx[i], r->dy[i], r->dz[i]), r->mint[i], r->maxt[i]);
         Its its;
         uint32_t prim = 0;
-        bool hit = bvh_intersect(*s, ray, its, any_hit != 0, &prim);
+        float bary[2] = {0.f, 0.f};
+        bool hit = bvh_intersect(*s, ray, its, any_hit != 0, &prim, bary);
         out->hit[i] = hit ? 1 : 0;
-        if (!any_hit) {
+        if (!any_hit) {  // u, v: Moller-Trumbore barycentrics (spheres: 0)
             out->t[i] = hit ? its.t : INFINITY;
-            out->u[i] = hit ? its.u : 0.f;
-            out->v[i] = hit ? its.v : 0.f;
+            out->u[i] = hit ? bary[0] : 0.f;
+            out->v[i] = hit ? bary[1] : 0.f;
             if (out->prim) out->prim[i] = hit ? prim : 0xffffffffu;
             if (out->shape) out->shape[i] = hit ? (uint32_t)its.shape : 0xffffffffu;
         }

@@ -1,0 +1,91 @@
+"""Regenerates the committed golden fixtures from the reference checkout (this container only).
+
+    python tests/golden/make_fixtures.py [/root/reference]
+
+Writes (all data, no reference source):
+  pcg32_kat.json          the pcg32 known-answer output (ext/pcg32/pcg32-demo.out), parsed,
+                          cross-checked against oracle/_ref/pcg32-demo built from the reference's
+                          own pcg32-demo.cpp when that binary exists
+  reference_scenes.json   scene inputs the reference's own tests and benchmarks use: the Cornell
+                          box (scenes/pa4/cbox), the path-integrator known-answer tests
+                          (scenes/pa4/tests) and the microfacet BSDF tests (scenes/pa3/tests
+                          ttest/chi2test XML). Stored as {relative path: file text}; tests write
+                          them to a temporary directory and load them through nh_scene_load_xml.
+"""
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+SCENE_FILES = [
+    "scenes/pa4/cbox/cbox_path_mis.xml",
+    "scenes/pa4/cbox/cbox_path_mats.xml",
+    "scenes/pa4/cbox/meshes/walls.obj",
+    "scenes/pa4/cbox/meshes/leftwall.obj",
+    "scenes/pa4/cbox/meshes/rightwall.obj",
+    "scenes/pa4/cbox/meshes/light.obj",
+    "scenes/pa4/tests/test-furnace.xml",
+    "scenes/pa4/tests/test-direct.xml",
+    "scenes/pa4/tests/furnace.obj",
+    "scenes/pa4/tests/floor.obj",
+    "scenes/pa4/tests/polylum1.obj",
+    "scenes/pa4/tests/polylum2.obj",
+    "scenes/pa4/tests/polylum3.obj",
+    "scenes/pa4/tests/polylum4.obj",
+    "scenes/pa4/tests/polylum5.obj",
+    "scenes/pa3/tests/ttest-microfacet.xml",
+    "scenes/pa3/tests/chi2test-microfacet.xml",
+]
+
+
+def parse_demo(text):
+    rounds = []
+    cur = None
+    lines = text.splitlines()
+    i = 0
+    while i < len(lines):
+        ln = lines[i]
+        s = ln.strip()
+        if s.startswith("Round"):
+            cur = {"u32": [], "coins": "", "rolls": [], "cards": []}
+            rounds.append(cur)
+        elif s.startswith("32bit:"):
+            cur["u32"] = [int(x, 16) for x in s.split()[1:]]
+        elif s.startswith("Coins:"):
+            cur["coins"] = s.split()[1]
+        elif s.startswith("Rolls:"):
+            cur["rolls"] = [int(x) for x in s.split()[1:]]
+        elif s.startswith("Cards:"):
+            cards = s.split()[1:]
+            j = i + 1
+            while j < len(lines) and lines[j].startswith("\t"):
+                cards += lines[j].split()
+                j += 1
+            cur["cards"] = cards
+            i = j - 1
+        i += 1
+    return rounds
+
+
+def main():
+    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    demo_out = open(os.path.join(ref, "ext/pcg32/pcg32-demo.out")).read()
+    kat = {"seed": [42, 54], "source": "ext/pcg32/pcg32-demo.out", "rounds": parse_demo(demo_out)}
+    exe = os.path.join(REPO, "oracle", "_ref", "pcg32-demo")
+    if os.path.exists(exe):
+        built = subprocess.run([exe, "5"], capture_output=True, text=True, check=True).stdout
+        assert parse_demo(built) == kat["rounds"], "reference pcg32-demo build disagrees with pcg32-demo.out"
+        kat["cross_checked_with"] = "oracle/_ref/pcg32-demo (built from ext/pcg32/pcg32-demo.cpp)"
+    with open(os.path.join(HERE, "pcg32_kat.json"), "w") as f:
+        json.dump(kat, f, indent=1)
+    scenes = {p: open(os.path.join(ref, p)).read() for p in SCENE_FILES}
+    with open(os.path.join(HERE, "reference_scenes.json"), "w") as f:
+        json.dump(scenes, f, indent=0)
+    print("wrote pcg32_kat.json, reference_scenes.json")
+
+
+if __name__ == "__main__":
+    main()

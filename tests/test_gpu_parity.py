@@ -1,0 +1,163 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on identical inputs.
+
+Traversal results are integer/index work plus fp32 arithmetic done in the same order, so
+they must be bit-exact. Images: rel-L2 < 1e-4 (BASELINE.json north_star tolerance); the
+megakernel and oracle evaluate the same fp32 operations in the same order, so in practice
+they agree to the last bit and the test also reports the max abs difference.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import nori_hip as nh
+import nori_oracle as no
+import scenegen
+
+pytestmark = pytest.mark.gpu
+
+TOL_REL_L2 = 1e-4
+
+
+def rel_l2(a, b):
+    return float(np.sqrt(np.sum((a.astype(np.float64) - b) ** 2) / max(np.sum(b.astype(np.float64) ** 2), 1e-300)))
+
+
+def random_rays(n, lo, hi, seed):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    mint = np.full(n, 1e-4, np.float32)
+    maxt = np.full(n, np.inf, np.float32)
+    # some finite segments and some axis-aligned directions (the d == 0 slab branch)
+    maxt[::7] = rng.uniform(0.1, 3.0, size=maxt[::7].shape).astype(np.float32)
+    d[::11, 0] = 0.0
+    d[::13, 1] = 0.0
+    return o, d.astype(np.float32), mint, maxt
+
+
+def secondary_rays(oracle, n, seed):
+    """Rays leaving surface points (origins on geometry, adaptive epsilon in play)."""
+    o, d, mint, maxt = random_rays(n, -1.0, 2.0, seed)
+    h = oracle.trace(o, d, mint, maxt)
+    m = h["hit"] == 1
+    p = o[m] + h["t"][m][:, None] * d[m]
+    rng = np.random.default_rng(seed + 1)
+    d2 = rng.normal(size=p.shape).astype(np.float32)
+    d2 /= np.linalg.norm(d2, axis=1, keepdims=True)
+    return p.astype(np.float32), d2.astype(np.float32), np.full(len(p), 1e-4, np.float32), \
+        np.full(len(p), np.inf, np.float32)
+
+
+def compare_trace(ctx, oracle, o, d, mint, maxt, traversal):
+    g = ctx.trace(o, d, mint, maxt, any_hit=False, traversal=traversal)
+    r = oracle.trace(o, d, mint, maxt, any_hit=False)
+    np.testing.assert_array_equal(g["hit"], r["hit"])
+    m = r["hit"] == 1
+    np.testing.assert_array_equal(g["t"][m], r["t"][m])
+    np.testing.assert_array_equal(g["prim"][m], r["prim"][m])
+    np.testing.assert_array_equal(g["shape"][m], r["shape"][m])
+    np.testing.assert_array_equal(g["u"][m], r["u"][m])
+    np.testing.assert_array_equal(g["v"][m], r["v"][m])
+    ga = ctx.trace(o, d, mint, maxt, any_hit=True, traversal=traversal)
+    ra = oracle.trace(o, d, mint, maxt, any_hit=True)
+    np.testing.assert_array_equal(ga["hit"], ra["hit"])
+    return int(m.sum())
+
+
+def setup(xml, width=None, height=None):
+    s = nh.Scene(xml)
+    if width:
+        s.set_resolution(width, height)
+    b = nh.Bvh(s)
+    ctx = nh.Context(0)
+    ctx.upload(s, b)
+    return s, b, ctx
+
+
+@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED])
+def test_trace_parity_cbox(gpu, scene_dir, traversal):
+    s, b, ctx = setup(os.path.join(scene_dir, "scenes/pa4/cbox/cbox_path_mis.xml"))
+    orc = no.OracleScene(s)
+    hits = compare_trace(ctx, orc, *random_rays(20000, -1.2, 2.0, 7), traversal)
+    assert hits > 5000
+    compare_trace(ctx, orc, *secondary_rays(orc, 20000, 11), traversal)
+
+
+@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED])
+def test_trace_parity_bumpy_mesh(gpu, tmp_path, traversal):
+    xml, ntri = scenegen.bumpy_cbox_xml(str(tmp_path), 200, 100)
+    assert ntri > 30000
+    s, b, ctx = setup(xml)
+    orc = no.OracleScene(s)
+    compare_trace(ctx, orc, *random_rays(20000, -0.6, 1.2, 3), traversal)
+    compare_trace(ctx, orc, *secondary_rays(orc, 20000, 5), traversal)
+
+
+def render_pair(xml, w, h, spp, seed=5, traversal=nh.TRAVERSAL_REFERENCE, integrator=None):
+    s = nh.Scene(xml)
+    s.set_resolution(w, h)
+    if integrator is not None:
+        s.set_integrator(integrator)
+    b = nh.Bvh(s)
+    ctx = nh.Context(0)
+    ctx.upload(s, b)
+    ctx.render(0, spp, seed=seed, traversal=traversal, clear=True)
+    g = ctx.framebuffer()
+    r = no.OracleScene(s).render(0, spp, seed=seed)
+    return g, r, s
+
+
+@pytest.mark.parametrize("variant", ["c1", "c2"])
+@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED])
+def test_render_parity_cbox(gpu, tmp_path, variant, traversal):
+    xml = scenegen.cbox_xml(str(tmp_path), variant)
+    g, r, s = render_pair(xml, 64, 48, 16, traversal=traversal)
+    e = rel_l2(g, r)
+    print(f"{variant} traversal={traversal}: rel-L2 {e:.3e}, max|d| {np.abs(g - r).max():.3e}")
+    assert e < TOL_REL_L2
+    img_g, img_r = nh.to_rgb(g, s.border), nh.to_rgb(r, s.border)
+    assert rel_l2(img_g, img_r) < TOL_REL_L2
+    assert img_r.mean() > 0.05
+
+
+def test_render_parity_path_mats(gpu, tmp_path):
+    xml = scenegen.cbox_xml(str(tmp_path), "c1")
+    g, r, _ = render_pair(xml, 48, 48, 16, integrator=nh.INTEGRATOR_PATH_MATS)
+    assert rel_l2(g, r) < TOL_REL_L2
+
+
+def test_render_parity_microfacet_mesh(gpu, tmp_path):
+    xml, _ = scenegen.bumpy_cbox_xml(str(tmp_path), 120, 60)
+    g, r, _ = render_pair(xml, 48, 40, 8, traversal=nh.TRAVERSAL_ORDERED)
+    e = rel_l2(g, r)
+    print(f"microfacet mesh rel-L2 {e:.3e}")
+    assert e < TOL_REL_L2
+
+
+def test_render_deterministic_and_sharded(gpu, tmp_path):
+    """Two identical renders are bitwise equal; rendering two disjoint block sets into two
+    framebuffers and summing equals the full render up to fp32 summation order."""
+    xml = scenegen.cbox_xml(str(tmp_path), "c1")
+    s = nh.Scene(xml)
+    s.set_resolution(96, 80)
+    b = nh.Bvh(s)
+    ctx = nh.Context(0)
+    ctx.upload(s, b)
+    ctx.render(0, 8, seed=3, clear=True)
+    full = ctx.framebuffer()
+    ctx.render(0, 8, seed=3, clear=True)
+    np.testing.assert_array_equal(full, ctx.framebuffer())
+    nb = 3 * 3
+    parts = []
+    for r in range(2):
+        c2 = nh.Context(0)
+        c2.upload(s, b)
+        c2.render(0, 8, seed=3, blocks=list(range(r, nb, 2)), clear=True)
+        parts.append(c2.framebuffer())
+    assert rel_l2(parts[0] + parts[1], full) < 1e-6
+    # sample-range split accumulates: [0,3) + [3,8) == [0,8) up to summation order
+    ctx.render(0, 3, seed=3, clear=True)
+    ctx.render(3, 8, seed=3, clear=False)
+    assert rel_l2(ctx.framebuffer(), full) < 1e-6
