@@ -1,0 +1,234 @@
+"""Benchmark of the MI355X path_mis hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--traversal ordered]
+
+Workload (N=1, BASELINE.json configs[1]): Cornell box diffuse-only (C2: both spheres
+diffuse), 1024x1024, 256 spp, path_mis, per-path pcg32 seeding. One step = `--rounds`
+(default 16) sample rounds over the whole image, i.e. one nh_render call = one path
+megakernel launch + one ImageBlock splat launch; the default K=16 steps render the full
+256 spp. Multi-GPU: one process per GPU (torchrun), 32x32 image blocks dealt round-robin
+to ranks (tile shard, fixed total image => strong scaling), one RCCL reduce (sum) of the
+RGBW framebuffer to rank 0 inside the timed region.
+
+The JSON line also carries:
+  roofline      path megakernel: algorithmic bytes per launch (BVH nodes x 64 B + primitive
+                tests x 48 B + 20 B sample record per path, counted in-kernel in a separate
+                calibration launch on the same seeds) / average launch time from HIP events on
+                the kernel's stream, against 8 TB/s HBM; traffic from the committed rocprofv3
+                PMC summary when one exists for this workload, else null
+  cpu_baseline  the CPU oracle (oracle/, a restatement of the reference's path_mis) timed on
+                this host on a bounded sample of the same workload (rank 0, N=1 only)
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "optix-renderer_amd"))
+
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
+NODE_BYTES, PRIM_BYTES, RECORD_BYTES = 64, 48, 20
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=16)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--rounds", type=int, default=16, help="sample rounds per step")
+    p.add_argument("--config", default="c2", choices=["c1", "c2", "c4", "bumpy1m"])
+    p.add_argument("--width", type=int, default=None)
+    p.add_argument("--height", type=int, default=None)
+    p.add_argument("--traversal", default="ordered", choices=["ordered", "reference"])
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-calibrate", action="store_true")
+    p.add_argument("--seed", type=int, default=1234)
+    return p.parse_args()
+
+
+def build_scene(args, tmp):
+    import scenegen
+    if args.config in ("c1", "c2", "c4"):
+        w = args.width or (2048 if args.config == "c4" else 1024)
+        h = args.height or w
+        xml = scenegen.cbox_xml(tmp, "c2" if args.config == "c2" else "c1", width=w, height=h)
+        desc = f"Cornell box ({'diffuse-only' if args.config == 'c2' else 'mirror+dielectric'}) {w}x{h}"
+    else:
+        w = args.width or 1024
+        h = args.height or w
+        xml, ntri = scenegen.bumpy_cbox_xml(tmp, 2000, 250, width=w, height=h)
+        desc = f"cbox + synthetic bumpy sphere ({ntri} tris, Beckmann microfacet) {w}x{h}"
+    return xml, w, h, desc
+
+
+def pmc_traffic(workload_key):
+    """HBM bytes per path-kernel launch from a committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        data = json.load(open(path))
+        return data.get(workload_key, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(scene, budget_s, seed):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import nori_oracle as no
+    threads = int(os.environ.get("NH_CPU_THREADS", "16"))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    orc = no.OracleScene(scene)
+    rgbw = None
+    t0 = time.perf_counter()
+    rounds = 0
+    while True:
+        rgbw = orc.render(rounds, rounds + 1, seed=seed, threads=threads, rgbw=rgbw)
+        rounds += 1
+        if time.perf_counter() - t0 >= budget_s or rounds >= 256:
+            break
+    dt = time.perf_counter() - t0
+    n = rounds * orc.width * orc.height
+    return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{rounds} spp of the same {orc.width}x{orc.height} image ({n} samples, {dt:.1f} s), "
+                      f"oracle/nori_oracle.cpp restatement of path_mis, {threads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import nori_hip as nh
+
+    tmp = tempfile.mkdtemp(prefix="nh_bench_")
+    xml, W, H, scene_desc = build_scene(args, tmp)
+    scene = nh.Scene(xml)
+    t0 = time.perf_counter()
+    bvh = nh.Bvh(scene, n_threads=16)
+    bvh_s = time.perf_counter() - t0
+    ctx = nh.Context(local)
+    t0 = time.perf_counter()
+    ctx.upload(scene, bvh)
+    upload_s = time.perf_counter() - t0
+    nbx, nby = (W + 31) // 32, (H + 31) // 32
+    blocks = [b for b in range(nbx * nby) if b % world == rank] if world > 1 else None
+    trav = nh.TRAVERSAL_ORDERED if args.traversal == "ordered" else nh.TRAVERSAL_REFERENCE
+    R = args.rounds
+
+    # calibration launch (in-kernel counters; same seeds as the first timed step)
+    calib = None
+    if not args.no_calibrate:
+        ctx.reset_stats()
+        ctx.render(0, R, seed=args.seed, blocks=blocks, traversal=trav, clear=True, stats=True)
+        calib = ctx.stats()
+
+    # warmup (rounds past the timed range, separate framebuffer content)
+    for w in range(args.warmup):
+        ctx.render(R * (args.steps + w), R * (args.steps + w + 1), seed=args.seed, blocks=blocks, traversal=trav,
+                   clear=(w == 0))
+    ctx.synchronize()
+    ctx.reset_stats()
+    if dist is not None:
+        import torch
+        torch.cuda.synchronize()
+        dist.barrier()
+    ctx.render(0, 0, seed=args.seed, blocks=blocks, traversal=trav, clear=True)
+    ctx.synchronize()
+    t_start = time.perf_counter()
+    for s in range(args.steps):
+        ctx.render(s * R, (s + 1) * R, seed=args.seed, blocks=blocks, traversal=trav, clear=False)
+    if dist is not None:
+        ptr, n = ctx.framebuffer_device_ptr()
+        ctx.synchronize()
+        fb = _wrap_device(ptr, n, local)
+        dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+    ctx.synchronize()
+    t_end = time.perf_counter()
+    elapsed = t_end - t_start
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = ctx.stats()
+    total_samples = W * H * R * args.steps
+
+    if rank == 0:
+        value = total_samples / elapsed / 1e6
+        # roofline of the path megakernel (dominant kernel)
+        roof = None
+        if calib is not None and calib["samples"] > 0:
+            paths = calib["samples"]
+            bytes_calib = calib["nodes_visited"] * NODE_BYTES + calib["prims_tested"] * PRIM_BYTES + paths * RECORD_BYTES
+            bytes_per_sample = bytes_calib / paths
+            launches = max(st["launches_path"], 1)
+            avg_ms = st["kernel_ms_path"] / launches
+            samples_per_launch = st["samples"] / launches
+            bytes_per_launch = bytes_per_sample * samples_per_launch
+            achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+            key = f"{args.config}_{W}x{H}_r{R}_{args.traversal}"
+            traffic = pmc_traffic(key)
+            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "nh_path_kernel", "avg_launch_ms": round(avg_ms, 4),
+                    "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                    "bytes_per_sample": round(bytes_per_sample, 1),
+                    "ray_queries_per_sample": round(calib["ray_queries"] / paths, 3),
+                    "nodes_per_query": round(calib["nodes_visited"] / max(calib["ray_queries"], 1), 3),
+                    "prims_per_query": round(calib["prims_tested"] / max(calib["ray_queries"], 1), 3),
+                    "splat_ms_per_launch": round(st["kernel_ms_splat"] / max(st["launches_splat"], 1), 4)}
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(scene, args.cpu_seconds, args.seed)
+        line = {
+            "metric": "Msamples/sec (whole node) + traversal HBM GB/s, cbox 1024x1024 256spp",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (reference Cornell box scene files, per-path pcg32 seeds)",
+            "config": {"workload": f"{scene_desc}, {R * args.steps} spp, path_mis", "config": args.config,
+                       "width": W, "height": H, "spp": R * args.steps, "rounds_per_step": R,
+                       "mode": "megakernel", "traversal": args.traversal,
+                       "parallelism": f"tile-shard x{world} + RCCL reduce" if world > 1 else "single GPU",
+                       "bvh_build_s": round(bvh_s, 3), "upload_s": round(upload_s, 3)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _wrap_device(ptr, n, device):
+    """torch view of the context's device framebuffer (fp32, n elements) for RCCL."""
+    import torch
+
+    class _CAI:
+        __cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (ptr, False), "version": 3}
+
+    return torch.as_tensor(_CAI(), device=f"cuda:{device}")
+
+
+if __name__ == "__main__":
+    main()
