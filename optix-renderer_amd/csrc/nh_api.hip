@@ -35,6 +35,7 @@ struct nh_ctx {
     int width = 0, height = 0, border = 0, n_emitters = 0, integrator = 0;
     nh_filter filter{};
     nhd::DScene S{};
+    nhd::DScene *d_scene = nullptr;  // device copy of S read by the kernels
     nhd::Traversal tv{};
     std::vector<void *> scene_bufs, bvh_bufs;
     bool has_scene = false, has_bvh = false;
@@ -46,6 +47,10 @@ struct nh_ctx {
     float *rec_jy = nullptr;
     size_t rec_cap = 0;  // entries
     int *pixel_list = nullptr, *pixel_map = nullptr, *block_rank = nullptr;
+    int *block_ids = nullptr, *block_slot = nullptr;
+    int n_blocks = 0;
+    float4 *staging = nullptr;
+    size_t staging_cap = 0;  // float4 entries
     int n_list = 0, nbx = 0, nby = 0;
     std::vector<int32_t> list_key;
     bool have_list = false;
@@ -154,7 +159,11 @@ void nh_destroy(nh_ctx *c) {
     hipFree(c->pixel_list);
     hipFree(c->pixel_map);
     hipFree(c->block_rank);
+    hipFree(c->block_ids);
+    hipFree(c->block_slot);
+    hipFree(c->staging);
     hipFree(c->counters);
+    hipFree(c->d_scene);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -367,6 +376,8 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     c->bvh_indices.assign(b->indices, b->indices + b->n_indices);
     c->shape_offset = off;
     c->depth = (int)b->max_depth + 2;
+    if (!c->d_scene) HIP_TRY(c, hipMalloc(&c->d_scene, sizeof(nhd::DScene)));
+    HIP_TRY(c, hipMemcpyAsync(c->d_scene, &c->S, sizeof(nhd::DScene), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->has_bvh = true;
     return NH_OK;
@@ -392,7 +403,7 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
     HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.u = (float *)p;
     HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.v = (float *)p;
     HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.k = (int *)p;
-    nh::launch_trace(c->S, c->tv, rb, hb, n, any_hit != 0, traversal == NH_TRAVERSAL_ORDERED, false, c->depth,
+    nh::launch_trace(c->d_scene, c->tv, rb, hb, n, any_hit != 0, traversal == NH_TRAVERSAL_ORDERED, false, c->depth,
                      c->counters, c->stream);
     HIP_TRY(c, hipGetLastError());
     std::vector<int> k(nn);
@@ -438,9 +449,19 @@ static int ensure_pixel_list(nh_ctx *c, const nh_render_req *q) {
                 list.push_back(pix);
             }
     }
+    std::vector<int> slot_map((size_t)c->nbx * c->nby, -1);
+    for (size_t i = 0; i < blocks.size(); ++i) slot_map[blocks[i]] = (int)i;
     hipFree(c->pixel_list);
     hipFree(c->pixel_map);
-    c->pixel_list = c->pixel_map = nullptr;
+    hipFree(c->block_ids);
+    hipFree(c->block_slot);
+    c->pixel_list = c->pixel_map = c->block_ids = c->block_slot = nullptr;
+    HIP_TRY(c, hipMalloc(&c->block_ids, std::max<size_t>(blocks.size(), 1) * sizeof(int)));
+    HIP_TRY(c, hipMalloc(&c->block_slot, slot_map.size() * sizeof(int)));
+    if (!blocks.empty())
+        HIP_TRY(c, hipMemcpyAsync(c->block_ids, blocks.data(), blocks.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->block_slot, slot_map.data(), slot_map.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    c->n_blocks = (int)blocks.size();
     HIP_TRY(c, hipMalloc(&c->pixel_list, std::max<size_t>(list.size(), 1) * sizeof(int)));
     HIP_TRY(c, hipMalloc(&c->pixel_map, map.size() * sizeof(int)));
     if (!list.empty())
@@ -469,7 +490,10 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     size_t budget = (size_t)1 << 30;
     if (const char *e = std::getenv("NH_RECORD_BUDGET_MB")) budget = (size_t)std::max(1L, std::atol(e)) << 20;
     size_t per_round = (size_t)c->n_list;
-    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / (per_round * 20)));
+    if (c->border > 4) return fail(c, "reconstruction filters wider than border 4 are not supported"), NH_ERR_UNSUPPORTED;
+    const size_t block_px = (size_t)(32 + 2 * c->border) * (32 + 2 * c->border);
+    const size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px * 16;
+    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / per_round_bytes));
     while ((size_t)chunk * per_round > (size_t)0x7fffffff) chunk = std::max(1, chunk / 2);
     if (c->rec_cap < (size_t)chunk * per_round) {
         hipFree(c->rec);
@@ -479,6 +503,12 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         c->rec_cap = (size_t)chunk * per_round;
         HIP_TRY(c, hipMalloc(&c->rec, c->rec_cap * sizeof(float4)));
         HIP_TRY(c, hipMalloc(&c->rec_jy, c->rec_cap * sizeof(float)));
+    }
+    if (c->staging_cap < (size_t)chunk * c->n_blocks * block_px) {
+        hipFree(c->staging);
+        c->staging = nullptr;
+        c->staging_cap = (size_t)chunk * c->n_blocks * block_px;
+        HIP_TRY(c, hipMalloc(&c->staging, c->staging_cap * sizeof(float4)));
     }
     if (q->collect_stats) HIP_TRY(c, hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), c->stream));
     struct Ev {
@@ -512,12 +542,16 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         P.radius = c->filter.radius;
         P.lookup = c->filter.lookup_factor;
         std::memcpy(P.table, c->filter.table, sizeof(P.table));
+        P.blocks = c->block_ids;
+        P.block_slot = c->block_slot;
+        P.n_blocks = c->n_blocks;
+        P.staging = c->staging;
         Ev ev;
         HIP_TRY(c, hipEventCreate(&ev.a));
         HIP_TRY(c, hipEventCreate(&ev.b));
         HIP_TRY(c, hipEventCreate(&ev.d));
         HIP_TRY(c, hipEventRecord(ev.a, c->stream));
-        nh::launch_path(c->S, c->tv, L, q->traversal == NH_TRAVERSAL_ORDERED, q->collect_stats != 0, c->depth, c->stream);
+        nh::launch_path(c->d_scene, c->tv, L, q->traversal == NH_TRAVERSAL_ORDERED, q->collect_stats != 0, c->depth, c->stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev.b, c->stream));
         if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters + 4, c->stream);

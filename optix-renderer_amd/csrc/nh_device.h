@@ -24,6 +24,39 @@ constexpr uint64_t kPcgMult = 0x5851f42d4c957f2dULL;
 
 NHD float f_sin(float x) { return (float)sin((double)x); }
 NHD float f_cos(float x) { return (float)cos((double)x); }
+
+// sin and cos of one fp32 argument in [-8, 8] (every device call site passes a warp angle
+// in [0, 2*pi]), evaluated in fp64 to ~1 ulp and rounded once: the fp32 results equal the
+// correctly rounded sinf/cosf except on ~2^-29 of inputs. One shared reduction
+// x = k*pi/2 + r (two-part Cody-Waite: k*PIO2_HI is exact for |k| < 2^20) and the classic
+// degree-13 / degree-14 minimax kernels on |r| <= pi/4 (public-domain fdlibm constants).
+// Much smaller than the general fp64 library routines (no large-argument path), which
+// matters for the megakernel's register budget.
+NHD void f_sincos(float xf, float &s_out, float &c_out) {
+    const double x = (double)xf;
+    const double k = __builtin_rint(x * 6.36619772367581382433e-01);  // 2/pi
+    const double r = (x - k * 1.57079632673412561417e+00) - k * 6.07710050650619224932e-11;
+    const double z = r * r;
+    const double sp = r + r * z * (-1.66666666666666324348e-01 +
+                                   z * (8.33333333332248946124e-03 +
+                                        z * (-1.98412698298579493134e-04 +
+                                             z * (2.75573137070700676789e-06 +
+                                                  z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)))));
+    const double cp = 1.0 - 0.5 * z +
+                      z * z * (4.16666666666666019037e-02 +
+                               z * (-1.38888888888741095749e-03 +
+                                    z * (2.48015872894767294178e-05 +
+                                         z * (-2.75573143513906633035e-07 +
+                                              z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+    const int q = ((int)k) & 3;
+    double sv, cv;
+    if (q == 0) { sv = sp; cv = cp; }
+    else if (q == 1) { sv = cp; cv = -sp; }
+    else if (q == 2) { sv = -sp; cv = -cp; }
+    else { sv = -cp; cv = sp; }
+    s_out = (float)sv;
+    c_out = (float)cv;
+}
 NHD float f_exp(float x) { return (float)exp((double)x); }
 NHD float f_log(float x) { return (float)log((double)x); }
 NHD float f_acos(float x) { return (float)acos((double)x); }
@@ -183,7 +216,9 @@ NHD float fresnel(float cos_i, float ext_ior, float int_ior) {
 NHD F3 cosine_hemisphere(float sx, float sy) {  // warp.cpp:48-52, 111-122
     float rho = f_sqrt(sx);
     float theta = sy * 2.0f * kPi;
-    float x = rho * f_cos(theta), y = rho * f_sin(theta);
+    float st, ct;
+    f_sincos(theta, st, ct);
+    float x = rho * ct, y = rho * st;
     return f3(x, y, f_sqrt(1.f - (x * x + y * y)));
 }
 NHD F3 beckmann(float sx, float sy, float alpha) {  // warp.cpp:131-150
@@ -193,7 +228,9 @@ NHD F3 beckmann(float sx, float sy, float alpha) {  // warp.cpp:131-150
     float phi = sy * 2.f * kPi;
     float ct = 1.f / f_sqrt(1 + tan2);
     float st = f_sqrt(1.f - ct * ct);
-    F3 r = f3(st * f_cos(phi), st * f_sin(phi), ct);
+    float sphi, cphi;
+    f_sincos(phi, sphi, cphi);
+    F3 r = f3(st * cphi, st * sphi, ct);
     if (r.z < 0) r = neg(r);
     return r;
 }
@@ -202,8 +239,10 @@ NHD F3 uniform_sphere(float sx, float sy) {  // warp.cpp:74-82
     w.z = 2.0f * sx - 1.0f;
     float r = f_sqrt(1.0f - w.z * w.z);
     float sigma = 2.0f * kPi * sy;
-    w.x = r * f_cos(sigma);
-    w.y = r * f_sin(sigma);
+    float ss, cs;
+    f_sincos(sigma, ss, cs);
+    w.x = r * cs;
+    w.y = r * ss;
     return normalized(w);
 }
 

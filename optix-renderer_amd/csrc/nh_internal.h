@@ -33,12 +33,17 @@ struct SplatLaunch {
     const float *rec_jy;
     float radius, lookup;
     float table[33];
+    // block-local ImageBlocks (one per (round, rendered block)), (32+2b)^2 RGBW each
+    const int *blocks;      // rendered block ids, slot order
+    const int *block_slot;  // block id -> slot or -1
+    int n_blocks;
+    float4 *staging;
 };
 
 namespace nh {
-void launch_trace(const nhd::DScene &S, const nhd::Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n,
+void launch_trace(const nhd::DScene *S, const nhd::Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n,
                   bool any, bool ordered, bool stats, int depth, unsigned long long *ctr, hipStream_t st);
-void launch_path(const nhd::DScene &S, const nhd::Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
+void launch_path(const nhd::DScene *S, const nhd::Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
                  int depth, hipStream_t st);
 void launch_splat(const SplatLaunch &P, hipStream_t st);
 void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st);

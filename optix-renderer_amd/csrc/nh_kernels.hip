@@ -5,12 +5,18 @@
 //                     renderBlock's per-pixel body + PathMISIntegrator::Li / PathMatsIntegrator::Li
 //                     (src/utils/render.cpp:436-458, src/integrators/path_mis.cpp:16-150,
 //                     path_mats.cpp:16-78), writing (radiance, jitter) sample records
-//   nh_splat_kernel   ImageBlock::put(pos, value) into per-block blocks + ImageBlock::put(block)
-//                     into the master (src/utils/block.cpp:93-134) as a gather per master
-//                     pixel that reproduces the reference's summation order: per round, blocks
-//                     in BlockGenerator spiral order, within a block samples in
-//                     getSampleIndices order (x outer, y inner)
+//   nh_block_splat_kernel  ImageBlock::put(pos, value) into each (round, block)'s own
+//                     ImageBlock in LDS, samples in getSampleIndices order (x outer, y inner)
+//   nh_merge_kernel   ImageBlock::put(block) into the master (src/utils/block.cpp:93-134):
+//                     per master pixel, rounds in order, blocks in BlockGenerator spiral order
+//                     -- the serial reference's summation order, bit for bit
+#include <cstdlib>
+
 #include "nh_internal.h"
+
+#ifndef NH_DEFAULT_PATH_WAVES
+#define NH_DEFAULT_PATH_WAVES 4
+#endif
 #include "nh_traverse.h"
 
 using namespace nhd;
@@ -184,8 +190,13 @@ __device__ __forceinline__ bool closest(const Traversal &tv, const DScene &S, F3
     return trace<DEPTH, ORDERED, false, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st);
 }
 
-// PathMISIntegrator::Li (src/integrators/path_mis.cpp:16-150). The BSDF-sampled ray is
-// both the MIS probe (:117-119) and the next bounce (:146 -> :34): it is traced once.
+// PathMISIntegrator::Li (src/integrators/path_mis.cpp:16-150). Lanes of a wave stay in
+// lockstep: shade, then one shadow traversal (any hit, :89) for the lanes that sample a
+// light, then one closest-hit traversal of the BSDF-sampled ray for every lane -- that ray
+// is both the MIS probe (:117-119) and the next bounce (:146 -> :34) and is traced once.
+// Everything that does not depend on a traversal result is evaluated before it (pure
+// functions, same operands, same random-number draw order: traversals draw nothing), which
+// keeps the state that is live across traversals small.
 template <int DEPTH, bool ORDERED, bool STATS>
 __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, F3 d, float mint, float maxt,
                           uint2 *stk, int stride, TravStats &st, uint32_t &queries) {
@@ -194,70 +205,78 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
     const float n_lights = (float)S.n_emitters;
     Hit h;
     if (STATS) queries++;
-    bool found = closest<DEPTH, ORDERED, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st);
-    Its its;
-    if (found) hit_info(S, tv, h, o, d, its);
-    while (true) {
-        if (!found) break;  // no environment map: nothing is added on a miss (path_mis.cpp:34-44)
+    bool found = trace<DEPTH, ORDERED, false, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st);
+    while (found) {
+        Its its;
+        hit_info(S, tv, h, o, d, its);
         const DShape shape = S.shapes[its.shape];
         const DBsdf bsdf = S.bsdfs[shape.bsdf];
-        if (shape.emitter >= 0) {
+        if (shape.emitter >= 0) {  // path_mis.cpp:51-56
             const DEmitter em = S.emitters[shape.emitter];
-            F3 wi = normalized(sub(its.p, o));
-            F3 e = emitter_eval(em, o, its.sh.n, wi);
-            li = add(li, mulc(scl(w_mats, t), e));
+            const F3 wi = normalized(sub(its.p, o));
+            li = add(li, mulc(scl(w_mats, t), emitter_eval(em, o, its.sh.n, wi)));
         }
-        float succ = e_min(max_coeff(t), 0.99f);
+        float succ = e_min(max_coeff(t), 0.99f);  // RR from depth 0 (path_mis.cpp:58-71)
         succ = e_max(succ, kEps);
         if (rng.next1d() > succ) break;
         t = divs(t, succ);
 
-        // ---- emitter sampling (path_mis.cpp:75-106)
+        // emitter sampling (path_mis.cpp:75-102)
         const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, rng.next1d());
         const DEmitter em = S.emitters[ei];
         const float ex = rng.next1d(), ey = rng.next1d();
         ESample es;
-        F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
-        F3 we = to_local(its.sh, es.wi);
+        const F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
         const F3 wi_l = to_local(its.sh, neg(d));
+        const bool nee = !is_zero(ems_col);
         F3 li_ems = f3(0, 0, 0);
         float pdfems = 0.f, pdfems_mats = 0.f;
-        if (!is_zero(ems_col)) {
+        if (nee) {
+            const F3 we = to_local(its.sh, es.wi);
+            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
+            const float cs = we.z;
+            li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
+                        ems_col.z * cs * f.z * n_lights);
+            pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
+            pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
+        }
+        // BSDF sampling (path_mis.cpp:109-113)
+        const float bx = rng.next1d(), by = rng.next1d();
+        F3 wo;
+        int measure;
+        const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
+        const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);  // used only if the probe hits an emitter
+        const F3 nd = to_world(its.sh, wo);
+        const F3 no = its.p;
+
+        if (nee) {  // shadow ray (path_mis.cpp:89): occluded -> no contribution, pdfs stay 0
             Hit hs;
             if (STATS) queries++;
-            if (!trace<DEPTH, ORDERED, true, STATS>(tv, S, es.so, es.sd, es.smint, es.smaxt, hs, stk, stride, st)) {
-                F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
-                float cs = we.z;
-                li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
-                            ems_col.z * cs * f.z * n_lights);
-                pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
-                pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
+            if (trace<DEPTH, ORDERED, true, STATS>(tv, S, es.so, es.sd, es.smint, es.smaxt, hs, stk, stride, st)) {
+                li_ems = f3(0, 0, 0);
+                pdfems = 0.f;
+                pdfems_mats = 0.f;
             }
         }
         if ((pdfems_mats + pdfems) > kEps) w_ems = pdfems / (pdfems_mats + pdfems);
 
-        // ---- BSDF sampling + probe (path_mis.cpp:108-146)
-        const float bx = rng.next1d(), by = rng.next1d();
-        F3 wo;
-        int measure;
-        F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
-        const F3 nd = to_world(its.sh, wo);
-        const F3 no = its.p;
-        Its its_s;
+        // probe ray == next bounce (path_mis.cpp:115-146); a zero direction misses every
+        // primitive (det == 0 / NaN roots), so its traversal is skipped
         if (nd.x == 0 && nd.y == 0 && nd.z == 0) {
-            found = false;  // zero direction: every primitive test rejects (det == 0 / NaN roots)
+            found = false;
         } else {
             if (STATS) queries++;
-            found = closest<DEPTH, ORDERED, STATS>(tv, S, no, nd, kEps, INFINITY, h, stk, stride, st);
-            if (found) hit_info(S, tv, h, no, nd, its_s);
+            found = trace<DEPTH, ORDERED, false, STATS>(tv, S, no, nd, kEps, INFINITY, h, stk, stride, st);
         }
         if (!is_zero(bsdf_col) && found) {
-            const DShape hs = S.shapes[its_s.shape];
-            if (hs.emitter >= 0) {
-                const DEmitter em2 = S.emitters[hs.emitter];
-                F3 wim = normalized(sub(its_s.p, its.p));
-                float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
-                float pdfmat_ems = emitter_pdf(S, em2, its.p, its_s.p, its_s.sh.n, wim) / n_lights;
+            const int hs_shape = __float_as_int(tv.prims[3 * h.k + 1].w);
+            const int hem = S.shapes[hs_shape].emitter;
+            if (hem >= 0) {
+                Its its_s;
+                hit_info(S, tv, h, no, nd, its_s);
+                const DEmitter em2 = S.emitters[hem];
+                const F3 wim = normalized(sub(its_s.p, no));
+                const float pdfmat_ems = emitter_pdf(S, em2, no, its_s.p, its_s.sh.n, wim) / n_lights;
                 if ((pdfmat + pdfmat_ems) > kEps) w_mats = pdfmat / (pdfmat + pdfmat_ems);
             }
         }
@@ -269,7 +288,6 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
         t = mulc(t, bsdf_col);
         o = no;
         d = nd;
-        its = its_s;
     }
     return li;
 }
@@ -330,9 +348,10 @@ __device__ __forceinline__ void flush_stats(const TravStats &st, uint32_t querie
 }  // namespace
 
 template <int BLOCK, int DEPTH, bool ORDERED, bool ANY, bool STATS>
-__global__ __launch_bounds__(BLOCK) void nh_trace_kernel(DScene S, Traversal tv, RayBatch rb, HitBatch hb, int n,
-                                                         unsigned long long *counters) {
+__global__ __launch_bounds__(BLOCK) void nh_trace_kernel(const DScene *__restrict__ Sp, Traversal tv, RayBatch rb,
+                                                         HitBatch hb, int n, unsigned long long *counters) {
     __shared__ uint2 stk[DEPTH * BLOCK];
+    const DScene &S = *Sp;
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     TravStats st{0, 0, 0};
     if (i < n) {
@@ -350,9 +369,10 @@ __global__ __launch_bounds__(BLOCK) void nh_trace_kernel(DScene S, Traversal tv,
     if (STATS) flush_stats(st, i < n ? 1u : 0u, counters);
 }
 
-template <int BLOCK, int DEPTH, bool ORDERED, bool STATS>
-__global__ __launch_bounds__(BLOCK) void nh_path_kernel(DScene S, Traversal tv, PathLaunch L) {
+template <int BLOCK, int DEPTH, bool ORDERED, bool STATS, int MINW>
+__global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__restrict__ Sp, Traversal tv, PathLaunch L) {
     __shared__ uint2 stk[DEPTH * BLOCK];
+    const DScene &S = *Sp;
     const int gid = blockIdx.x * BLOCK + threadIdx.x;
     TravStats st{0, 0, 0};
     uint32_t queries = 0;
@@ -380,69 +400,123 @@ __global__ __launch_bounds__(BLOCK) void nh_path_kernel(DScene S, Traversal tv, 
     if (STATS) flush_stats(st, queries, L.counters);
 }
 
-// One thread per master-block pixel; loops over the chunk's rounds.
-__global__ __launch_bounds__(256) void nh_splat_kernel(SplatLaunch P) {
+// ImageBlock::put(pos, value) into the per-block ImageBlock of one (round, block)
+// (src/utils/render.cpp:421-458 + src/utils/block.cpp:93-123). One workgroup per
+// (block, round): phase 1 computes every sample's filter footprint once into LDS; phase 2
+// gives each block-array pixel the ordered sum of its contributions, in the reference's
+// getSampleIndices order (x outer, y inner), starting from the cleared block (0).
+constexpr int kSplatMaxCols = 40;  // 32 + 2*border, border <= 4
+__global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
+    // sample (lx, ly) lives at lx*33 + ly: neighbouring lanes step lx, the odd stride keeps
+    // them on distinct LDS banks
+    __shared__ float s_val[3][32 * 33];
+    __shared__ float s_pos[2][32 * 33];
+    __shared__ int s_box[32 * 33];  // x0 | x1<<8 | y0<<16 | y1<<24 (block-array coords), x1 < x0: empty
+    __shared__ float s_tab[33];
+    const int slot = blockIdx.x, k = blockIdx.y;
+    const int bid = P.blocks[slot];
+    const int by = bid / P.nbx, bx = bid - by * P.nbx;
+    const int ox = bx * 32, oy = by * 32;
+    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+    const int cols = 32 + 2 * P.border;
+    const float r = P.radius;
+    if (threadIdx.x < 33) s_tab[threadIdx.x] = P.table[threadIdx.x];
+    const size_t rbase = (size_t)k * P.n_list;
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        const int lx = i >> 5, ly = i & 31;  // sample index i = lx*32 + ly: x-major order
+        int box = 0xff;                      // x0 = 255 > x1 = 0: empty
+        float vx = 0.f, vy = 0.f, vz = 0.f, px = 0.f, py = 0.f;
+        if (lx < sxb && ly < syb) {
+            const int li = P.pixel_map[(oy + ly) * P.width + (ox + lx)];
+            if (li >= 0) {
+                const float4 rec = P.rec_rgbx[rbase + li];
+                if (is_valid(f3(rec.x, rec.y, rec.z))) {  // invalid samples drop with their weight
+                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li];
+                    px = spx - 0.5f - (float)(ox - P.border);
+                    py = spy - 0.5f - (float)(oy - P.border);
+                    int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
+                    int x1 = min((int)floorf(px + r), cols - 1), y1 = min((int)floorf(py + r), cols - 1);
+                    box = x0 | (x1 << 8) | (y0 << 16) | (y1 << 24);
+                    vx = rec.x; vy = rec.y; vz = rec.z;
+                }
+            }
+        }
+        const int j = lx * 33 + ly;
+        s_val[0][j] = vx; s_val[1][j] = vy; s_val[2][j] = vz;
+        s_pos[0][j] = px; s_pos[1][j] = py;
+        s_box[j] = box;
+    }
+    __syncthreads();
+    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+    const int R = P.reach, bd = P.border;
+    for (int q = threadIdx.x; q < cols * cols; q += 256) {
+        const int yt = q / cols, xt = q - yt * cols;
+        float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
+        const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
+        const int ly0 = max(yt - bd - R, 0), ly1 = min(yt - bd + R, syb - 1);
+        for (int lx = lx0; lx <= lx1; ++lx)
+            for (int ly = ly0; ly <= ly1; ++ly) {
+                const int i = lx * 33 + ly;
+                const int box = s_box[i];
+                const int x0 = box & 0xff, x1 = (box >> 8) & 0xff, y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
+                if (xt < x0 || xt > x1 || yt < y0 || yt > y1) continue;
+                const float wx = s_tab[(int)(fabsf((float)xt - s_pos[0][i]) * P.lookup)];
+                const float wy = s_tab[(int)(fabsf((float)yt - s_pos[1][i]) * P.lookup)];
+                ar += s_val[0][i] * wx * wy;
+                ag += s_val[1][i] * wx * wy;
+                ab += s_val[2][i] * wx * wy;
+                aw += 1.0f * wx * wy;
+            }
+        out[q] = make_float4(ar, ag, ab, aw);
+    }
+}
+
+// ImageBlock::put(ImageBlock&) into the master (src/utils/block.cpp:125-134): per master
+// pixel, per round, the overlapping rendered blocks in BlockGenerator spiral order.
+__global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     const int mx = blockIdx.x * 16 + (threadIdx.x & 15), my = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (mx >= mcols || my >= mrows) return;
-    const int qx = mx - P.border, qy = my - P.border;
-    const int R = P.reach;
-    const int xa = max(qx - R, 0), xb = min(qx + R, P.width - 1);
-    const int ya = max(qy - R, 0), yb = min(qy + R, P.height - 1);
-    if (xa > xb || ya > yb) return;
-    // candidate blocks (at most 2x2), sorted by spiral rank
-    int blk[4], nb = 0;
-    for (int by = ya >> 5; by <= (yb >> 5); ++by)
-        for (int bx = xa >> 5; bx <= (xb >> 5); ++bx) blk[nb++] = by * P.nbx + bx;
-    for (int a = 1; a < nb; ++a)
-        for (int b = a; b > 0 && P.block_rank[blk[b]] < P.block_rank[blk[b - 1]]; --b) {
-            int tmp = blk[b]; blk[b] = blk[b - 1]; blk[b - 1] = tmp;
-        }
-    float4 *mp = reinterpret_cast<float4 *>(P.fb) + (size_t)my * mcols + mx;
-    float4 m = *mp;
     const int cols = 32 + 2 * P.border;
-    const float r = P.radius;
-    for (int k = 0; k < P.n_rounds; ++k) {
-        const size_t rbase = (size_t)k * P.n_list;
-        for (int q = 0; q < nb; ++q) {
-            const int bid = blk[q], by = bid / P.nbx, bx = bid - by * P.nbx;
+    // blocks whose merged region (sx+2b)x(sy+2b) at offset (ox, oy) covers (mx, my)
+    int blk[4], slot[4], nb = 0;
+    const int bx_lo = max((mx - cols + 1 + 31) >> 5, 0), bx_hi = min(mx >> 5, P.nbx - 1);
+    const int nby = (P.height + 31) >> 5;
+    const int by_lo = max((my - cols + 1 + 31) >> 5, 0), by_hi = min(my >> 5, nby - 1);
+    for (int by = by_lo; by <= by_hi; ++by)
+        for (int bx = bx_lo; bx <= bx_hi; ++bx) {
+            const int bid = by * P.nbx + bx;
+            const int sl = P.block_slot[bid];
+            if (sl < 0) continue;
             const int ox = bx * 32, oy = by * 32;
             const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-            const int xt = mx - ox, yt = my - oy;  // block-array coordinates of this master pixel
-            if (xt < 0 || yt < 0 || xt >= sxb + 2 * P.border || yt >= syb + 2 * P.border) continue;
-            float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
-            bool any = false;
-            const int x0 = max(xa, ox), x1 = min(xb, ox + 31), y0 = max(ya, oy), y1 = min(yb, oy + 31);
-            for (int px = x0; px <= x1; ++px)
-                for (int py = y0; py <= y1; ++py) {
-                    const int li = P.pixel_map[py * P.width + px];
-                    if (li < 0) continue;
-                    const float4 rec = P.rec_rgbx[rbase + li];
-                    const F3 v = f3(rec.x, rec.y, rec.z);
-                    if (!is_valid(v)) continue;  // dropped with its filter weight
-                    const float jy = P.rec_jy[rbase + li];
-                    const float spx = (float)px + rec.w, spy = (float)py + jy;
-                    const float posx = spx - 0.5f - (float)(ox - P.border);
-                    const float posy = spy - 0.5f - (float)(oy - P.border);
-                    int bx0 = (int)ceilf(posx - r), by0 = (int)ceilf(posy - r);
-                    int bx1 = (int)floorf(posx + r), by1 = (int)floorf(posy + r);
-                    bx0 = max(bx0, 0); by0 = max(by0, 0);
-                    bx1 = min(bx1, cols - 1); by1 = min(by1, cols - 1);
-                    if (xt < bx0 || xt > bx1 || yt < by0 || yt > by1) continue;
-                    const float wx = P.table[(int)(fabsf((float)xt - posx) * P.lookup)];
-                    const float wy = P.table[(int)(fabsf((float)yt - posy) * P.lookup)];
-                    ar += v.x * wx * wy;
-                    ag += v.y * wx * wy;
-                    ab += v.z * wx * wy;
-                    aw += 1.0f * wx * wy;
-                    any = true;
-                }
-            if (any) {
-                m.x += ar;
-                m.y += ag;
-                m.z += ab;
-                m.w += aw;
-            }
+            if (mx - ox >= sxb + 2 * P.border || my - oy >= syb + 2 * P.border) continue;
+            blk[nb] = bid;
+            slot[nb] = sl;
+            ++nb;
+        }
+    if (nb == 0) return;
+    for (int a = 1; a < nb; ++a)
+        for (int b = a; b > 0 && P.block_rank[blk[b]] < P.block_rank[blk[b - 1]]; --b) {
+            int t = blk[b]; blk[b] = blk[b - 1]; blk[b - 1] = t;
+            t = slot[b]; slot[b] = slot[b - 1]; slot[b - 1] = t;
+        }
+    int off[4];
+    for (int q = 0; q < nb; ++q) {
+        const int by = blk[q] / P.nbx, bx = blk[q] - by * P.nbx;
+        off[q] = (my - by * 32) * cols + (mx - bx * 32);
+    }
+    float4 *mp = reinterpret_cast<float4 *>(P.fb) + (size_t)my * mcols + mx;
+    float4 m = *mp;
+    const size_t per_round = (size_t)P.n_blocks * (size_t)(cols * cols);
+    for (int k = 0; k < P.n_rounds; ++k) {
+        const float4 *base = P.staging + (size_t)k * per_round;
+        for (int q = 0; q < nb; ++q) {
+            const float4 v = base[(size_t)slot[q] * (cols * cols) + off[q]];
+            m.x += v.x;
+            m.y += v.y;
+            m.z += v.z;
+            m.w += v.w;
         }
     }
     *mp = m;
@@ -466,7 +540,7 @@ __global__ __launch_bounds__(256) void nh_count_invalid_kernel(const float4 *rec
 namespace nh {
 
 template <int BLOCK, int DEPTH>
-static void launch_trace_d(const DScene &S, const Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n,
+static void launch_trace_d(const DScene *S, const Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n,
                            bool any, bool ordered, bool stats, unsigned long long *ctr, hipStream_t st) {
     dim3 grid((n + BLOCK - 1) / BLOCK);
 #define NH_TK(O, A, T) hipLaunchKernelGGL((nh_trace_kernel<BLOCK, DEPTH, O, A, T>), grid, dim3(BLOCK), 0, st, S, tv, rb, hb, n, ctr)
@@ -480,7 +554,7 @@ static void launch_trace_d(const DScene &S, const Traversal &tv, const RayBatch 
 #undef NH_TK
 }
 
-void launch_trace(const DScene &S, const Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n, bool any,
+void launch_trace(const DScene *S, const Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n, bool any,
                   bool ordered, bool stats, int depth, unsigned long long *ctr, hipStream_t st) {
     if (n <= 0) return;
     if (depth <= 16) launch_trace_d<128, 16>(S, tv, rb, hb, n, any, ordered, stats, ctr, st);
@@ -489,17 +563,38 @@ void launch_trace(const DScene &S, const Traversal &tv, const RayBatch &rb, cons
     else launch_trace_d<64, 128>(S, tv, rb, hb, n, any, ordered, stats, ctr, st);
 }
 
-template <int BLOCK, int DEPTH>
-static void launch_path_d(const DScene &S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
+template <int BLOCK, int DEPTH, int MINW>
+static void launch_path_w(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
                           hipStream_t st) {
     dim3 grid((L.n_paths + BLOCK - 1) / BLOCK);
-#define NH_PK(O, T) hipLaunchKernelGGL((nh_path_kernel<BLOCK, DEPTH, O, T>), grid, dim3(BLOCK), 0, st, S, tv, L)
+#define NH_PK(O, T) hipLaunchKernelGGL((nh_path_kernel<BLOCK, DEPTH, O, T, MINW>), grid, dim3(BLOCK), 0, st, S, tv, L)
     if (ordered) { if (stats) NH_PK(true, true); else NH_PK(true, false); }
     else { if (stats) NH_PK(false, true); else NH_PK(false, false); }
 #undef NH_PK
 }
 
-void launch_path(const DScene &S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats, int depth,
+// occupancy target of the megakernel (waves per SIMD the register allocator must allow)
+static int path_min_waves() {
+    static int w = [] {
+        const char *e = std::getenv("NH_PATH_WAVES");
+        int v = e ? std::atoi(e) : NH_DEFAULT_PATH_WAVES;
+        return (v >= 1 && v <= 4) ? v : NH_DEFAULT_PATH_WAVES;
+    }();
+    return w;
+}
+
+template <int BLOCK, int DEPTH>
+static void launch_path_d(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
+                          hipStream_t st) {
+    switch (path_min_waves()) {
+        case 1: launch_path_w<BLOCK, DEPTH, 1>(S, tv, L, ordered, stats, st); break;
+        case 2: launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, st); break;
+        case 3: launch_path_w<BLOCK, DEPTH, 3>(S, tv, L, ordered, stats, st); break;
+        default: launch_path_w<BLOCK, DEPTH, 4>(S, tv, L, ordered, stats, st); break;
+    }
+}
+
+void launch_path(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats, int depth,
                  hipStream_t st) {
     if (L.n_paths <= 0) return;
     if (depth <= 16) launch_path_d<128, 16>(S, tv, L, ordered, stats, st);
@@ -509,9 +604,10 @@ void launch_path(const DScene &S, const Traversal &tv, const PathLaunch &L, bool
 }
 
 void launch_splat(const SplatLaunch &P, hipStream_t st) {
+    hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     dim3 grid((mcols + 15) / 16, (mrows + 15) / 16);
-    hipLaunchKernelGGL(nh_splat_kernel, grid, dim3(256), 0, st, P);
+    hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, P);
 }
 
 void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st) {

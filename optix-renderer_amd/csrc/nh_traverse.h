@@ -209,4 +209,102 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
     return ANY ? false : found;
 }
 
+
+// Same traversal with the any-hit flag decided per lane at run time, so a caller that
+// alternates closest and any-hit queries inlines a single traversal loop.
+template <bool STATS>
+NHD bool leaf_test_rt(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float &maxt, Hit &best, bool &found,
+                      bool any, TravStats &st) {
+    const int2 lf = tv.leaves[leaf];
+    for (int k = lf.x, e = lf.x + lf.y; k < e; ++k) {
+        const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
+        if (STATS) st.prims++;
+        float t, u = 0.f, v = 0.f;
+        bool hit = (__float_as_int(c.w) == 0) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
+                                              : sphere_test(a, o, d, mint, maxt, t);
+        if (!hit) continue;
+        if (t < maxt || k > best.k) {
+            found = true;
+            maxt = t;
+            best.t = t;
+            best.u = u;
+            best.v = v;
+            best.k = k;
+        }
+        if (any) return true;
+    }
+    return false;
+}
+
+template <int DEPTH, bool ORDERED, bool STATS>
+NHD bool trace_rt(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, float maxt, bool any, Hit &best,
+                  uint2 *stk, int stride, TravStats &st) {
+    if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));
+    best.k = -1;
+    best.t = INFINITY;
+    if (S.root_kind == 0 || maxt < mint) return false;
+    const F3 r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    bool found = false;
+    float near_t;
+    if (STATS) st.boxes++;
+    if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d, r,
+                  mint, maxt, near_t))
+        return false;
+    if (S.root_kind == 2) {
+        leaf_test_rt<STATS>(tv, 0, o, d, mint, maxt, best, found, any, st);
+        return found;
+    }
+    int sp = 0;
+    int cur = 0;
+    for (;;) {
+        while (cur >= 0) {
+            const float4 n0 = tv.nodes[4 * cur], n1 = tv.nodes[4 * cur + 1], n2 = tv.nodes[4 * cur + 2];
+            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * cur + 3]);
+            if (STATS) { st.nodes++; st.boxes += 2; }
+            float nl, nr;
+            const bool hl = box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, nl);
+            const bool hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
+            int next;
+            if (hl && hr) {
+                int first = n3.x, second = n3.y;
+                float second_near = nr;
+                if (ORDERED && nr < nl) {
+                    first = n3.y;
+                    second = n3.x;
+                    second_near = nl;
+                }
+                stk[sp * stride] = make_uint2((uint32_t)second, __float_as_uint(second_near));
+                ++sp;
+                next = first;
+            } else if (hl) {
+                next = n3.x;
+            } else if (hr) {
+                next = n3.y;
+            } else {
+                break;
+            }
+            if (next >= 0) {
+                cur = next;
+                continue;
+            }
+            if (leaf_test_rt<STATS>(tv, ~next, o, d, mint, maxt, best, found, any, st)) return true;
+            break;
+        }
+        cur = -1;
+        while (sp > 0) {
+            --sp;
+            const uint2 e = stk[sp * stride];
+            if (!(__uint_as_float(e.y) <= maxt)) continue;
+            const int ref = (int)e.x;
+            if (ref >= 0) {
+                cur = ref;
+                break;
+            }
+            if (leaf_test_rt<STATS>(tv, ~ref, o, d, mint, maxt, best, found, any, st)) return true;
+        }
+        if (cur < 0) break;
+    }
+    return found;
+}
+
 }  // namespace nhd
