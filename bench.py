@@ -123,8 +123,7 @@ def main():
     t0 = time.perf_counter()
     ctx.upload(scene, bvh)
     upload_s = time.perf_counter() - t0
-    nbx, nby = (W + 31) // 32, (H + 31) // 32
-    blocks = [b for b in range(nbx * nby) if b % world == rank] if world > 1 else None
+    blocks = nh.tile_shard(W, H, world, rank) if world > 1 else None
     trav = nh.TRAVERSAL_ORDERED if args.traversal == "ordered" else nh.TRAVERSAL_REFERENCE
     R = args.rounds
 

@@ -340,6 +340,13 @@ class Context:
         return res
 
 
+def tile_shard(width: int, height: int, world: int, rank: int) -> list:
+    """32x32 image blocks (block id = by*nbx + bx, BlockGenerator numbering) dealt
+    round-robin to ranks: the multi-GPU partition of the image."""
+    nbx, nby = (width + 31) // 32, (height + 31) // 32
+    return [b for b in range(nbx * nby) if b % world == rank]
+
+
 def reduce_framebuffers(ctxs, root: int = 0):
     arr = (_vp * len(ctxs))(*[c._h for c in ctxs])
     rc = _lib.nh_reduce_framebuffers(arr, len(ctxs), root)

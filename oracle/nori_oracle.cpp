@@ -23,6 +23,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <memory>
 #include <thread>
@@ -192,11 +193,23 @@ float fresnel(float cos_i, float ext_ior, float int_ior) {
 // ---------------------------------------------------------------------------
 // warps (src/utils/warp.cpp)
 // ---------------------------------------------------------------------------
+// NO_UNQUALIFIED_DOUBLE=1: unqualified sqrt/cos/sin/log on float arguments in warp.cpp /
+// sphere.cpp resolve to the C double functions (a build whose ImathPlatform.h does not pull
+// the C++ <math.h> overloads into the global namespace); default 0: float overloads (IlmBase's
+// ImathPlatform.h includes <math.h>). Only the rounding points differ.
+#ifndef NO_UNQUALIFIED_DOUBLE
+#define NO_UNQUALIFIED_DOUBLE 0
+#endif
 void square_to_uniform_disk(float sx, float sy, float &x, float &y) {  // warp.cpp:48-52
     float rho = f_sqrt(sx);
     float theta = sy * 2.0f * kPi;
+#if NO_UNQUALIFIED_DOUBLE
+    x = (float)((double)rho * std::cos((double)theta));
+    y = (float)((double)rho * std::sin((double)theta));
+#else
     x = rho * f_cos(theta);
     y = rho * f_sin(theta);
+#endif
 }
 V3 square_to_cosine_hemisphere(float sx, float sy) {  // warp.cpp:111-122
     float x, y;
@@ -208,7 +221,11 @@ V3 square_to_beckmann(float sx, float sy, float alpha) {  // warp.cpp:131-150
     if (std::isinf(log_sample)) log_sample = 0;
     float tan2 = -alpha * alpha * log_sample;
     float phi = sy * 2.f * kPi;
+#if NO_UNQUALIFIED_DOUBLE
+    float cos_t = (float)(1.f / std::sqrt((double)(1 + tan2)));
+#else
     float cos_t = 1.f / f_sqrt(1 + tan2);
+#endif
     float sin_t = f_sqrt(1.f - cos_t * cos_t);
     V3 res = mk(sin_t * f_cos(phi), sin_t * f_sin(phi), cos_t);
     if (res.z < 0) res = -res;
@@ -224,8 +241,13 @@ V3 square_to_uniform_sphere(float sx, float sy) {  // warp.cpp:74-82
     w.z = 2.0f * sx - 1.0f;
     float r = f_sqrt(1.0f - w.z * w.z);
     float sigma = 2.0f * kPi * sy;
+#if NO_UNQUALIFIED_DOUBLE
+    w.x = (float)((double)r * std::cos((double)sigma));
+    w.y = (float)((double)r * std::sin((double)sigma));
+#else
     w.x = r * f_cos(sigma);
     w.y = r * f_sin(sigma);
+#endif
     return normalized(w);
 }
 
@@ -431,8 +453,13 @@ bool sphere_intersect(const nh_shape &sh, const Ray &ray, float &t) {  // sphere
     float cc = dot(L, L) - sh.radius * sh.radius;
     float discr = b * b - 4.f * a * cc;
     if (discr < 0.f) return false;
+#if NO_UNQUALIFIED_DOUBLE
+    const float tmin = (float)(((double)(-b) - std::sqrt((double)discr)) / 2 / (double)a);
+    const float tmax = (float)(((double)(-b) + std::sqrt((double)discr)) / 2 / (double)a);
+#else
     const float tmin = (-b - f_sqrt(discr)) / 2 / a;
     const float tmax = (-b + f_sqrt(discr)) / 2 / a;
+#endif
     if (ray.mint <= tmin && ray.maxt >= tmin) { t = tmin; return true; }
     if (ray.mint <= tmax && ray.maxt >= tmax) { t = tmax; return true; }
     return false;
@@ -1256,6 +1283,42 @@ int no_bsdf_sample(const nh_bsdf *b, const float *wi, const float *sample, float
     weight3[0] = w.x; weight3[1] = w.y; weight3[2] = w.z;
     *pdf = bsdf_pdf(*b, r);
     *measure = (int32_t)r.measure;
+    return NH_OK;
+}
+
+// ChiSquareTest::execute sampling loop (src/utils/chi2test.cpp:150-170): histogram of
+// sample() directions over cos(theta) x phi cells; rng state in/out.
+int no_chi2_histogram(const nh_bsdf *b, const float *wi, uint64_t *state, uint64_t *inc, int32_t n, int32_t res_theta,
+                      int32_t res_phi, double *obs) {
+    Pcg32 rng;
+    rng.state = *state;
+    rng.inc = *inc;
+    BRec r;
+    r.wi = mk(wi[0], wi[1], wi[2]);
+    for (int32_t i = 0; i < n; ++i) {
+        float a = rng.next_float();
+        float c = rng.next_float();
+        V3 res = bsdf_sample(*b, r, a, c);
+        if (res.x == 0 && res.y == 0 && res.z == 0) continue;
+        int ct = std::min(std::max(0, (int)std::floor((r.wo.z * 0.5f + 0.5f) * res_theta)), res_theta - 1);
+        float scaled_phi = f_atan2(r.wo.y, r.wo.x) * 0.15915494309189533577f;
+        if (scaled_phi < 0) scaled_phi += 1;
+        int pb = std::min(std::max(0, (int)std::floor(scaled_phi * res_phi)), res_phi - 1);
+        obs[ct * res_phi + pb] += 1;
+    }
+    *state = rng.state;
+    *inc = rng.inc;
+    return NH_OK;
+}
+
+int no_bsdf_pdf_batch(const nh_bsdf *b, const float *wi, int32_t n, const float *wo, float *out) {
+    for (int32_t i = 0; i < n; ++i) {
+        BRec r;
+        r.wi = mk(wi[0], wi[1], wi[2]);
+        r.wo = mk(wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]);
+        r.measure = ESolidAngle;
+        out[i] = bsdf_pdf(*b, r);
+    }
     return NH_OK;
 }
 

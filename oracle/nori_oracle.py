@@ -48,6 +48,8 @@ _sig("no_ttest_bsdf", _i32, C.POINTER(nh.nh_bsdf), C.c_float, _u64p, _u64p, _i32
      C.POINTER(C.c_double))
 _sig("no_bsdf_sample", _i32, C.POINTER(nh.nh_bsdf), _fp, _fp, _fp, _fp, _fp, C.POINTER(_i32))
 _sig("no_bsdf_pdf", C.c_float, C.POINTER(nh.nh_bsdf), _fp, _fp)
+_sig("no_bsdf_pdf_batch", _i32, C.POINTER(nh.nh_bsdf), _fp, _i32, _fp, _fp)
+_sig("no_chi2_histogram", _i32, C.POINTER(nh.nh_bsdf), _fp, _u64p, _u64p, _i32, _i32, _i32, C.POINTER(C.c_double))
 
 
 class Pcg32:
@@ -159,3 +161,20 @@ def bsdf_pdf(bsdf, wi, wo):
     wi = np.asarray(wi, np.float32)
     wo = np.asarray(wo, np.float32)
     return _lib.no_bsdf_pdf(C.byref(bsdf), wi.ctypes.data_as(_fp), wo.ctypes.data_as(_fp))
+
+
+def bsdf_pdf_batch(bsdf, wi, wo):
+    wi = np.ascontiguousarray(wi, np.float32)
+    wo = np.ascontiguousarray(wo, np.float32).reshape(-1, 3)
+    out = np.zeros(len(wo), np.float32)
+    _lib.no_bsdf_pdf_batch(C.byref(bsdf), wi.ctypes.data_as(_fp), len(wo), wo.ctypes.data_as(_fp),
+                           out.ctypes.data_as(_fp))
+    return out
+
+
+def chi2_histogram(bsdf, wi, rng: Pcg32, n, res_theta, res_phi):
+    wi = np.ascontiguousarray(wi, np.float32)
+    obs = np.zeros(res_theta * res_phi, np.float64)
+    _lib.no_chi2_histogram(C.byref(bsdf), wi.ctypes.data_as(_fp), C.byref(rng.state), C.byref(rng.inc), n, res_theta,
+                           res_phi, obs.ctypes.data_as(C.POINTER(C.c_double)))
+    return obs

@@ -1,0 +1,194 @@
+"""The oracle against the reference's own known answers (CPU only).
+
+  - pcg32: ext/pcg32/pcg32-demo.out (5 rounds of u32 / coins / rolls / card shuffles) -- bit-exact;
+  - path integrators: scenes/pa4/tests/test-furnace.xml and test-direct.xml, run with the
+    reference's StudentsTTest scene procedure (src/utils/ttest.cpp:191-240: one default-seeded
+    Independent sampler drawn sequentially across the file's scenes, 100k paths each, Welford
+    mean/variance, Student-t test with Sidak correction at alpha = 0.01);
+  - microfacet BSDF: scenes/pa3/tests/ttest-microfacet.xml (ttest.cpp:147-190) and
+    chi2test-microfacet.xml (src/utils/chi2test.cpp:121-230: 10x20 cos(theta)/phi table,
+    5000 samples per cell, pooled cells below 5 expected, Sidak-corrected chi^2 test).
+"""
+import json
+import math
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+import pytest
+from scipy import stats
+
+import nori_hip as nh
+import nori_oracle as no
+import scenegen
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+# ---------------------------------------------------------------------------------------
+def pcg_bounded(r, bound):
+    """pcg32::nextUInt(bound) (ext/pcg32/pcg32.h:69-98)."""
+    threshold = ((1 << 32) - bound) % bound
+    while True:
+        x = r.next_uint()
+        if x >= threshold:
+            return x % bound
+
+
+def test_pcg32_demo_known_answers():
+    kat = json.load(open(os.path.join(GOLDEN, "pcg32_kat.json")))
+    r = no.Pcg32.seeded(*kat["seed"])
+    number, suit = "A23456789TJQK", "hcds"
+    for rnd in kat["rounds"]:
+        assert [r.next_uint() for _ in range(6)] == rnd["u32"]
+        assert "".join("H" if pcg_bounded(r, 2) else "T" for _ in range(65)) == rnd["coins"]
+        assert [pcg_bounded(r, 6) + 1 for _ in range(33)] == rnd["rolls"]
+        cards = list(range(52))
+        for i in range(51, 0, -1):  # pcg32::shuffle (Knuth)
+            j = pcg_bounded(r, i + 1)
+            cards[i], cards[j] = cards[j], cards[i]
+        assert [number[c // 4] + suit[c % 4] for c in cards] == rnd["cards"]
+
+
+def splitmix64(x):
+    m = (1 << 64) - 1
+    z = (x + 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def pcg_seed_py(initstate, initseq):
+    m = (1 << 64) - 1
+    mult = 0x5851F42D4C957F2D
+    inc = ((initseq << 1) | 1) & m
+    state = 0
+    state = (state * mult + inc) & m
+    state = (state + initstate) & m
+    state = (state * mult + inc) & m
+    return state, inc
+
+
+@pytest.mark.parametrize("seed,pixel,sample", [(0, 0, 0), (1234, 1023 * 1024 + 5, 255), (2**63 + 7, 12345, 99999)])
+def test_per_path_seeding_contract(seed, pixel, sample):
+    """pcg32.seed(splitmix64(seed ^ pixel), sample) -- the contract the GPU uses."""
+    r = no.Pcg32.per_path(seed, pixel, sample)
+    st, inc = pcg_seed_py(splitmix64(seed ^ pixel), sample)
+    assert (r.state.value, r.inc.value) == (st, inc)
+
+
+# ---------------------------------------------------------------------------------------
+def students_t_test(mean, variance, reference, n, alpha, num_tests):
+    """hypothesis::students_t_test (ext/hypothesis/hypothesis.h:314-346)."""
+    t = abs(mean - reference) * math.sqrt(n / max(variance, 1e-5))
+    pval = 2 * (1 - stats.t.cdf(t, n - 1))
+    sidak = 1.0 - (1.0 - alpha) ** (1.0 / num_tests)
+    return not (pval < sidak or not math.isfinite(pval)), pval
+
+
+@pytest.mark.parametrize("name", ["test-furnace.xml", "test-direct.xml"])
+def test_scene_ttests(scene_dir, name):
+    path = os.path.join(scene_dir, "scenes/pa4/tests", name)
+    refs = scenegen.test_references(path)
+    rng = no.Pcg32()  # Independent sampler created once, never prepare()d (ttest.cpp:193-194)
+    results = []
+    for i, ref in enumerate(refs):
+        s = nh.Scene(path, i)
+        mean, var = no.OracleScene(s).ttest(rng, 100000)
+        ok, p = students_t_test(mean, var, ref, 100000, 0.01, len(refs))
+        results.append((i, mean, ref, p, ok))
+    assert all(r[-1] for r in results), results
+
+
+def microfacet_from_xml(node):
+    b = nh.nh_bsdf()
+    b.type = nh.BSDF_MICROFACET
+    vals = {f.get("name"): f.get("value") for f in node}
+    b.alpha = float(vals.get("alpha", 0.1))
+    b.int_ior = float(vals.get("intIOR", 1.5046))
+    b.ext_ior = float(vals.get("extIOR", 1.000277))
+    kd = np.array([float(x) for x in vals.get("kd", "0.5 0.5 0.5").replace(",", " ").split()], np.float32)
+    for i in range(3):
+        b.kd[i] = kd[i]
+    m = kd[1] if not (kd[1] < kd[2]) else kd[2]
+    m = kd[0] if not (kd[0] < m) else m
+    b.ks = float(np.float32(1) - m)
+    return b
+
+
+def test_microfacet_ttest(scene_dir):
+    root = ET.parse(os.path.join(scene_dir, "scenes/pa3/tests/ttest-microfacet.xml")).getroot()
+    strings = {s.get("name"): s.get("value") for s in root.findall("string")}
+    angles = [float(x) for x in strings["angles"].replace(",", " ").split()]
+    refs = [float(x) for x in strings["references"].replace(",", " ").split()]
+    rng = no.Pcg32()
+    for bnode in root.findall("bsdf"):
+        b = microfacet_from_xml(bnode)
+        for angle, ref in zip(angles, refs):
+            mean, var = no.ttest_bsdf(b, angle, rng, 100000)
+            ok, p = students_t_test(mean, var, ref, 100000, 0.01, len(refs))
+            assert ok, (angle, mean, ref, p)
+
+
+def chi2_test(obs, exp, n, min_exp, alpha, num_tests):
+    """hypothesis::chi2_test: pool low-expectation cells, Pearson statistic, Sidak correction."""
+    order = np.argsort(exp, kind="stable")
+    pooled_o = pooled_e = 0.0
+    chsq, dof = 0.0, 0
+    for i in order:
+        if exp[i] == 0:
+            if obs[i] > n * 1e-5:
+                return False
+        elif exp[i] < min_exp:
+            pooled_o += obs[i]
+            pooled_e += exp[i]
+        elif pooled_e > 0 and pooled_e < min_exp:
+            pooled_o += obs[i]
+            pooled_e += exp[i]
+        else:
+            chsq += (obs[i] - exp[i]) ** 2 / exp[i]
+            dof += 1
+    if pooled_e > 0 or pooled_o > 0:
+        chsq += (pooled_o - pooled_e) ** 2 / max(pooled_e, 1e-300)
+        dof += 1
+    dof -= 1
+    pval = 1 - stats.chi2.cdf(chsq, dof)
+    sidak = 1.0 - (1.0 - alpha) ** (1.0 / num_tests)
+    return not (pval < sidak or not math.isfinite(pval))
+
+
+def expected_frequencies(b, wi, res_t, res_p, n, quad=48):
+    """Integral of pdf(wi, .) over each cos(theta) x phi cell (Gauss-Legendre per cell)."""
+    x, w = np.polynomial.legendre.leggauss(quad)
+    exp = np.zeros(res_t * res_p)
+    for i in range(res_t):
+        c0, c1 = -1.0 + i * 2.0 / res_t, -1.0 + (i + 1) * 2.0 / res_t
+        ct = 0.5 * (c1 - c0) * x + 0.5 * (c1 + c0)
+        for j in range(res_p):
+            p0, p1 = j * 2 * math.pi / res_p, (j + 1) * 2 * math.pi / res_p
+            ph = 0.5 * (p1 - p0) * x + 0.5 * (p1 + p0)
+            CT, PH = np.meshgrid(ct, ph, indexing="ij")
+            st = np.sqrt(1 - CT * CT)
+            wo = np.stack([st * np.cos(PH), st * np.sin(PH), CT], -1).astype(np.float32)
+            pdf = no.bsdf_pdf_batch(b, wi, wo.reshape(-1, 3)).reshape(CT.shape).astype(np.float64)
+            exp[i * res_p + j] = (np.outer(w, w) * pdf).sum() * 0.25 * (c1 - c0) * (p1 - p0) * n
+    return exp
+
+
+def test_microfacet_chi2(scene_dir):
+    root = ET.parse(os.path.join(scene_dir, "scenes/pa3/tests/chi2test-microfacet.xml")).getroot()
+    res_t, res_p, tests_per_bsdf = 10, 20, 5
+    n = res_t * res_p * 5000
+    bsdfs = [microfacet_from_xml(b) for b in root.findall("bsdf")]
+    rng = no.Pcg32()
+    passed = 0
+    for b in bsdfs:
+        for _ in range(tests_per_bsdf):
+            cos_t = rng.next_float()
+            sin_t = math.sqrt(max(0.0, 1 - cos_t * cos_t))
+            phi = np.float32(2.0 * np.float32(math.pi)) * np.float32(rng.next_float())
+            wi = np.array([math.cos(phi) * sin_t, math.sin(phi) * sin_t, cos_t], np.float32)
+            obs = no.chi2_histogram(b, wi, rng, n, res_t, res_p)
+            exp = expected_frequencies(b, wi, res_t, res_p, n)
+            passed += chi2_test(obs, exp, n, 5, 0.01, tests_per_bsdf * len(bsdfs))
+    assert passed == tests_per_bsdf * len(bsdfs), passed
