@@ -186,7 +186,7 @@ __device__ __forceinline__ void camera_ray(const DScene &S, float px, float py, 
 
 template <int DEPTH, bool ORDERED, bool STATS>
 __device__ __forceinline__ bool closest(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, float maxt,
-                                        Hit &h, uint2 *stk, int stride, TravStats &st) {
+                                        Hit &h, uint32_t *stk, int stride, TravStats &st) {
     return trace<DEPTH, ORDERED, false, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st);
 }
 
@@ -199,7 +199,7 @@ __device__ __forceinline__ bool closest(const Traversal &tv, const DScene &S, F3
 // keeps the state that is live across traversals small.
 template <int DEPTH, bool ORDERED, bool STATS>
 __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, F3 d, float mint, float maxt,
-                          uint2 *stk, int stride, TravStats &st, uint32_t &queries) {
+                          uint32_t *stk, int stride, TravStats &st, uint32_t &queries) {
     F3 li = f3(0, 0, 0), t = f3(1, 1, 1);
     float w_mats = 1.f, w_ems = 0.f;
     const float n_lights = (float)S.n_emitters;
@@ -295,7 +295,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
 // PathMatsIntegrator::Li (src/integrators/path_mats.cpp:16-78)
 template <int DEPTH, bool ORDERED, bool STATS>
 __device__ F3 li_path_mats(const DScene &S, const Traversal &tv, Rng &rng, F3 o, F3 d, float mint, float maxt,
-                           uint2 *stk, int stride, TravStats &st, uint32_t &queries) {
+                           uint32_t *stk, int stride, TravStats &st, uint32_t &queries) {
     F3 li = f3(0, 0, 0), t = f3(1, 1, 1);
     int counter = 0;
     Hit h;
@@ -350,7 +350,7 @@ __device__ __forceinline__ void flush_stats(const TravStats &st, uint32_t querie
 template <int BLOCK, int DEPTH, bool ORDERED, bool ANY, bool STATS>
 __global__ __launch_bounds__(BLOCK) void nh_trace_kernel(const DScene *__restrict__ Sp, Traversal tv, RayBatch rb,
                                                          HitBatch hb, int n, unsigned long long *counters) {
-    __shared__ uint2 stk[DEPTH * BLOCK];
+    __shared__ uint32_t stk[DEPTH * BLOCK];
     const DScene &S = *Sp;
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     TravStats st{0, 0, 0};
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(BLOCK) void nh_trace_kernel(const DScene *__restric
 
 template <int BLOCK, int DEPTH, bool ORDERED, bool STATS, int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__restrict__ Sp, Traversal tv, PathLaunch L) {
-    __shared__ uint2 stk[DEPTH * BLOCK];
+    __shared__ uint32_t stk[DEPTH * BLOCK];
     const DScene &S = *Sp;
     const int gid = blockIdx.x * BLOCK + threadIdx.x;
     TravStats st{0, 0, 0};
@@ -586,12 +586,10 @@ static int path_min_waves() {
 template <int BLOCK, int DEPTH>
 static void launch_path_d(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
                           hipStream_t st) {
-    switch (path_min_waves()) {
-        case 1: launch_path_w<BLOCK, DEPTH, 1>(S, tv, L, ordered, stats, st); break;
-        case 2: launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, st); break;
-        case 3: launch_path_w<BLOCK, DEPTH, 3>(S, tv, L, ordered, stats, st); break;
-        default: launch_path_w<BLOCK, DEPTH, 4>(S, tv, L, ordered, stats, st); break;
-    }
+    // 4 waves/SIMD measured best (13.7 / 13.8 / 9.8 / 8.3 ms per 16M C2 samples at 1 / 2 / 3 / 4);
+    // the 2-wave build stays selectable (NH_PATH_WAVES=2) for register-heavy experiments
+    if (path_min_waves() == 2) launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, st);
+    else launch_path_w<BLOCK, DEPTH, 4>(S, tv, L, ordered, stats, st);
 }
 
 void launch_path(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats, int depth,

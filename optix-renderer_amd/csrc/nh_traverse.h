@@ -133,18 +133,27 @@ NHD bool leaf_test(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float 
     return false;
 }
 
+// Child box of an inner node: side 0 = left, 1 = right.
+NHD bool child_box_test(const float4 &n0, const float4 &n1, const float4 &n2, int side, F3 o, F3 d, F3 r, float mint,
+                        float maxt, float &near_t) {
+    return side == 0 ? box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, near_t)
+                     : box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, near_t);
+}
+
 // Closest / any hit. stk points at this thread's first LDS stack slot; consecutive
-// entries are `stride` uint2 apart (lane-interleaved, bank-conflict free).
+// entries are `stride` words apart (lane-interleaved, bank-conflict free). An entry is
+// (parent inner node << 1) | side: the deferred child's box is tested again when it is
+// popped, with the maxt of that moment -- the reference's visit-time test verbatim.
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS>
-NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, float maxt, Hit &best, uint2 *stk,
+NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, float maxt, Hit &best, uint32_t *stk,
                int stride, TravStats &st) {
     // adaptive ray epsilon (bvh.cpp:407-410)
     if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));
+    best.k = -1;
+    best.t = INFINITY;
     if (S.root_kind == 0 || maxt < mint) return false;
     const F3 r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     bool found = false;
-    best.k = -1;
-    best.t = INFINITY;
     float near_t;
     if (STATS) st.boxes++;
     if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d, r,
@@ -166,16 +175,10 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
             const bool hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
             int next;
             if (hl && hr) {
-                int first = n3.x, second = n3.y;
-                float second_near = nr;
-                if (ORDERED && nr < nl) {
-                    first = n3.y;
-                    second = n3.x;
-                    second_near = nl;
-                }
-                stk[sp * stride] = make_uint2((uint32_t)second, __float_as_uint(second_near));
+                const bool right_first = ORDERED && nr < nl;
+                stk[sp * stride] = ((uint32_t)cur << 1) | (right_first ? 0u : 1u);
                 ++sp;
-                next = first;
+                next = right_first ? n3.y : n3.x;
             } else if (hl) {
                 next = n3.x;
             } else if (hr) {
@@ -190,13 +193,17 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
             if (leaf_test<ANY, STATS>(tv, ~next, o, d, mint, maxt, best, found, st)) return true;
             break;
         }
-        // pop, re-checking the deferred entry distance against the current maxt
+        // pop: re-test the deferred child against the current maxt
         cur = -1;
         while (sp > 0) {
             --sp;
-            const uint2 e = stk[sp * stride];
-            if (!(__uint_as_float(e.y) <= maxt)) continue;
-            const int ref = (int)e.x;
+            const uint32_t e = stk[sp * stride];
+            const int parent = (int)(e >> 1), side = (int)(e & 1u);
+            const float4 n0 = tv.nodes[4 * parent], n1 = tv.nodes[4 * parent + 1], n2 = tv.nodes[4 * parent + 2];
+            if (STATS) st.boxes++;
+            if (!child_box_test(n0, n1, n2, side, o, d, r, mint, maxt, near_t)) continue;
+            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * parent + 3]);
+            const int ref = side ? n3.y : n3.x;
             if (ref >= 0) {
                 cur = ref;
                 break;
@@ -207,104 +214,6 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
     }
     (void)DEPTH;
     return ANY ? false : found;
-}
-
-
-// Same traversal with the any-hit flag decided per lane at run time, so a caller that
-// alternates closest and any-hit queries inlines a single traversal loop.
-template <bool STATS>
-NHD bool leaf_test_rt(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float &maxt, Hit &best, bool &found,
-                      bool any, TravStats &st) {
-    const int2 lf = tv.leaves[leaf];
-    for (int k = lf.x, e = lf.x + lf.y; k < e; ++k) {
-        const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
-        if (STATS) st.prims++;
-        float t, u = 0.f, v = 0.f;
-        bool hit = (__float_as_int(c.w) == 0) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
-                                              : sphere_test(a, o, d, mint, maxt, t);
-        if (!hit) continue;
-        if (t < maxt || k > best.k) {
-            found = true;
-            maxt = t;
-            best.t = t;
-            best.u = u;
-            best.v = v;
-            best.k = k;
-        }
-        if (any) return true;
-    }
-    return false;
-}
-
-template <int DEPTH, bool ORDERED, bool STATS>
-NHD bool trace_rt(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, float maxt, bool any, Hit &best,
-                  uint2 *stk, int stride, TravStats &st) {
-    if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));
-    best.k = -1;
-    best.t = INFINITY;
-    if (S.root_kind == 0 || maxt < mint) return false;
-    const F3 r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    bool found = false;
-    float near_t;
-    if (STATS) st.boxes++;
-    if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d, r,
-                  mint, maxt, near_t))
-        return false;
-    if (S.root_kind == 2) {
-        leaf_test_rt<STATS>(tv, 0, o, d, mint, maxt, best, found, any, st);
-        return found;
-    }
-    int sp = 0;
-    int cur = 0;
-    for (;;) {
-        while (cur >= 0) {
-            const float4 n0 = tv.nodes[4 * cur], n1 = tv.nodes[4 * cur + 1], n2 = tv.nodes[4 * cur + 2];
-            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * cur + 3]);
-            if (STATS) { st.nodes++; st.boxes += 2; }
-            float nl, nr;
-            const bool hl = box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, nl);
-            const bool hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
-            int next;
-            if (hl && hr) {
-                int first = n3.x, second = n3.y;
-                float second_near = nr;
-                if (ORDERED && nr < nl) {
-                    first = n3.y;
-                    second = n3.x;
-                    second_near = nl;
-                }
-                stk[sp * stride] = make_uint2((uint32_t)second, __float_as_uint(second_near));
-                ++sp;
-                next = first;
-            } else if (hl) {
-                next = n3.x;
-            } else if (hr) {
-                next = n3.y;
-            } else {
-                break;
-            }
-            if (next >= 0) {
-                cur = next;
-                continue;
-            }
-            if (leaf_test_rt<STATS>(tv, ~next, o, d, mint, maxt, best, found, any, st)) return true;
-            break;
-        }
-        cur = -1;
-        while (sp > 0) {
-            --sp;
-            const uint2 e = stk[sp * stride];
-            if (!(__uint_as_float(e.y) <= maxt)) continue;
-            const int ref = (int)e.x;
-            if (ref >= 0) {
-                cur = ref;
-                break;
-            }
-            if (leaf_test_rt<STATS>(tv, ~ref, o, d, mint, maxt, best, found, any, st)) return true;
-        }
-        if (cur < 0) break;
-    }
-    return found;
 }
 
 }  // namespace nhd
