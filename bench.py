@@ -33,6 +33,7 @@ sys.path.insert(0, os.path.join(REPO, "optix-renderer_amd"))
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 NODE_BYTES, PRIM_BYTES, RECORD_BYTES = 64, 48, 20
+EXTEND_IO_BYTES = 4 + 32 + 16
 
 
 def parse():
@@ -45,6 +46,7 @@ def parse():
     p.add_argument("--width", type=int, default=None)
     p.add_argument("--height", type=int, default=None)
     p.add_argument("--traversal", default="ordered", choices=["ordered", "reference"])
+    p.add_argument("--mode", default="megakernel", choices=["megakernel", "wavefront"])
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-calibrate", action="store_true")
@@ -77,6 +79,44 @@ def pmc_traffic(workload_key):
         return data.get(workload_key, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+def roofline(args, calib, st, W, H, R):
+    """Roofline of the dominant kernel. Algorithmic bytes come from the calibration launch's
+    in-kernel counters (same seeds as the first timed step), scaled per sample; the time is the
+    kernel's summed HIP-event duration over the timed region on the context's stream.
+      megakernel: nh_path_kernel -- BVH nodes x 64 B + primitive tests x 48 B (closest, probe and
+                  shadow queries) + 20 B sample record per path
+      wavefront:  wf_extend -- the closest-hit share of nodes/prims + 52 B per query (queue index
+                  4 B, ray 32 B in, hit 16 B out)"""
+    paths = calib["samples"]
+    if args.mode == "wavefront":
+        q = calib["ray_queries"] - calib["shadow_queries"]
+        nodes = calib["nodes_visited"] - calib["shadow_nodes_visited"]
+        prims = calib["prims_tested"] - calib["shadow_prims_tested"]
+        bytes_calib = nodes * NODE_BYTES + prims * PRIM_BYTES + q * EXTEND_IO_BYTES
+        launches, ms, kernel = max(st["launches_extend"], 1), st["kernel_ms_extend"], "wf_extend"
+    else:
+        q, nodes, prims = calib["ray_queries"], calib["nodes_visited"], calib["prims_tested"]
+        bytes_calib = nodes * NODE_BYTES + prims * PRIM_BYTES + paths * RECORD_BYTES
+        launches, ms, kernel = max(st["launches_path"], 1), st["kernel_ms_path"], "nh_path_kernel"
+    bytes_per_sample = bytes_calib / paths
+    avg_ms = ms / launches
+    bytes_per_launch = bytes_per_sample * st["samples"] / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    key = f"{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}"
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(key),
+            "kernel": kernel, "avg_launch_ms": round(avg_ms, 4), "launches": launches,
+            "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "bytes_per_sample": round(bytes_per_sample, 1),
+            "queries_per_sample": round(q / paths, 3),
+            "nodes_per_query": round(nodes / max(q, 1), 3),
+            "prims_per_query": round(prims / max(q, 1), 3),
+            "splat_ms_per_launch": round(st["kernel_ms_splat"] / max(st["launches_splat"], 1), 4)}
+    if args.mode == "wavefront":
+        roof["stage_ms"] = {k: round(st[f"kernel_ms_{k}"], 3) for k in ("extend", "shadow", "shade", "splat")}
+    return roof
 
 
 def cpu_baseline(scene, budget_s, seed):
@@ -125,19 +165,20 @@ def main():
     upload_s = time.perf_counter() - t0
     blocks = nh.tile_shard(W, H, world, rank) if world > 1 else None
     trav = nh.TRAVERSAL_ORDERED if args.traversal == "ordered" else nh.TRAVERSAL_REFERENCE
+    mode = nh.MODE_WAVEFRONT if args.mode == "wavefront" else nh.MODE_MEGAKERNEL
     R = args.rounds
 
     # calibration launch (in-kernel counters; same seeds as the first timed step)
     calib = None
     if not args.no_calibrate:
         ctx.reset_stats()
-        ctx.render(0, R, seed=args.seed, blocks=blocks, traversal=trav, clear=True, stats=True)
+        ctx.render(0, R, seed=args.seed, blocks=blocks, traversal=trav, clear=True, stats=True, mode=mode)
         calib = ctx.stats()
 
     # warmup (rounds past the timed range, separate framebuffer content)
     for w in range(args.warmup):
         ctx.render(R * (args.steps + w), R * (args.steps + w + 1), seed=args.seed, blocks=blocks, traversal=trav,
-                   clear=(w == 0))
+                   clear=(w == 0), mode=mode)
     ctx.synchronize()
     ctx.reset_stats()
     if dist is not None:
@@ -148,7 +189,7 @@ def main():
     ctx.synchronize()
     t_start = time.perf_counter()
     for s in range(args.steps):
-        ctx.render(s * R, (s + 1) * R, seed=args.seed, blocks=blocks, traversal=trav, clear=False)
+        ctx.render(s * R, (s + 1) * R, seed=args.seed, blocks=blocks, traversal=trav, clear=False, mode=mode)
     if dist is not None:
         ptr, n = ctx.framebuffer_device_ptr()
         ctx.synchronize()
@@ -170,25 +211,7 @@ def main():
         # roofline of the path megakernel (dominant kernel)
         roof = None
         if calib is not None and calib["samples"] > 0:
-            paths = calib["samples"]
-            bytes_calib = calib["nodes_visited"] * NODE_BYTES + calib["prims_tested"] * PRIM_BYTES + paths * RECORD_BYTES
-            bytes_per_sample = bytes_calib / paths
-            launches = max(st["launches_path"], 1)
-            avg_ms = st["kernel_ms_path"] / launches
-            samples_per_launch = st["samples"] / launches
-            bytes_per_launch = bytes_per_sample * samples_per_launch
-            achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-            key = f"{args.config}_{W}x{H}_r{R}_{args.traversal}"
-            traffic = pmc_traffic(key)
-            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "nh_path_kernel", "avg_launch_ms": round(avg_ms, 4),
-                    "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                    "bytes_per_sample": round(bytes_per_sample, 1),
-                    "ray_queries_per_sample": round(calib["ray_queries"] / paths, 3),
-                    "nodes_per_query": round(calib["nodes_visited"] / max(calib["ray_queries"], 1), 3),
-                    "prims_per_query": round(calib["prims_tested"] / max(calib["ray_queries"], 1), 3),
-                    "splat_ms_per_launch": round(st["kernel_ms_splat"] / max(st["launches_splat"], 1), 4)}
+            roof = roofline(args, calib, st, W, H, R)
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(scene, args.cpu_seconds, args.seed)
@@ -207,7 +230,7 @@ def main():
             "data": "synthetic (reference Cornell box scene files, per-path pcg32 seeds)",
             "config": {"workload": f"{scene_desc}, {R * args.steps} spp, path_mis", "config": args.config,
                        "width": W, "height": H, "spp": R * args.steps, "rounds_per_step": R,
-                       "mode": "megakernel", "traversal": args.traversal,
+                       "mode": args.mode, "traversal": args.traversal,
                        "parallelism": f"tile-shard x{world} + RCCL reduce" if world > 1 else "single GPU",
                        "bvh_build_s": round(bvh_s, 3), "upload_s": round(upload_s, 3)},
             "roofline": roof,

@@ -202,6 +202,9 @@ typedef struct nh_render_stats {
     uint64_t boxes_tested;        /* child boxes tested (collect_stats) */
     uint64_t prims_tested;        /* primitive intersection tests (collect_stats) */
     uint64_t invalid_samples;     /* ImageBlock::put drops (NaN/Inf/negative) */
+    /* wavefront mode: the any-hit kernel's share of ray_queries / nodes_visited / boxes_tested /
+       prims_tested (the rest is the extend kernel's) */
+    uint64_t shadow_queries, shadow_nodes_visited, shadow_boxes_tested, shadow_prims_tested;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "nh_internal.h"
@@ -54,8 +55,13 @@ struct nh_ctx {
     int n_list = 0, nbx = 0, nby = 0;
     std::vector<int32_t> list_key;
     bool have_list = false;
-    unsigned long long *counters = nullptr;  // queries, nodes, boxes, prims, invalid
+    unsigned long long *counters = nullptr;  // [0-3] queries, nodes, boxes, prims; [4] invalid; [8-11] wavefront shadow share
     nh_render_stats stats{};
+    // wavefront path state (nh_internal.h WfState), sized for wf_cap paths
+    WfState wf{};
+    std::vector<void *> wf_bufs;
+    size_t wf_cap = 0;
+    unsigned *h_counts = nullptr;  // pinned host mirror of wf.counts
 };
 
 namespace {
@@ -86,7 +92,7 @@ int upload(nh_ctx *c, std::vector<void *> &owner, const T *src, size_t n, const 
 }
 
 void free_all(std::vector<void *> &v) {
-    for (void *p : v) hipFree(p);
+    for (void *p : v) (void)hipFree(p);
     v.clear();
 }
 
@@ -138,33 +144,35 @@ int nh_create(int device, nh_ctx **out) {
     auto *c = new nh_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->counters, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->counters, 16 * sizeof(unsigned long long)) != hipSuccess) {
         delete c;
         return NH_ERR_DEVICE;
     }
-    hipMemset(c->counters, 0, 8 * sizeof(unsigned long long));
+    (void)hipMemset(c->counters, 0, 16 * sizeof(unsigned long long));
     *out = c;
     return NH_OK;
 }
 
 void nh_destroy(nh_ctx *c) {
     if (!c) return;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_all(c->scene_bufs);
     free_all(c->bvh_bufs);
-    hipFree(c->fb);
-    hipFree(c->rec);
-    hipFree(c->rec_jy);
-    hipFree(c->pixel_list);
-    hipFree(c->pixel_map);
-    hipFree(c->block_rank);
-    hipFree(c->block_ids);
-    hipFree(c->block_slot);
-    hipFree(c->staging);
-    hipFree(c->counters);
-    hipFree(c->d_scene);
-    if (c->stream) hipStreamDestroy(c->stream);
+    (void)hipFree(c->fb);
+    (void)hipFree(c->rec);
+    (void)hipFree(c->rec_jy);
+    (void)hipFree(c->pixel_list);
+    (void)hipFree(c->pixel_map);
+    (void)hipFree(c->block_rank);
+    (void)hipFree(c->block_ids);
+    (void)hipFree(c->block_slot);
+    (void)hipFree(c->staging);
+    (void)hipFree(c->counters);
+    (void)hipFree(c->d_scene);
+    free_all(c->wf_bufs);
+    if (c->h_counts) (void)hipHostFree(c->h_counts);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -262,14 +270,14 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     c->integrator = S.integrator;
 
     // master ImageBlock
-    hipFree(c->fb);
+    (void)hipFree(c->fb);
     c->fb = nullptr;
     c->fb_floats = 4 * (size_t)(c->width + 2 * c->border) * (size_t)(c->height + 2 * c->border);
     HIP_TRY(c, hipMalloc(&c->fb, c->fb_floats * sizeof(float)));
     HIP_TRY(c, hipMemsetAsync(c->fb, 0, c->fb_floats * sizeof(float), c->stream));
     // block spiral ranks
     auto rank = spiral_rank(c->width, c->height, 32, c->nbx, c->nby);
-    hipFree(c->block_rank);
+    (void)hipFree(c->block_rank);
     HIP_TRY(c, hipMalloc(&c->block_rank, rank.size() * sizeof(int)));
     HIP_TRY(c, hipMemcpyAsync(c->block_rank, rank.data(), rank.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -430,6 +438,106 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
     return NH_OK;
 }
 
+
+constexpr size_t kWfBytesPerPath = 16 * 9 + 8 + 8 + 4 + 1 + 12;
+
+static int ensure_wf(nh_ctx *c, size_t n) {
+    if (c->wf_cap >= n) return NH_OK;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    free_all(c->wf_bufs);
+    c->wf = WfState{};
+    c->wf_cap = 0;
+    auto alloc = [&](auto *&ptr, size_t count) -> bool {
+        void *p = nullptr;
+        if (hipMalloc(&p, count * sizeof(*ptr)) != hipSuccess) return false;
+        c->wf_bufs.push_back(p);
+        ptr = static_cast<std::remove_reference_t<decltype(ptr)>>(p);
+        return true;
+    };
+    WfState &W = c->wf;
+    bool ok = alloc(W.ray_o, n) && alloc(W.ray_d, n) && alloc(W.hit, n) && alloc(W.rng, n) && alloc(W.li, n) &&
+              alloc(W.thr, n) && alloc(W.pend_ems, n) && alloc(W.pend_col, n) && alloc(W.pend_mis, n) &&
+              alloc(W.sh_o, n) && alloc(W.sh_d, n) && alloc(W.flags, n) && alloc(W.occl, n) &&
+              alloc(W.q_ext[0], n) && alloc(W.q_ext[1], n) && alloc(W.q_sh, n) && alloc(W.counts, 2);
+    if (!ok) {
+        free_all(c->wf_bufs);
+        c->wf = WfState{};
+        return fail(c, "hipMalloc failed for wavefront path state"), NH_ERR_DEVICE;
+    }
+    if (!c->h_counts && hipHostMalloc(reinterpret_cast<void **>(&c->h_counts), 2 * sizeof(unsigned)) != hipSuccess)
+        return fail(c, "hipHostMalloc failed"), NH_ERR_DEVICE;
+    c->wf_cap = n;
+    return NH_OK;
+}
+
+// One chunk of rounds through generate -> {extend, shadow} -> shade until no path is alive.
+// The live counts come back through pinned memory once per bounce (the host needs them to size
+// the next grids); the kernel times are summed per stage.
+static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch &P) {
+    WfLaunch L{};
+    L.st = c->wf;
+    L.n_paths = P.n_paths;
+    L.n_list = P.n_list;
+    L.s0 = P.s0;
+    L.seed = P.seed;
+    L.pixel_list = P.pixel_list;
+    L.rec_rgbx = P.rec_rgbx;
+    L.rec_jy = P.rec_jy;
+    L.counters = P.counters;
+    const bool ordered = q->traversal == NH_TRAVERSAL_ORDERED, stats = q->collect_stats != 0;
+    hipEvent_t ev[4];
+    for (auto &e : ev) HIP_TRY(c, hipEventCreate(&e));
+    struct Guard {
+        hipEvent_t *e;
+        ~Guard() {
+            for (int i = 0; i < 4; ++i) (void)hipEventDestroy(e[i]);
+        }
+    } guard{ev};
+    HIP_TRY(c, hipEventRecord(ev[0], c->stream));
+    nh::launch_wf_generate(c->d_scene, L, c->stream);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(ev[1], c->stream));
+    HIP_TRY(c, hipEventSynchronize(ev[1]));
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+    c->stats.kernel_ms_shade += ms;
+    c->stats.launches_shade++;
+    L.n_ext = P.n_paths;
+    L.n_sh = 0;
+    L.in_q = 0;
+    while (L.n_ext > 0) {
+        HIP_TRY(c, hipMemsetAsync(c->wf.counts, 0, 2 * sizeof(unsigned), c->stream));
+        HIP_TRY(c, hipEventRecord(ev[0], c->stream));
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, c->depth, c->stream);
+        HIP_TRY(c, hipEventRecord(ev[1], c->stream));
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, c->depth, c->stream);
+        HIP_TRY(c, hipEventRecord(ev[2], c->stream));
+        nh::launch_wf_shade(c->d_scene, c->tv, L, c->stream);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipEventRecord(ev[3], c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->h_counts, c->wf.counts, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        float a = 0.f, b = 0.f, d = 0.f;
+        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+        (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+        (void)hipEventElapsedTime(&d, ev[2], ev[3]);
+        c->stats.kernel_ms_extend += a;
+        c->stats.launches_extend++;
+        if (L.n_sh > 0) {
+            c->stats.kernel_ms_shadow += b;
+            c->stats.launches_shadow++;
+        }
+        c->stats.kernel_ms_shade += d;
+        c->stats.launches_shade++;
+        if (c->h_counts[0] > (unsigned)P.n_paths || c->h_counts[1] > c->h_counts[0])
+            return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
+        L.n_ext = (int)c->h_counts[0];
+        L.n_sh = (int)c->h_counts[1];
+        L.in_q ^= 1;
+    }
+    return NH_OK;
+}
+
 static int ensure_pixel_list(nh_ctx *c, const nh_render_req *q) {
     std::vector<int32_t> key;
     if (q->n_blocks > 0 && q->blocks) key.assign(q->blocks, q->blocks + q->n_blocks);
@@ -451,10 +559,10 @@ static int ensure_pixel_list(nh_ctx *c, const nh_render_req *q) {
     }
     std::vector<int> slot_map((size_t)c->nbx * c->nby, -1);
     for (size_t i = 0; i < blocks.size(); ++i) slot_map[blocks[i]] = (int)i;
-    hipFree(c->pixel_list);
-    hipFree(c->pixel_map);
-    hipFree(c->block_ids);
-    hipFree(c->block_slot);
+    (void)hipFree(c->pixel_list);
+    (void)hipFree(c->pixel_map);
+    (void)hipFree(c->block_ids);
+    (void)hipFree(c->block_slot);
     c->pixel_list = c->pixel_map = c->block_ids = c->block_slot = nullptr;
     HIP_TRY(c, hipMalloc(&c->block_ids, std::max<size_t>(blocks.size(), 1) * sizeof(int)));
     HIP_TRY(c, hipMalloc(&c->block_slot, slot_map.size() * sizeof(int)));
@@ -479,7 +587,8 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     if (!c->has_scene || !c->has_bvh) return fail(c, "nh_render: scene and BVH must be uploaded"), NH_ERR_STATE;
     if (q->sample_end < q->sample_begin || q->sample_begin < 0) return fail(c, "invalid sample range"), NH_ERR_INVALID;
     if (c->integrator == 0 && c->n_emitters == 0) return fail(c, "No Emitter in scene!"), NH_ERR_INVALID;
-    if (q->mode != NH_MODE_MEGAKERNEL) return fail(c, "wavefront mode is not built yet"), NH_ERR_UNSUPPORTED;
+    if (q->mode != NH_MODE_MEGAKERNEL && q->mode != NH_MODE_WAVEFRONT) return fail(c, "unknown render mode"), NH_ERR_INVALID;
+    const bool wavefront = q->mode == NH_MODE_WAVEFRONT;
     HIP_TRY(c, hipSetDevice(c->device));
     int rc = ensure_pixel_list(c, q);
     if (rc) return rc;
@@ -492,12 +601,17 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     size_t per_round = (size_t)c->n_list;
     if (c->border > 4) return fail(c, "reconstruction filters wider than border 4 are not supported"), NH_ERR_UNSUPPORTED;
     const size_t block_px = (size_t)(32 + 2 * c->border) * (32 + 2 * c->border);
-    const size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px * 16;
+    size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px * 16;
+    if (wavefront) {  // path state: ~200 B per path in flight
+        per_round_bytes += per_round * kWfBytesPerPath;
+        budget = (size_t)4 << 30;
+        if (const char *e = std::getenv("NH_WF_BUDGET_MB")) budget = (size_t)std::max(1L, std::atol(e)) << 20;
+    }
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / per_round_bytes));
     while ((size_t)chunk * per_round > (size_t)0x7fffffff) chunk = std::max(1, chunk / 2);
     if (c->rec_cap < (size_t)chunk * per_round) {
-        hipFree(c->rec);
-        hipFree(c->rec_jy);
+        (void)hipFree(c->rec);
+        (void)hipFree(c->rec_jy);
         c->rec = nullptr;
         c->rec_jy = nullptr;
         c->rec_cap = (size_t)chunk * per_round;
@@ -505,12 +619,16 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         HIP_TRY(c, hipMalloc(&c->rec_jy, c->rec_cap * sizeof(float)));
     }
     if (c->staging_cap < (size_t)chunk * c->n_blocks * block_px) {
-        hipFree(c->staging);
+        (void)hipFree(c->staging);
         c->staging = nullptr;
         c->staging_cap = (size_t)chunk * c->n_blocks * block_px;
         HIP_TRY(c, hipMalloc(&c->staging, c->staging_cap * sizeof(float4)));
     }
-    if (q->collect_stats) HIP_TRY(c, hipMemsetAsync(c->counters, 0, 8 * sizeof(unsigned long long), c->stream));
+    if (wavefront) {
+        rc = ensure_wf(c, (size_t)chunk * per_round);
+        if (rc) return rc;
+    }
+    if (q->collect_stats) HIP_TRY(c, hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), c->stream));
     struct Ev {
         hipEvent_t a, b, d;
     };
@@ -551,7 +669,13 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         HIP_TRY(c, hipEventCreate(&ev.b));
         HIP_TRY(c, hipEventCreate(&ev.d));
         HIP_TRY(c, hipEventRecord(ev.a, c->stream));
-        nh::launch_path(c->d_scene, c->tv, L, q->traversal == NH_TRAVERSAL_ORDERED, q->collect_stats != 0, c->depth, c->stream);
+        if (wavefront) {
+            rc = render_wavefront(c, q, L);
+            if (rc) return rc;
+        } else {
+            nh::launch_path(c->d_scene, c->tv, L, q->traversal == NH_TRAVERSAL_ORDERED, q->collect_stats != 0, c->depth,
+                            c->stream);
+        }
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev.b, c->stream));
         if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters + 4, c->stream);
@@ -563,25 +687,29 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     for (auto &ev : evs) {
         float a = 0, b = 0;
-        hipEventElapsedTime(&a, ev.a, ev.b);
-        hipEventElapsedTime(&b, ev.b, ev.d);
+        (void)hipEventElapsedTime(&a, ev.a, ev.b);
+        (void)hipEventElapsedTime(&b, ev.b, ev.d);
         c->stats.kernel_ms_path += a;
         c->stats.kernel_ms_splat += b;
-        c->stats.launches_path++;
+        c->stats.launches_path += wavefront ? 0 : 1;
         c->stats.launches_splat++;
-        hipEventDestroy(ev.a);
-        hipEventDestroy(ev.b);
-        hipEventDestroy(ev.d);
+        (void)hipEventDestroy(ev.a);
+        (void)hipEventDestroy(ev.b);
+        (void)hipEventDestroy(ev.d);
     }
     c->stats.samples += (uint64_t)rounds * (uint64_t)c->n_list;
     if (q->collect_stats) {
-        unsigned long long h[8];
+        unsigned long long h[16];
         HIP_TRY(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost));
-        c->stats.ray_queries += h[0];
-        c->stats.nodes_visited += h[1];
-        c->stats.boxes_tested += h[2];
-        c->stats.prims_tested += h[3];
+        c->stats.ray_queries += h[0] + h[8];
+        c->stats.nodes_visited += h[1] + h[9];
+        c->stats.boxes_tested += h[2] + h[10];
+        c->stats.prims_tested += h[3] + h[11];
         c->stats.invalid_samples += h[4];
+        c->stats.shadow_queries += h[8];
+        c->stats.shadow_nodes_visited += h[9];
+        c->stats.shadow_boxes_tested += h[10];
+        c->stats.shadow_prims_tested += h[11];
     }
     return NH_OK;
 }
@@ -637,13 +765,13 @@ int nh_reduce_framebuffers(nh_ctx **ctxs, int32_t n, int32_t root) {
     }
     ncclGroupStart();
     for (int i = 0; i < n; ++i) {
-        hipSetDevice(ctxs[i]->device);
+        (void)hipSetDevice(ctxs[i]->device);
         ncclReduce(ctxs[i]->fb, ctxs[i]->fb, ctxs[i]->fb_floats, ncclFloat, ncclSum, root, comms[i], ctxs[i]->stream);
     }
     ncclResult_t r = ncclGroupEnd();
     for (int i = 0; i < n; ++i) {
-        hipSetDevice(ctxs[i]->device);
-        hipStreamSynchronize(ctxs[i]->stream);
+        (void)hipSetDevice(ctxs[i]->device);
+        (void)hipStreamSynchronize(ctxs[i]->stream);
         ncclCommDestroy(comms[i]);
     }
     if (r != ncclSuccess) {

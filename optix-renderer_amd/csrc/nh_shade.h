@@ -1,0 +1,169 @@
+// Shading-side device functions shared by the megakernel and the wavefront kernels:
+// Mesh/Sphere::setHitInformation, area/point emitters, PerspectiveCamera::sampleRay.
+#pragma once
+#include "nh_traverse.h"
+
+namespace nhd {
+
+struct Its {  // Intersection (include/nori/shape.h:41-79); geoFrame only where needed
+    F3 p;
+    float u, v;
+    Frame sh;
+    int shape;
+};
+
+// Mesh::setHitInformation (mesh.cpp:141-196) / Sphere::setHitInformation (sphere.cpp:96-124)
+__device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, const Hit &h, F3 o, F3 d, Its &its) {
+    const float4 a = tv.prims[3 * h.k], b = tv.prims[3 * h.k + 1];
+    const int shape = __float_as_int(b.w);
+    const DShape sh = S.shapes[shape];
+    its.shape = shape;
+    if (sh.type == SHAPE_SPHERE) {
+        its.p = add(o, scl(h.t, d));
+        F3 n = normalized(sub(its.p, f3(sh.cx, sh.cy, sh.cz)));
+        F3 mn = neg(n);
+        float theta = f_acos(mn.z), phi = f_atan2(mn.y, mn.x);
+        if (phi < 0) phi += 2 * kPi;
+        its.u = phi / (2.f * kPi);
+        its.v = theta / kPi;
+        F3 t = normalized(cross(f3(0, 0, 1), n));
+        its.sh.s = t;
+        its.sh.t = cross(n, t);
+        its.sh.n = n;
+        return;
+    }
+    const int local = __float_as_int(a.w);
+    const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + local);
+    const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
+    const float bx = 1 - (h.u + h.v), by = h.u, bz = h.v;
+    const F3 p0 = ldv(S.V, i0), p1 = ldv(S.V, i1), p2 = ldv(S.V, i2);
+    its.p = add(add(scl(bx, p0), scl(by, p1)), scl(bz, p2));
+    its.u = h.u;
+    its.v = h.v;
+    if (sh.has_uv) {
+        its.u = bx * S.UV[2 * i0] + by * S.UV[2 * i1] + bz * S.UV[2 * i2];
+        its.v = bx * S.UV[2 * i0 + 1] + by * S.UV[2 * i1 + 1] + bz * S.UV[2 * i2 + 1];
+    }
+    if (sh.has_n) {
+        F3 nrm = normalized(add(add(scl(bx, ldv(S.N, i0)), scl(by, ldv(S.N, i1))), scl(bz, ldv(S.N, i2))));
+        if (sh.has_uv) {
+            its.sh.s = normalized(add(add(scl(bx, ldv(S.T, i0)), scl(by, ldv(S.T, i1))), scl(bz, ldv(S.T, i2))));
+            its.sh.t = normalized(add(add(scl(bx, ldv(S.BT, i0)), scl(by, ldv(S.BT, i1))), scl(bz, ldv(S.BT, i2))));
+            its.sh.n = nrm;
+        } else {
+            its.sh = frame_from_n(nrm);
+        }
+    } else {
+        its.sh = frame_from_n(normalized(cross(sub(p1, p0), sub(p2, p0))));
+    }
+}
+
+// AreaEmitter / PointLight (src/emitters/arealight.cpp:58-125, pointlight.cpp:47-78)
+__device__ __forceinline__ float emitter_pdf(const DScene &S, const DEmitter &e, F3 ref, F3 p, F3 n, F3 wi) {
+    if (e.type == EMITTER_POINT) return 1.f;
+    if (dot(n, neg(wi)) < 0.f) return 0.f;
+    const DShape sh = S.shapes[e.shape];
+    // Sphere::pdfSurface: std::pow(1.f / r, 2) (double, exact square) * (0.25f / M_PI)
+    float prob = sh.type == SHAPE_MESH
+                     ? sh.pdf_norm
+                     : (float)((double)(1.f / sh.radius) * (double)(1.f / sh.radius) * (double)(0.25f / kPi));
+    return prob * dot(sub(p, ref), sub(p, ref)) / fabsf(dot(n, neg(wi)));
+}
+__device__ __forceinline__ F3 emitter_eval(const DEmitter &e, F3 ref, F3 n, F3 wi) {
+    if (e.type == EMITTER_POINT) {
+        F3 dd = sub(ref, f3(e.px, e.py, e.pz));
+        float q = dot(dd, dd);
+        return f3(e.lr / q, e.lg / q, e.lb / q);
+    }
+    if (dot(n, neg(wi)) < 0.f) return f3(0, 0, 0);
+    return f3(e.lr, e.lg, e.lb);
+}
+
+struct ESample {
+    F3 wi, p, n;
+    F3 so, sd;  // shadow ray, from the light towards ref
+    float smint, smaxt;
+};
+
+__device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e, F3 ref, float sx, float sy,
+                                             ESample &es) {
+    if (e.type == EMITTER_POINT) {
+        F3 pos = f3(e.px, e.py, e.pz);
+        F3 rp = sub(ref, pos);
+        es.so = pos;
+        es.sd = normalized(rp);
+        es.smint = kEps;
+        es.smaxt = f_sqrt(dot(rp, rp)) - kEps;
+        es.wi = normalized(sub(pos, ref));
+        es.p = f3(0, 0, 0);
+        es.n = f3(0, 0, 0);
+        return emitter_eval(e, ref, es.n, es.wi);
+    }
+    const DShape sh = S.shapes[e.shape];
+    F3 p, n;
+    if (sh.type == SHAPE_MESH) {  // Mesh::sampleSurface (mesh.cpp:50-71)
+        const float *cdf = S.area_cdf + sh.pdf_off;
+        int idt = dpdf_sample(cdf, sh.n_faces, sx);
+        sx = (sx - cdf[idt]) / (cdf[idt + 1] - cdf[idt]);
+        float su1 = f_sqrt(sx);  // squareToUniformTriangle (warp.cpp:162-166)
+        float bu = 1.f - su1, bv = sy * su1, bw = 1.f - bu - bv;
+        const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + idt);
+        const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
+        const F3 p0 = ldv(S.V, i0), p1 = ldv(S.V, i1), p2 = ldv(S.V, i2);
+        p = add(add(scl(bu, p0), scl(bv, p1)), scl(bw, p2));
+        if (sh.has_n)
+            n = normalized(add(add(scl(bu, ldv(S.N, i0)), scl(bv, ldv(S.N, i1))), scl(bw, ldv(S.N, i2))));
+        else
+            n = normalized(cross(sub(p1, p0), sub(p2, p0)));
+    } else {  // Sphere::sampleSurface (sphere.cpp:126-131)
+        F3 q = uniform_sphere(sx, sy);
+        p = add(f3(sh.cx, sh.cy, sh.cz), scl(sh.radius, q));
+        n = q;
+    }
+    es.p = p;
+    es.n = n;
+    F3 pr = sub(p, ref);
+    es.wi = normalized(pr);
+    es.so = p;
+    es.sd = neg(es.wi);
+    es.smint = kEps;
+    es.smaxt = f_sqrt(dot(pr, pr)) - kEps;
+    float probs = emitter_pdf(S, e, ref, p, n, es.wi);
+    if (fabsf(probs) < kEps) return f3(0, 0, 0);
+    F3 ev = emitter_eval(e, ref, n, es.wi);
+    return f3(ev.x / probs, ev.y / probs, ev.z / probs);
+}
+
+// PerspectiveCamera::sampleRay without depth of field (perspective.cpp:97-141)
+__device__ __forceinline__ void camera_ray(const DScene &S, float px, float py, F3 &o, F3 &d, float &mint,
+                                           float &maxt) {
+    const float in0 = px * S.inv_w, in1 = py * S.inv_h;
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float acc = S.s2c[4 * i] * in0;
+        acc = acc + S.s2c[4 * i + 1] * in1;
+        acc = acc + S.s2c[4 * i + 2] * 0.0f;
+        acc = acc + S.s2c[4 * i + 3] * 1.0f;
+        r[i] = acc;
+    }
+    F3 dl = normalized(f3(r[0] / r[3], r[1] / r[3], r[2] / r[3]));
+    float ow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float acc = S.c2w[4 * i] * 0.0f;
+        acc = acc + S.c2w[4 * i + 1] * 0.0f;
+        acc = acc + S.c2w[4 * i + 2] * 0.0f;
+        acc = acc + S.c2w[4 * i + 3] * 1.0f;
+        ow[i] = acc;
+    }
+    o = f3(ow[0] / ow[3], ow[1] / ow[3], ow[2] / ow[3]);
+    const float *w = S.c2w;
+    d = f3(w[0] * dl.x + (w[1] * dl.y + w[2] * dl.z), w[4] * dl.x + (w[5] * dl.y + w[6] * dl.z),
+           w[8] * dl.x + (w[9] * dl.y + w[10] * dl.z));
+    const float inv_z = 1.0f / dl.z;
+    mint = S.near_clip * inv_z;
+    maxt = S.far_clip * inv_z;
+}
+
+}  // namespace nhd

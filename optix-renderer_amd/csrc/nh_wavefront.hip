@@ -1,0 +1,311 @@
+// Wavefront path_mis / path_mats for gfx950: the same per-path semantics as the megakernel
+// (nh_kernels.hip li_path_mis, i.e. src/integrators/path_mis.cpp:16-150), split into
+// kernels over SoA path state in HBM so each stage runs at its own occupancy:
+//
+//   wf_generate  renderBlock's per-pixel prologue (render.cpp:441-447): seeding, jitter,
+//                camera ray (perspective.cpp:97-141)
+//   wf_extend    closest-hit traversal of every live path's ray (the BSDF-sampled ray is the
+//                MIS probe and the next bounce at once, path_mis.cpp:117/:146) -- the
+//                BVH-traversal kernel whose roofline bench.py reports
+//   wf_shadow    any-hit traversal of the shadow rays queued by the previous shade (:89)
+//   wf_shade     finishes the previous bounce (shadow result -> w_ems, probe hit -> w_mats,
+//                discrete override, Li accumulation, :103-146), then shades the new hit
+//                (emitter term, Russian roulette, NEE sample, BSDF sample) and appends the
+//                path to the next extend queue and, when it sampled a light, to the shadow
+//                queue (wave-aggregated atomics: one atomic per wave per queue)
+//
+// Each path's random numbers come from its own pcg32 stream in the reference's draw order,
+// so the wavefront and megakernel renders are identical.
+#include "nh_internal.h"
+#include "nh_shade.h"
+
+using namespace nhd;
+
+namespace {
+
+enum : int { F_FIRST = 1 << 2, F_NEE = 1 << 3 };  // bits 0-1: measure; bits 4-5: path_mats counter
+
+__device__ __forceinline__ int wave_append(unsigned *counter, bool pred) {
+    const unsigned long long mask = __ballot(pred);
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)mask) - 1;
+    unsigned base = 0;
+    if (mask != 0ull && lane == leader) base = atomicAdd(counter, (unsigned)__popcll(mask));
+    base = __shfl(base, leader < 0 ? 0 : leader, 64);
+    return (int)base + __popcll(mask & ((1ull << lane) - 1ull));
+}
+
+__device__ __forceinline__ F3 xyz(float4 v) { return f3(v.x, v.y, v.z); }
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void wf_generate(const DScene *__restrict__ Sp, WfLaunch L) {
+    const DScene &S = *Sp;
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= L.n_paths) return;
+    const int k = p / L.n_list, i = p - k * L.n_list;
+    const int pix = L.pixel_list[i];
+    const int py = pix / S.width, px = pix - py * S.width;
+    Rng rng = path_rng(L.seed, (uint64_t)pix, (uint64_t)(L.s0 + k));
+    const float jx = rng.next1d(), jy = rng.next1d();
+    rng.next1d();  // apertureSample (render.cpp:443), unused without depth of field
+    rng.next1d();
+    F3 o, d;
+    float mint, maxt;
+    camera_ray(S, (float)px + jx, (float)py + jy, o, d, mint, maxt);
+    WfState &W = L.st;
+    W.ray_o[p] = make_float4(o.x, o.y, o.z, mint);
+    W.ray_d[p] = make_float4(d.x, d.y, d.z, maxt);
+    W.rng[p] = rng.state;
+    W.li[p] = make_float4(0.f, 0.f, 0.f, 1.f);   // Li, w_mats
+    W.thr[p] = make_float4(1.f, 1.f, 1.f, 0.f);  // throughput, w_ems
+    W.flags[p] = F_FIRST;
+    W.q_ext[0][p] = p;
+    L.rec_rgbx[p] = make_float4(0.f, 0.f, 0.f, jx);
+    L.rec_jy[p] = jy;
+}
+
+template <int DEPTH, bool ORDERED, bool STATS>
+__global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+    __shared__ uint32_t stk[DEPTH * 128];
+    const DScene &S = *Sp;
+    const int q = blockIdx.x * 128 + threadIdx.x;
+    TravStats st{0, 0, 0};
+    bool live = false;
+    if (q < L.n_ext) {
+        const int p = L.st.q_ext[L.in_q][q];
+        const float4 ro = L.st.ray_o[p], rd = L.st.ray_d[p];
+        Hit h;
+        // a zero BSDF direction (maxt = -inf) misses every primitive: not traversed, as in the megakernel
+        live = rd.w >= ro.w;
+        const bool found = live && trace<DEPTH, ORDERED, false, STATS>(tv, S, xyz(ro), xyz(rd), ro.w, rd.w, h,
+                                                                       stk + threadIdx.x, 128, st);
+        L.st.hit[p] = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
+    }
+    if (STATS) {
+        unsigned long long v[4] = {live ? 1ull : 0ull, st.nodes, st.boxes, st.prims};
+        for (int j = 0; j < 4; ++j) {
+            unsigned long long x = v[j];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            if ((threadIdx.x & 63) == 0) atomicAdd(&L.counters[j], x);
+        }
+    }
+}
+
+template <int DEPTH, bool ORDERED, bool STATS>
+__global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+    __shared__ uint32_t stk[DEPTH * 128];
+    const DScene &S = *Sp;
+    const int q = blockIdx.x * 128 + threadIdx.x;
+    TravStats st{0, 0, 0};
+    if (q < L.n_sh) {
+        const int p = L.st.q_sh[q];
+        const float4 so = L.st.sh_o[p], sd = L.st.sh_d[p];
+        Hit h;
+        const bool occ = trace<DEPTH, ORDERED, true, STATS>(tv, S, xyz(so), xyz(sd), so.w, sd.w, h,
+                                                            stk + threadIdx.x, 128, st);
+        L.st.occl[p] = occ ? 1 : 0;
+    }
+    if (STATS) {
+        unsigned long long v[4] = {q < L.n_sh ? 1ull : 0ull, st.nodes, st.boxes, st.prims};
+        for (int j = 0; j < 4; ++j) {
+            unsigned long long x = v[j];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            if ((threadIdx.x & 63) == 0) atomicAdd(&L.counters[8 + j], x);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void wf_shade(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+    const DScene &S = *Sp;
+    WfState &W = L.st;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    bool cont = false, nee = false;
+    int p = -1;
+    if (q < L.n_ext) {
+        p = W.q_ext[L.in_q][q];
+        const float4 ro = W.ray_o[p], rd = W.ray_d[p], hv = W.hit[p];
+        const F3 o = xyz(ro), d = xyz(rd);
+        float4 li4 = W.li[p], th4 = W.thr[p];
+        F3 li = xyz(li4), t = xyz(th4);
+        float w_mats = li4.w, w_ems = th4.w;
+        int flags = W.flags[p];
+        Hit h;
+        h.t = hv.x;
+        h.u = hv.y;
+        h.v = hv.z;
+        h.k = __float_as_int(hv.w);
+        const bool found = h.k >= 0;
+        Its its;
+        bool have_its = false;
+        const float n_lights = (float)S.n_emitters;
+        Rng rng;
+        rng.state = W.rng[p];
+        rng.inc = ((uint64_t)(L.s0 + p / L.n_list) << 1u) | 1u;
+        bool alive = true;
+        if (S.integrator == 1) {  // ---------------- path_mats (path_mats.cpp:16-78)
+            if (!(flags & F_FIRST)) t = mulc(t, xyz(W.pend_col[p]));
+            if (!found) {
+                alive = false;
+            } else {
+                hit_info(S, tv, h, o, d, its);
+                const DShape shape = S.shapes[its.shape];
+                const DBsdf bsdf = S.bsdfs[shape.bsdf];
+                if (shape.emitter >= 0) {
+                    const F3 wi = normalized(sub(its.p, o));
+                    li = add(li, mulc(t, emitter_eval(S.emitters[shape.emitter], o, its.sh.n, wi)));
+                }
+                int counter = (flags >> 4) & 3;
+                const float succ = e_min(max_coeff(t), 0.99f);
+                if (counter < 3) counter++;
+                else if (rng.next1d() > succ) alive = false;
+                else t = divs(t, succ);
+                if (alive) {
+                    const float bx = rng.next1d(), by = rng.next1d();
+                    F3 wo;
+                    int measure;
+                    const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure);
+                    const F3 nd = to_world(its.sh, wo);
+                    W.pend_col[p] = make_float4(col.x, col.y, col.z, 0.f);
+                    W.ray_o[p] = make_float4(its.p.x, its.p.y, its.p.z, kEps);
+                    W.ray_d[p] = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
+                    flags = counter << 4;
+                }
+            }
+        } else {  // ---------------- path_mis
+            if (!(flags & F_FIRST)) {  // finish the previous bounce (path_mis.cpp:103-146)
+                float4 pe = W.pend_ems[p], pc = W.pend_col[p];
+                const float2 pm = W.pend_mis[p];
+                F3 li_ems = xyz(pe);
+                float pdfems = pe.w, pdfems_mats = pc.w;
+                const F3 bsdf_col = xyz(pc);
+                if ((flags & F_NEE) && W.occl[p]) {
+                    li_ems = f3(0, 0, 0);
+                    pdfems = 0.f;
+                    pdfems_mats = 0.f;
+                }
+                if ((pdfems_mats + pdfems) > kEps) w_ems = pdfems / (pdfems_mats + pdfems);
+                if (!is_zero(bsdf_col) && found) {
+                    hit_info(S, tv, h, o, d, its);
+                    have_its = true;
+                    const int hem = S.shapes[its.shape].emitter;
+                    if (hem >= 0) {
+                        const F3 wim = normalized(sub(its.p, o));
+                        const float pdfmat_ems = emitter_pdf(S, S.emitters[hem], o, its.p, its.sh.n, wim) / n_lights;
+                        if ((pm.x + pdfmat_ems) > kEps) w_mats = pm.x / (pm.x + pdfmat_ems);
+                    }
+                }
+                if ((flags & 3) == M_DISCRETE) {
+                    w_ems = 0.f;
+                    w_mats = 1.f;
+                }
+                li = add(li, mulc(scl(w_ems, t), li_ems));
+                t = mulc(t, bsdf_col);
+            }
+            if (!found) {
+                alive = false;
+            } else {
+                if (!have_its) hit_info(S, tv, h, o, d, its);
+                const DShape shape = S.shapes[its.shape];
+                const DBsdf bsdf = S.bsdfs[shape.bsdf];
+                if (shape.emitter >= 0) {  // path_mis.cpp:51-56, ref = ray origin
+                    const F3 wi = normalized(sub(its.p, o));
+                    li = add(li, mulc(scl(w_mats, t), emitter_eval(S.emitters[shape.emitter], o, its.sh.n, wi)));
+                }
+                float succ = e_min(max_coeff(t), 0.99f);
+                succ = e_max(succ, kEps);
+                if (rng.next1d() > succ) {
+                    alive = false;
+                } else {
+                    t = divs(t, succ);
+                    const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, rng.next1d());
+                    const DEmitter em = S.emitters[ei];
+                    const float ex = rng.next1d(), ey = rng.next1d();
+                    ESample es;
+                    const F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
+                    const F3 wi_l = to_local(its.sh, neg(d));
+                    nee = !is_zero(ems_col);
+                    F3 li_ems = f3(0, 0, 0);
+                    float pdfems = 0.f, pdfems_mats = 0.f;
+                    if (nee) {
+                        const F3 we = to_local(its.sh, es.wi);
+                        const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
+                        const float cs = we.z;
+                        li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
+                                    ems_col.z * cs * f.z * n_lights);
+                        pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
+                        pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
+                        W.sh_o[p] = make_float4(es.so.x, es.so.y, es.so.z, es.smint);
+                        W.sh_d[p] = make_float4(es.sd.x, es.sd.y, es.sd.z, es.smaxt);
+                    }
+                    const float bx = rng.next1d(), by = rng.next1d();
+                    F3 wo;
+                    int measure;
+                    const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
+                    const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
+                    const F3 nd = to_world(its.sh, wo);
+                    W.pend_ems[p] = make_float4(li_ems.x, li_ems.y, li_ems.z, pdfems);
+                    W.pend_col[p] = make_float4(bsdf_col.x, bsdf_col.y, bsdf_col.z, pdfems_mats);
+                    W.pend_mis[p] = make_float2(pdfmat, 0.f);
+                    W.ray_o[p] = make_float4(its.p.x, its.p.y, its.p.z, kEps);
+                    W.ray_d[p] = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
+                    flags = (measure & 3) | (nee ? F_NEE : 0);
+                }
+            }
+        }
+        cont = alive;
+        if (alive) {
+            W.li[p] = make_float4(li.x, li.y, li.z, w_mats);
+            W.thr[p] = make_float4(t.x, t.y, t.z, w_ems);
+            W.rng[p] = rng.state;
+            W.flags[p] = flags;
+        } else {
+            float4 *r = &L.rec_rgbx[p];
+            r->x = li.x;
+            r->y = li.y;
+            r->z = li.z;
+        }
+    }
+    const int se = wave_append(&W.counts[0], cont);
+    if (cont) W.q_ext[1 - L.in_q][se] = p;
+    const int ss = wave_append(&W.counts[1], cont && nee);
+    if (cont && nee) W.q_sh[ss] = p;
+}
+
+namespace nh {
+
+template <int DEPTH>
+static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
+                              bool shadow, hipStream_t st) {
+    const int n = shadow ? L.n_sh : L.n_ext;
+    if (n <= 0) return;
+    dim3 grid((n + 127) / 128);
+#define NH_WF(K, O, T) hipLaunchKernelGGL((K<DEPTH, O, T>), grid, dim3(128), 0, st, S, tv, L)
+    if (shadow) {
+        if (ordered) { if (stats) NH_WF(wf_shadow, true, true); else NH_WF(wf_shadow, true, false); }
+        else { if (stats) NH_WF(wf_shadow, false, true); else NH_WF(wf_shadow, false, false); }
+    } else {
+        if (ordered) { if (stats) NH_WF(wf_extend, true, true); else NH_WF(wf_extend, true, false); }
+        else { if (stats) NH_WF(wf_extend, false, true); else NH_WF(wf_extend, false, false); }
+    }
+#undef NH_WF
+}
+
+void launch_wf_trace(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool shadow,
+                     int depth, hipStream_t st) {
+    if (depth <= 16) launch_wf_trace_d<16>(S, tv, L, ordered, stats, shadow, st);
+    else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, st);
+    else if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, st);
+    else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, st);
+}
+
+void launch_wf_generate(const DScene *S, const WfLaunch &L, hipStream_t st) {
+    hipLaunchKernelGGL(wf_generate, dim3((L.n_paths + 255) / 256), dim3(256), 0, st, S, L);
+}
+
+void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, hipStream_t st) {
+    if (L.n_ext <= 0) return;
+    hipLaunchKernelGGL(wf_shade, dim3((L.n_ext + 255) / 256), dim3(256), 0, st, S, tv, L);
+}
+
+}  // namespace nh

@@ -106,7 +106,9 @@ class nh_render_stats(C.Structure):
                 ("launches_splat", C.c_uint64), ("launches_extend", C.c_uint64), ("launches_shadow", C.c_uint64),
                 ("launches_shade", C.c_uint64), ("samples", C.c_uint64), ("ray_queries", C.c_uint64),
                 ("nodes_visited", C.c_uint64), ("boxes_tested", C.c_uint64), ("prims_tested", C.c_uint64),
-                ("invalid_samples", C.c_uint64)]
+                ("invalid_samples", C.c_uint64), ("shadow_queries", C.c_uint64),
+                ("shadow_nodes_visited", C.c_uint64), ("shadow_boxes_tested", C.c_uint64),
+                ("shadow_prims_tested", C.c_uint64)]
 
 
 def _sig(name, res, *args):

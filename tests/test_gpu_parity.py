@@ -95,7 +95,10 @@ def test_trace_parity_bumpy_mesh(gpu, tmp_path, traversal):
     compare_trace(ctx, orc, *secondary_rays(orc, 20000, 5), traversal)
 
 
-def render_pair(xml, w, h, spp, seed=5, traversal=nh.TRAVERSAL_REFERENCE, integrator=None):
+MODES = [pytest.param(nh.MODE_MEGAKERNEL, id="mega"), pytest.param(nh.MODE_WAVEFRONT, id="wave")]
+
+
+def render_pair(xml, w, h, spp, seed=5, traversal=nh.TRAVERSAL_REFERENCE, integrator=None, mode=nh.MODE_MEGAKERNEL):
     s = nh.Scene(xml)
     s.set_resolution(w, h)
     if integrator is not None:
@@ -103,34 +106,37 @@ def render_pair(xml, w, h, spp, seed=5, traversal=nh.TRAVERSAL_REFERENCE, integr
     b = nh.Bvh(s)
     ctx = nh.Context(0)
     ctx.upload(s, b)
-    ctx.render(0, spp, seed=seed, traversal=traversal, clear=True)
+    ctx.render(0, spp, seed=seed, traversal=traversal, clear=True, mode=mode)
     g = ctx.framebuffer()
     r = no.OracleScene(s).render(0, spp, seed=seed)
     return g, r, s
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("variant", ["c1", "c2"])
 @pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED])
-def test_render_parity_cbox(gpu, tmp_path, variant, traversal):
+def test_render_parity_cbox(gpu, tmp_path, variant, traversal, mode):
     xml = scenegen.cbox_xml(str(tmp_path), variant)
-    g, r, s = render_pair(xml, 64, 48, 16, traversal=traversal)
+    g, r, s = render_pair(xml, 64, 48, 16, traversal=traversal, mode=mode)
     e = rel_l2(g, r)
-    print(f"{variant} traversal={traversal}: rel-L2 {e:.3e}, max|d| {np.abs(g - r).max():.3e}")
+    print(f"{variant} traversal={traversal} mode={mode}: rel-L2 {e:.3e}, max|d| {np.abs(g - r).max():.3e}")
     assert e < TOL_REL_L2
     img_g, img_r = nh.to_rgb(g, s.border), nh.to_rgb(r, s.border)
     assert rel_l2(img_g, img_r) < TOL_REL_L2
     assert img_r.mean() > 0.05
 
 
-def test_render_parity_path_mats(gpu, tmp_path):
+@pytest.mark.parametrize("mode", MODES)
+def test_render_parity_path_mats(gpu, tmp_path, mode):
     xml = scenegen.cbox_xml(str(tmp_path), "c1")
-    g, r, _ = render_pair(xml, 48, 48, 16, integrator=nh.INTEGRATOR_PATH_MATS)
+    g, r, _ = render_pair(xml, 48, 48, 16, integrator=nh.INTEGRATOR_PATH_MATS, mode=mode)
     assert rel_l2(g, r) < TOL_REL_L2
 
 
-def test_render_parity_microfacet_mesh(gpu, tmp_path):
+@pytest.mark.parametrize("mode", MODES)
+def test_render_parity_microfacet_mesh(gpu, tmp_path, mode):
     xml, _ = scenegen.bumpy_cbox_xml(str(tmp_path), 120, 60)
-    g, r, _ = render_pair(xml, 48, 40, 8, traversal=nh.TRAVERSAL_ORDERED)
+    g, r, _ = render_pair(xml, 48, 40, 8, traversal=nh.TRAVERSAL_ORDERED, mode=mode)
     e = rel_l2(g, r)
     print(f"microfacet mesh rel-L2 {e:.3e}")
     assert e < TOL_REL_L2
@@ -161,3 +167,31 @@ def test_render_deterministic_and_sharded(gpu, tmp_path):
     ctx.render(0, 3, seed=3, clear=True)
     ctx.render(3, 8, seed=3, clear=False)
     assert rel_l2(ctx.framebuffer(), full) < 1e-6
+
+
+def test_wavefront_matches_megakernel(gpu, tmp_path, monkeypatch):
+    """Same per-path random streams and arithmetic: the two schedules give bitwise-equal
+    framebuffers and identical traversal work, also when the wavefront splits the rounds into
+    several chunks (a 1 MiB path-state budget) and renders a block subset."""
+    xml = scenegen.cbox_xml(str(tmp_path), "c2")
+    s = nh.Scene(xml)
+    s.set_resolution(160, 96)
+    b = nh.Bvh(s)
+    out = {}
+    for mode in (nh.MODE_MEGAKERNEL, nh.MODE_WAVEFRONT):
+        ctx = nh.Context(0)
+        ctx.upload(s, b)
+        ctx.render(0, 12, seed=9, traversal=nh.TRAVERSAL_ORDERED, clear=True, stats=True, mode=mode,
+                   blocks=[0, 2, 3, 5, 7, 8, 11])
+        out[mode] = (ctx.framebuffer(), ctx.stats())
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    for k in ("samples", "ray_queries", "nodes_visited", "prims_tested", "invalid_samples"):
+        assert out[0][1][k] == out[1][1][k], k
+    assert out[1][1]["launches_extend"] > 5
+    monkeypatch.setenv("NH_WF_BUDGET_MB", "1")
+    ctx = nh.Context(0)
+    ctx.upload(s, b)
+    ctx.render(0, 12, seed=9, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT,
+               blocks=[0, 2, 3, 5, 7, 8, 11])
+    np.testing.assert_array_equal(out[0][0], ctx.framebuffer())
+    assert ctx.stats()["launches_splat"] > 1
