@@ -439,7 +439,7 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
 }
 
 
-constexpr size_t kWfBytesPerPath = 16 * 9 + 8 + 8 + 4 + 1 + 12;
+constexpr size_t kWfBytesPerPath = 2 * (16 * 7 + 8 + 4 + 4 + 4 + 1) + 36;  // two buffers + shadow queue
 
 static int ensure_wf(nh_ctx *c, size_t n) {
     if (c->wf_cap >= n) return NH_OK;
@@ -455,16 +455,20 @@ static int ensure_wf(nh_ctx *c, size_t n) {
         return true;
     };
     WfState &W = c->wf;
-    bool ok = alloc(W.ray_o, n) && alloc(W.ray_d, n) && alloc(W.hit, n) && alloc(W.rng, n) && alloc(W.li, n) &&
-              alloc(W.thr, n) && alloc(W.pend_ems, n) && alloc(W.pend_col, n) && alloc(W.pend_mis, n) &&
-              alloc(W.sh_o, n) && alloc(W.sh_d, n) && alloc(W.flags, n) && alloc(W.occl, n) &&
-              alloc(W.q_ext[0], n) && alloc(W.q_ext[1], n) && alloc(W.q_sh, n) && alloc(W.counts, 2);
+    const size_t nq = n + (size_t)(kQueueShards + 2) * 256;  // shard segments round up to whole shade blocks
+    bool ok = true;
+    for (WfBuf &B : W.buf)
+        ok = ok && alloc(B.ray_o, nq) && alloc(B.ray_d, nq) && alloc(B.hit, nq) && alloc(B.rng, nq) &&
+             alloc(B.li, nq) && alloc(B.thr, nq) && alloc(B.pend_ems, nq) && alloc(B.pend_col, nq) &&
+             alloc(B.pdfmat, nq) && alloc(B.flags, nq) && alloc(B.pid, nq) && alloc(B.occl, nq);
+    ok = ok && alloc(W.sh_o, nq) && alloc(W.sh_d, nq) && alloc(W.sh_slot, nq) &&
+         alloc(W.counts, 2 * kQueueShards * kCountStride);
     if (!ok) {
         free_all(c->wf_bufs);
         c->wf = WfState{};
         return fail(c, "hipMalloc failed for wavefront path state"), NH_ERR_DEVICE;
     }
-    if (!c->h_counts && hipHostMalloc(reinterpret_cast<void **>(&c->h_counts), 2 * sizeof(unsigned)) != hipSuccess)
+    if (!c->h_counts && hipHostMalloc(reinterpret_cast<void **>(&c->h_counts), 2 * kQueueShards * kCountStride * sizeof(unsigned)) != hipSuccess)
         return fail(c, "hipHostMalloc failed"), NH_ERR_DEVICE;
     c->wf_cap = n;
     return NH_OK;
@@ -505,8 +509,16 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     L.n_ext = P.n_paths;
     L.n_sh = 0;
     L.in_q = 0;
+    const int per_block = 256;
+    const int max_blocks = (P.n_paths + per_block - 1) / per_block;
+    L.seg_cap = (max_blocks + kQueueShards - 1) / kQueueShards * per_block;
+    for (int s = 0; s <= kQueueShards; ++s) {
+        L.pre_ext[s] = s == 0 ? 0 : L.n_ext;  // generate wrote a dense queue
+        L.pre_sh[s] = 0;
+    }
+    const size_t count_bytes = 2 * kQueueShards * kCountStride * sizeof(unsigned);
     while (L.n_ext > 0) {
-        HIP_TRY(c, hipMemsetAsync(c->wf.counts, 0, 2 * sizeof(unsigned), c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->wf.counts, 0, count_bytes, c->stream));
         HIP_TRY(c, hipEventRecord(ev[0], c->stream));
         nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[1], c->stream));
@@ -515,7 +527,7 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         nh::launch_wf_shade(c->d_scene, c->tv, L, c->stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], c->stream));
-        HIP_TRY(c, hipMemcpyAsync(c->h_counts, c->wf.counts, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->h_counts, c->wf.counts, count_bytes, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         float a = 0.f, b = 0.f, d = 0.f;
         (void)hipEventElapsedTime(&a, ev[0], ev[1]);
@@ -529,10 +541,20 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         }
         c->stats.kernel_ms_shade += d;
         c->stats.launches_shade++;
-        if (c->h_counts[0] > (unsigned)P.n_paths || c->h_counts[1] > c->h_counts[0])
-            return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
-        L.n_ext = (int)c->h_counts[0];
-        L.n_sh = (int)c->h_counts[1];
+        size_t ne = 0, ns = 0;
+        for (int s = 0; s < kQueueShards; ++s) {
+            const unsigned ce = c->h_counts[s * kCountStride], cs = c->h_counts[(kQueueShards + s) * kCountStride];
+            if (ce > (unsigned)L.seg_cap || cs > ce) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
+            L.pre_ext[s] = (int)ne;
+            L.pre_sh[s] = (int)ns;
+            ne += ce;
+            ns += cs;
+        }
+        L.pre_ext[kQueueShards] = (int)ne;
+        L.pre_sh[kQueueShards] = (int)ns;
+        if (ne > (size_t)P.n_paths) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
+        L.n_ext = (int)ne;
+        L.n_sh = (int)ns;
         L.in_q ^= 1;
     }
     return NH_OK;
@@ -604,7 +626,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px * 16;
     if (wavefront) {  // path state: ~200 B per path in flight
         per_round_bytes += per_round * kWfBytesPerPath;
-        budget = (size_t)4 << 30;
+        budget = (size_t)8 << 30;
         if (const char *e = std::getenv("NH_WF_BUDGET_MB")) budget = (size_t)std::max(1L, std::atol(e)) << 20;
     }
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / per_round_bytes));

@@ -49,9 +49,13 @@ void launch_splat(const SplatLaunch &P, hipStream_t st);
 void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st);
 }  // namespace nh
 
-// Wavefront path state (nh_wavefront.hip): structure of arrays indexed by path id
-// p = round * n_list + list entry, the same index as the sample records.
-struct WfState {
+// Queue appends go to one counter per XCD (blocks are dealt round-robin over the 8 XCDs), so no
+// address takes device-scope atomics from more than one XCD.
+constexpr int kQueueShards = 8, kCountStride = 32;
+
+// Wavefront path state (nh_wavefront.hip): one side of the double-buffered, dense SoA state.
+// Slot s of a buffer holds one live path; pid is its sample-record index (round * n_list + entry).
+struct WfBuf {
     float4 *ray_o, *ray_d;   // (origin, mint), (direction, maxt) of the ray to trace next
     float4 *hit;             // (t, u, v, prim index bits or -1) from the extend kernel
     uint64_t *rng;           // pcg32 state (inc is derived from the sample index)
@@ -59,13 +63,17 @@ struct WfState {
     float4 *thr;             // (throughput, w_ems)
     float4 *pend_ems;        // pending NEE: (Li_ems, pdfems)
     float4 *pend_col;        // pending BSDF sample: (bsdf_col, pdfems_mats)
-    float2 *pend_mis;        // (pdfmat, unused)
-    float4 *sh_o, *sh_d;     // shadow ray (origin, mint), (direction, maxt)
+    float *pdfmat;           // pending BSDF sample pdf (MIS weight of an emitter hit)
     int *flags;              // measure | F_FIRST | F_NEE | path_mats counter
-    uint8_t *occl;           // any-hit result of the shadow ray
-    int *q_ext[2];           // extend queues (ping-pong)
-    int *q_sh;               // shadow queue
-    unsigned *counts;        // [0] next extend count, [1] shadow count
+    int *pid;
+    uint8_t *occl;           // any-hit result of the path's shadow ray
+};
+struct WfState {
+    WfBuf buf[2];
+    float4 *sh_o, *sh_d;     // shadow queue: (origin, mint), (direction, maxt)
+    int *sh_slot;            // slot of the shadow ray's path in the buffer shade wrote
+    unsigned *counts;        // per-shard append counters, one 128-B line each:
+                             // [s * kCountStride] paths, [(kQueueShards + s) * kCountStride] shadow rays
 };
 struct WfLaunch {
     WfState st;
@@ -75,6 +83,10 @@ struct WfLaunch {
     float4 *rec_rgbx;
     float *rec_jy;
     int n_ext, n_sh, in_q;
+    // queue entry q lives at slot s * seg_cap + (q - pre[s]) for the shard s with
+    // pre[s] <= q < pre[s + 1] (a dense queue is pre = {0, n, n, ...})
+    int seg_cap;
+    int pre_ext[kQueueShards + 1], pre_sh[kQueueShards + 1];
     unsigned long long *counters;
 };
 namespace nh {

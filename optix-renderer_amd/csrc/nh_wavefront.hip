@@ -10,14 +10,25 @@
 //   wf_shadow    any-hit traversal of the shadow rays queued by the previous shade (:89)
 //   wf_shade     finishes the previous bounce (shadow result -> w_ems, probe hit -> w_mats,
 //                discrete override, Li accumulation, :103-146), then shades the new hit
-//                (emitter term, Russian roulette, NEE sample, BSDF sample) and appends the
-//                path to the next extend queue and, when it sampled a light, to the shadow
-//                queue (wave-aggregated atomics: one atomic per wave per queue)
+//                (emitter term, Russian roulette, NEE sample, BSDF sample)
+//
+// Path state is double-buffered and kept DENSE: wf_shade reads live path i of buffer A and
+// writes each surviving path's whole state to the next free slot of buffer B (ranks from wave
+// ballots + LDS atomics, one device-scope atomic per workgroup and queue). Every kernel then
+// streams its arrays coalesced, with no index indirection. Shadow rays are written densely to
+// their own queue together with the slot of their path in B; wf_shadow stores the any-hit result
+// into B's occlusion byte for that slot.
+//
+// Queues and buffers are split into kQueueShards segments of seg_cap entries: workgroup b
+// appends to segment b % 8 (its XCD, as workgroups are dealt round-robin over the XCDs), so no
+// counter takes device-scope atomics from two XCDs (one shared counter serialised the kernel).
 //
 // Each path's random numbers come from its own pcg32 stream in the reference's draw order,
 // so the wavefront and megakernel renders are identical.
 #include "nh_internal.h"
 #include "nh_shade.h"
+
+#include <cstdlib>
 
 using namespace nhd;
 
@@ -25,6 +36,8 @@ namespace {
 
 enum : int { F_FIRST = 1 << 2, F_NEE = 1 << 3 };  // bits 0-1: measure; bits 4-5: path_mats counter
 
+// rank of this lane among the wave's lanes with pred set, offset by the wave's reservation in
+// *counter (an LDS counter here)
 __device__ __forceinline__ int wave_append(unsigned *counter, bool pred) {
     const unsigned long long mask = __ballot(pred);
     const int lane = threadIdx.x & 63;
@@ -36,6 +49,37 @@ __device__ __forceinline__ int wave_append(unsigned *counter, bool pred) {
 }
 
 __device__ __forceinline__ F3 xyz(float4 v) { return f3(v.x, v.y, v.z); }
+
+__device__ __forceinline__ int queue_slot(const int *pre, int seg_cap, int q) {
+    int slot = q;
+#pragma unroll
+    for (int s = 1; s < kQueueShards; ++s)
+        if (q >= pre[s]) slot = s * seg_cap + (q - pre[s]);
+    return slot;
+}
+
+// the state one shade step produces for a surviving path
+struct PState {
+    float4 ro, rd;   // next ray (origin, mint), (direction, maxt)
+    float4 li, thr;  // (Li, w_mats), (throughput, w_ems)
+    float4 pe, pc;   // pending NEE (Li_ems, pdfems), pending BSDF sample (bsdf_col, pdfems_mats)
+    float pdfmat;
+    uint64_t rng;
+    int flags, pid;
+};
+
+__device__ __forceinline__ void store_state(const WfBuf &B, int s, const PState &o) {
+    B.ray_o[s] = o.ro;
+    B.ray_d[s] = o.rd;
+    B.li[s] = o.li;
+    B.thr[s] = o.thr;
+    B.pend_ems[s] = o.pe;
+    B.pend_col[s] = o.pc;
+    B.pdfmat[s] = o.pdfmat;
+    B.rng[s] = o.rng;
+    B.flags[s] = o.flags;
+    B.pid[s] = o.pid;
+}
 
 }  // namespace
 
@@ -53,14 +97,14 @@ __global__ __launch_bounds__(256) void wf_generate(const DScene *__restrict__ Sp
     F3 o, d;
     float mint, maxt;
     camera_ray(S, (float)px + jx, (float)py + jy, o, d, mint, maxt);
-    WfState &W = L.st;
-    W.ray_o[p] = make_float4(o.x, o.y, o.z, mint);
-    W.ray_d[p] = make_float4(d.x, d.y, d.z, maxt);
-    W.rng[p] = rng.state;
-    W.li[p] = make_float4(0.f, 0.f, 0.f, 1.f);   // Li, w_mats
-    W.thr[p] = make_float4(1.f, 1.f, 1.f, 0.f);  // throughput, w_ems
-    W.flags[p] = F_FIRST;
-    W.q_ext[0][p] = p;
+    const WfBuf &B = L.st.buf[L.in_q];
+    B.ray_o[p] = make_float4(o.x, o.y, o.z, mint);
+    B.ray_d[p] = make_float4(d.x, d.y, d.z, maxt);
+    B.rng[p] = rng.state;
+    B.li[p] = make_float4(0.f, 0.f, 0.f, 1.f);   // Li, w_mats
+    B.thr[p] = make_float4(1.f, 1.f, 1.f, 0.f);  // throughput, w_ems
+    B.flags[p] = F_FIRST;
+    B.pid[p] = p;
     L.rec_rgbx[p] = make_float4(0.f, 0.f, 0.f, jx);
     L.rec_jy[p] = jy;
 }
@@ -73,14 +117,15 @@ __global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, 
     TravStats st{0, 0, 0};
     bool live = false;
     if (q < L.n_ext) {
-        const int p = L.st.q_ext[L.in_q][q];
-        const float4 ro = L.st.ray_o[p], rd = L.st.ray_d[p];
+        const WfBuf &B = L.st.buf[L.in_q];
+        const int s = queue_slot(L.pre_ext, L.seg_cap, q);
+        const float4 ro = B.ray_o[s], rd = B.ray_d[s];
         Hit h;
         // a zero BSDF direction (maxt = -inf) misses every primitive: not traversed, as in the megakernel
         live = rd.w >= ro.w;
         const bool found = live && trace<DEPTH, ORDERED, false, STATS>(tv, S, xyz(ro), xyz(rd), ro.w, rd.w, h,
                                                                        stk + threadIdx.x, 128, st);
-        L.st.hit[p] = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
+        B.hit[s] = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
     }
     if (STATS) {
         unsigned long long v[4] = {live ? 1ull : 0ull, st.nodes, st.boxes, st.prims};
@@ -99,12 +144,12 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
     const int q = blockIdx.x * 128 + threadIdx.x;
     TravStats st{0, 0, 0};
     if (q < L.n_sh) {
-        const int p = L.st.q_sh[q];
-        const float4 so = L.st.sh_o[p], sd = L.st.sh_d[p];
+        const int s = queue_slot(L.pre_sh, L.seg_cap, q);
+        const float4 so = L.st.sh_o[s], sd = L.st.sh_d[s];
         Hit h;
         const bool occ = trace<DEPTH, ORDERED, true, STATS>(tv, S, xyz(so), xyz(sd), so.w, sd.w, h,
                                                             stk + threadIdx.x, 128, st);
-        L.st.occl[p] = occ ? 1 : 0;
+        L.st.buf[L.in_q].occl[L.st.sh_slot[s]] = occ ? 1 : 0;
     }
     if (STATS) {
         unsigned long long v[4] = {q < L.n_sh ? 1ull : 0ull, st.nodes, st.boxes, st.prims};
@@ -116,160 +161,191 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
     }
 }
 
-__global__ __launch_bounds__(256) void wf_shade(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
-    const DScene &S = *Sp;
-    WfState &W = L.st;
-    const int q = blockIdx.x * 256 + threadIdx.x;
-    bool cont = false, nee = false;
-    int p = -1;
-    if (q < L.n_ext) {
-        p = W.q_ext[L.in_q][q];
-        const float4 ro = W.ray_o[p], rd = W.ray_d[p], hv = W.hit[p];
-        const F3 o = xyz(ro), d = xyz(rd);
-        float4 li4 = W.li[p], th4 = W.thr[p];
-        F3 li = xyz(li4), t = xyz(th4);
-        float w_mats = li4.w, w_ems = th4.w;
-        int flags = W.flags[p];
-        Hit h;
-        h.t = hv.x;
-        h.u = hv.y;
-        h.v = hv.z;
-        h.k = __float_as_int(hv.w);
-        const bool found = h.k >= 0;
-        Its its;
-        bool have_its = false;
-        const float n_lights = (float)S.n_emitters;
-        Rng rng;
-        rng.state = W.rng[p];
-        rng.inc = ((uint64_t)(L.s0 + p / L.n_list) << 1u) | 1u;
-        bool alive = true;
-        if (S.integrator == 1) {  // ---------------- path_mats (path_mats.cpp:16-78)
-            if (!(flags & F_FIRST)) t = mulc(t, xyz(W.pend_col[p]));
-            if (!found) {
-                alive = false;
-            } else {
-                hit_info(S, tv, h, o, d, its);
-                const DShape shape = S.shapes[its.shape];
-                const DBsdf bsdf = S.bsdfs[shape.bsdf];
-                if (shape.emitter >= 0) {
-                    const F3 wi = normalized(sub(its.p, o));
-                    li = add(li, mulc(t, emitter_eval(S.emitters[shape.emitter], o, its.sh.n, wi)));
-                }
-                int counter = (flags >> 4) & 3;
-                const float succ = e_min(max_coeff(t), 0.99f);
-                if (counter < 3) counter++;
-                else if (rng.next1d() > succ) alive = false;
-                else t = divs(t, succ);
-                if (alive) {
-                    const float bx = rng.next1d(), by = rng.next1d();
-                    F3 wo;
-                    int measure;
-                    const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure);
-                    const F3 nd = to_world(its.sh, wo);
-                    W.pend_col[p] = make_float4(col.x, col.y, col.z, 0.f);
-                    W.ray_o[p] = make_float4(its.p.x, its.p.y, its.p.z, kEps);
-                    W.ray_d[p] = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
-                    flags = counter << 4;
-                }
+// One shade step of the path in slot s of buffer B. Returns whether the path continues (its
+// next state in o); sets nee when it sampled a light (shadow ray in so/sd). A terminated path
+// writes its radiance to its sample record.
+__device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv, const WfLaunch &L, const WfBuf &B,
+                                           int s, PState &o, bool &nee, float4 &so, float4 &sd) {
+    const float4 ro = B.ray_o[s], rd = B.ray_d[s], hv = B.hit[s];
+    const F3 org = xyz(ro), d = xyz(rd);
+    const float4 li4 = B.li[s], th4 = B.thr[s];
+    F3 li = xyz(li4), t = xyz(th4);
+    float w_mats = li4.w, w_ems = th4.w;
+    const int flags = B.flags[s];
+    const int pid = B.pid[s];
+    Hit h;
+    h.t = hv.x;
+    h.u = hv.y;
+    h.v = hv.z;
+    h.k = __float_as_int(hv.w);
+    const bool found = h.k >= 0;
+    Its its;
+    bool have_its = false;
+    const float n_lights = (float)S.n_emitters;
+    Rng rng;
+    rng.state = B.rng[s];
+    rng.inc = ((uint64_t)(L.s0 + pid / L.n_list) << 1u) | 1u;
+    bool alive = true;
+    if (S.integrator == 1) {  // ---------------- path_mats (path_mats.cpp:16-78)
+        if (!(flags & F_FIRST)) t = mulc(t, xyz(B.pend_col[s]));
+        if (!found) {
+            alive = false;
+        } else {
+            hit_info(S, tv, h, org, d, its);
+            const DShape shape = S.shapes[its.shape];
+            const DBsdf bsdf = S.bsdfs[shape.bsdf];
+            if (shape.emitter >= 0) {
+                const F3 wi = normalized(sub(its.p, org));
+                li = add(li, mulc(t, emitter_eval(S.emitters[shape.emitter], org, its.sh.n, wi)));
             }
-        } else {  // ---------------- path_mis
-            if (!(flags & F_FIRST)) {  // finish the previous bounce (path_mis.cpp:103-146)
-                float4 pe = W.pend_ems[p], pc = W.pend_col[p];
-                const float2 pm = W.pend_mis[p];
-                F3 li_ems = xyz(pe);
-                float pdfems = pe.w, pdfems_mats = pc.w;
-                const F3 bsdf_col = xyz(pc);
-                if ((flags & F_NEE) && W.occl[p]) {
-                    li_ems = f3(0, 0, 0);
-                    pdfems = 0.f;
-                    pdfems_mats = 0.f;
-                }
-                if ((pdfems_mats + pdfems) > kEps) w_ems = pdfems / (pdfems_mats + pdfems);
-                if (!is_zero(bsdf_col) && found) {
-                    hit_info(S, tv, h, o, d, its);
-                    have_its = true;
-                    const int hem = S.shapes[its.shape].emitter;
-                    if (hem >= 0) {
-                        const F3 wim = normalized(sub(its.p, o));
-                        const float pdfmat_ems = emitter_pdf(S, S.emitters[hem], o, its.p, its.sh.n, wim) / n_lights;
-                        if ((pm.x + pdfmat_ems) > kEps) w_mats = pm.x / (pm.x + pdfmat_ems);
-                    }
-                }
-                if ((flags & 3) == M_DISCRETE) {
-                    w_ems = 0.f;
-                    w_mats = 1.f;
-                }
-                li = add(li, mulc(scl(w_ems, t), li_ems));
-                t = mulc(t, bsdf_col);
-            }
-            if (!found) {
-                alive = false;
-            } else {
-                if (!have_its) hit_info(S, tv, h, o, d, its);
-                const DShape shape = S.shapes[its.shape];
-                const DBsdf bsdf = S.bsdfs[shape.bsdf];
-                if (shape.emitter >= 0) {  // path_mis.cpp:51-56, ref = ray origin
-                    const F3 wi = normalized(sub(its.p, o));
-                    li = add(li, mulc(scl(w_mats, t), emitter_eval(S.emitters[shape.emitter], o, its.sh.n, wi)));
-                }
-                float succ = e_min(max_coeff(t), 0.99f);
-                succ = e_max(succ, kEps);
-                if (rng.next1d() > succ) {
-                    alive = false;
-                } else {
-                    t = divs(t, succ);
-                    const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, rng.next1d());
-                    const DEmitter em = S.emitters[ei];
-                    const float ex = rng.next1d(), ey = rng.next1d();
-                    ESample es;
-                    const F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
-                    const F3 wi_l = to_local(its.sh, neg(d));
-                    nee = !is_zero(ems_col);
-                    F3 li_ems = f3(0, 0, 0);
-                    float pdfems = 0.f, pdfems_mats = 0.f;
-                    if (nee) {
-                        const F3 we = to_local(its.sh, es.wi);
-                        const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
-                        const float cs = we.z;
-                        li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
-                                    ems_col.z * cs * f.z * n_lights);
-                        pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
-                        pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
-                        W.sh_o[p] = make_float4(es.so.x, es.so.y, es.so.z, es.smint);
-                        W.sh_d[p] = make_float4(es.sd.x, es.sd.y, es.sd.z, es.smaxt);
-                    }
-                    const float bx = rng.next1d(), by = rng.next1d();
-                    F3 wo;
-                    int measure;
-                    const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
-                    const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
-                    const F3 nd = to_world(its.sh, wo);
-                    W.pend_ems[p] = make_float4(li_ems.x, li_ems.y, li_ems.z, pdfems);
-                    W.pend_col[p] = make_float4(bsdf_col.x, bsdf_col.y, bsdf_col.z, pdfems_mats);
-                    W.pend_mis[p] = make_float2(pdfmat, 0.f);
-                    W.ray_o[p] = make_float4(its.p.x, its.p.y, its.p.z, kEps);
-                    W.ray_d[p] = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
-                    flags = (measure & 3) | (nee ? F_NEE : 0);
-                }
+            int counter = (flags >> 4) & 3;
+            const float succ = e_min(max_coeff(t), 0.99f);
+            if (counter < 3) counter++;
+            else if (rng.next1d() > succ) alive = false;
+            else t = divs(t, succ);
+            if (alive) {
+                const float bx = rng.next1d(), by = rng.next1d();
+                F3 wo;
+                int measure;
+                const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure);
+                const F3 nd = to_world(its.sh, wo);
+                o.pc = make_float4(col.x, col.y, col.z, 0.f);
+                o.pe = make_float4(0.f, 0.f, 0.f, 0.f);
+                o.pdfmat = 0.f;
+                o.ro = make_float4(its.p.x, its.p.y, its.p.z, kEps);
+                o.rd = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
+                o.flags = counter << 4;
             }
         }
-        cont = alive;
-        if (alive) {
-            W.li[p] = make_float4(li.x, li.y, li.z, w_mats);
-            W.thr[p] = make_float4(t.x, t.y, t.z, w_ems);
-            W.rng[p] = rng.state;
-            W.flags[p] = flags;
+    } else {  // ---------------- path_mis
+        if (!(flags & F_FIRST)) {  // finish the previous bounce (path_mis.cpp:103-146)
+            const float4 pc = B.pend_col[s];
+            const F3 bsdf_col = xyz(pc);
+            F3 li_ems = f3(0, 0, 0);
+            float pdfems = 0.f, pdfems_mats = 0.f;
+            if ((flags & F_NEE) && !B.occl[s]) {  // unoccluded light sample (an unqueued one is all zero)
+                const float4 pe = B.pend_ems[s];
+                li_ems = xyz(pe);
+                pdfems = pe.w;
+                pdfems_mats = pc.w;
+            }
+            if ((pdfems_mats + pdfems) > kEps) w_ems = pdfems / (pdfems_mats + pdfems);
+            if (!is_zero(bsdf_col) && found) {
+                hit_info(S, tv, h, org, d, its);
+                have_its = true;
+                const int hem = S.shapes[its.shape].emitter;
+                if (hem >= 0) {
+                    const float pdfmat = B.pdfmat[s];
+                    const F3 wim = normalized(sub(its.p, org));
+                    const float pdfmat_ems = emitter_pdf(S, S.emitters[hem], org, its.p, its.sh.n, wim) / n_lights;
+                    if ((pdfmat + pdfmat_ems) > kEps) w_mats = pdfmat / (pdfmat + pdfmat_ems);
+                }
+            }
+            if ((flags & 3) == M_DISCRETE) {
+                w_ems = 0.f;
+                w_mats = 1.f;
+            }
+            li = add(li, mulc(scl(w_ems, t), li_ems));
+            t = mulc(t, bsdf_col);
+        }
+        if (!found) {
+            alive = false;
         } else {
-            float4 *r = &L.rec_rgbx[p];
-            r->x = li.x;
-            r->y = li.y;
-            r->z = li.z;
+            if (!have_its) hit_info(S, tv, h, org, d, its);
+            const DShape shape = S.shapes[its.shape];
+            const DBsdf bsdf = S.bsdfs[shape.bsdf];
+            if (shape.emitter >= 0) {  // path_mis.cpp:51-56, ref = ray origin
+                const F3 wi = normalized(sub(its.p, org));
+                li = add(li, mulc(scl(w_mats, t), emitter_eval(S.emitters[shape.emitter], org, its.sh.n, wi)));
+            }
+            float succ = e_min(max_coeff(t), 0.99f);
+            succ = e_max(succ, kEps);
+            if (rng.next1d() > succ) {
+                alive = false;
+            } else {
+                t = divs(t, succ);
+                const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, rng.next1d());
+                const DEmitter em = S.emitters[ei];
+                const float ex = rng.next1d(), ey = rng.next1d();
+                ESample es;
+                const F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
+                const F3 wi_l = to_local(its.sh, neg(d));
+                nee = !is_zero(ems_col);
+                F3 li_ems = f3(0, 0, 0);
+                float pdfems = 0.f, pdfems_mats = 0.f;
+                if (nee) {
+                    const F3 we = to_local(its.sh, es.wi);
+                    const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
+                    const float cs = we.z;
+                    li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
+                                ems_col.z * cs * f.z * n_lights);
+                    pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
+                    pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
+                    so = make_float4(es.so.x, es.so.y, es.so.z, es.smint);
+                    sd = make_float4(es.sd.x, es.sd.y, es.sd.z, es.smaxt);
+                }
+                const float bx = rng.next1d(), by = rng.next1d();
+                F3 wo;
+                int measure;
+                const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
+                const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
+                const F3 nd = to_world(its.sh, wo);
+                o.pe = make_float4(li_ems.x, li_ems.y, li_ems.z, pdfems);
+                o.pc = make_float4(bsdf_col.x, bsdf_col.y, bsdf_col.z, pdfems_mats);
+                o.pdfmat = pdfmat;
+                o.ro = make_float4(its.p.x, its.p.y, its.p.z, kEps);
+                o.rd = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
+                o.flags = (measure & 3) | (nee ? F_NEE : 0);
+            }
         }
     }
-    const int se = wave_append(&W.counts[0], cont);
-    if (cont) W.q_ext[1 - L.in_q][se] = p;
-    const int ss = wave_append(&W.counts[1], cont && nee);
-    if (cont && nee) W.q_sh[ss] = p;
+    if (alive) {
+        o.li = make_float4(li.x, li.y, li.z, w_mats);
+        o.thr = make_float4(t.x, t.y, t.z, w_ems);
+        o.rng = rng.state;
+        o.pid = pid;
+    } else {
+        float4 *r = &L.rec_rgbx[pid];
+        r->x = li.x;
+        r->y = li.y;
+        r->z = li.z;
+    }
+    return alive;
+}
+
+// One queue entry per thread; survivors are ranked within the workgroup (wave ballots + LDS
+// atomics), the workgroup reserves its ranges of the next buffer and the shadow queue with one
+// device-scope atomic each, then every thread stores its state at its final slot.
+__global__ __launch_bounds__(256, 4) void wf_shade(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+    __shared__ unsigned s_n[2], s_base[2];
+    const DScene &S = *Sp;
+    if (threadIdx.x < 2) s_n[threadIdx.x] = 0u;
+    __syncthreads();
+    const int q = blockIdx.x * 256 + (int)threadIdx.x;
+    bool cont = false, nee = false;
+    PState o;
+    float4 so, sd;
+    if (q < L.n_ext)
+        cont = shade_path(S, tv, L, L.st.buf[L.in_q], queue_slot(L.pre_ext, L.seg_cap, q), o, nee, so, sd);
+    const int le = wave_append(&s_n[0], cont);
+    const int ls = wave_append(&s_n[1], cont && nee);
+    __syncthreads();
+    const int shard = blockIdx.x & (kQueueShards - 1);
+    if (threadIdx.x == 0) {
+        s_base[0] = s_n[0] ? atomicAdd(&L.st.counts[shard * kCountStride], s_n[0]) : 0u;
+        s_base[1] = s_n[1] ? atomicAdd(&L.st.counts[(kQueueShards + shard) * kCountStride], s_n[1]) : 0u;
+    }
+    __syncthreads();
+    if (cont) {
+        const int slot = shard * L.seg_cap + (int)s_base[0] + le;
+        store_state(L.st.buf[1 - L.in_q], slot, o);
+        if (nee) {
+            const int ss = shard * L.seg_cap + (int)s_base[1] + ls;
+            L.st.sh_o[ss] = so;
+            L.st.sh_d[ss] = sd;
+            L.st.sh_slot[ss] = slot;
+        }
+    }
 }
 
 namespace nh {
