@@ -1,21 +1,26 @@
 """Benchmark of the MI355X path_mis hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--traversal ordered]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--mode wavefront]
 
 Workload (N=1, BASELINE.json configs[1]): Cornell box diffuse-only (C2: both spheres
 diffuse), 1024x1024, 256 spp, path_mis, per-path pcg32 seeding. One step = `--rounds`
-(default 16) sample rounds over the whole image, i.e. one nh_render call = one path
-megakernel launch + one ImageBlock splat launch; the default K=16 steps render the full
-256 spp. Multi-GPU: one process per GPU (torchrun), 32x32 image blocks dealt round-robin
-to ranks (tile shard, fixed total image => strong scaling), one RCCL reduce (sum) of the
-RGBW framebuffer to rank 0 inside the timed region.
+(default 16) sample rounds over the whole image = one nh_render call: the wavefront pipeline
+(generate, then extend / any-hit / shade per bounce until no path is alive) or, with
+--mode megakernel, one path-kernel launch; then one ImageBlock splat. The default K=16 steps
+render the full 256 spp. Multi-GPU: one process per GPU (torchrun), 32x32 image blocks dealt
+round-robin to ranks (tile shard, fixed total image => strong scaling), one RCCL reduce (sum)
+of the RGBW framebuffer to rank 0 inside the timed region.
 
 The JSON line also carries:
-  roofline      path megakernel: algorithmic bytes per launch (BVH nodes x 64 B + primitive
-                tests x 48 B + 20 B sample record per path, counted in-kernel in a separate
-                calibration launch on the same seeds) / average launch time from HIP events on
-                the kernel's stream, against 8 TB/s HBM; traffic from the committed rocprofv3
-                PMC summary when one exists for this workload, else null
+  roofline      the dominant kernel (largest summed HIP-event time on the context's stream):
+                  wf_shade    path-state bytes loaded + stored (counted by construction from
+                              the queue counts)
+                  wf_extend   BVH nodes x 64 B + primitive tests x 48 B (in-kernel counters in
+                              a calibration launch on the same seeds) + 48 B ray/hit per query
+                  nh_path_kernel (megakernel) nodes x 64 + prims x 48 + 20 B record per path
+                ... / average launch duration, against 8 TB/s HBM; traffic = HBM bytes per
+                launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json)
+                when one exists for this workload, else null
   cpu_baseline  the CPU oracle (oracle/, a restatement of the reference's path_mis) timed on
                 this host on a bounded sample of the same workload (rank 0, N=1 only)
 """
@@ -46,7 +51,7 @@ def parse():
     p.add_argument("--width", type=int, default=None)
     p.add_argument("--height", type=int, default=None)
     p.add_argument("--traversal", default="ordered", choices=["ordered", "reference"])
-    p.add_argument("--mode", default="megakernel", choices=["megakernel", "wavefront"])
+    p.add_argument("--mode", default="wavefront", choices=["megakernel", "wavefront"])
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-calibrate", action="store_true")
@@ -91,15 +96,20 @@ def roofline(args, calib, st, W, H, R):
                   4 B, ray 32 B in, hit 16 B out)"""
     paths = calib["samples"]
     if args.mode == "wavefront":
+        # dominant stage by measured time
+        stage = max(("extend", "shadow", "shade"), key=lambda k: st[f"kernel_ms_{k}"])
         q = calib["ray_queries"] - calib["shadow_queries"]
         nodes = calib["nodes_visited"] - calib["shadow_nodes_visited"]
         prims = calib["prims_tested"] - calib["shadow_prims_tested"]
-        bytes_calib = nodes * NODE_BYTES + prims * PRIM_BYTES + q * EXTEND_IO_BYTES
-        launches, ms, kernel = max(st["launches_extend"], 1), st["kernel_ms_extend"], "wf_extend"
+        if stage == "shade":
+            bytes_calib = calib["shade_state_bytes"]
+        elif stage == "extend":
+            bytes_calib = nodes * NODE_BYTES + prims * PRIM_BYTES + calib["extend_queue_bytes"]
+        else:
+            bytes_calib = (calib["shadow_nodes_visited"] * NODE_BYTES + calib["shadow_prims_tested"] * PRIM_BYTES
+                           + calib["shadow_queue_bytes"])
+        launches, ms, kernel = max(st[f"launches_{stage}"], 1), st[f"kernel_ms_{stage}"], f"wf_{stage}"
     else:
-        q, nodes, prims = calib["ray_queries"], calib["nodes_visited"], calib["prims_tested"]
-        bytes_calib = nodes * NODE_BYTES + prims * PRIM_BYTES + paths * RECORD_BYTES
-        launches, ms, kernel = max(st["launches_path"], 1), st["kernel_ms_path"], "nh_path_kernel"
     bytes_per_sample = bytes_calib / paths
     avg_ms = ms / launches
     bytes_per_launch = bytes_per_sample * st["samples"] / launches
@@ -116,6 +126,17 @@ def roofline(args, calib, st, W, H, R):
             "splat_ms_per_launch": round(st["kernel_ms_splat"] / max(st["launches_splat"], 1), 4)}
     if args.mode == "wavefront":
         roof["stage_ms"] = {k: round(st[f"kernel_ms_{k}"], 3) for k in ("extend", "shadow", "shade", "splat")}
+        # every traversal/shade stage against HBM, algorithmic bytes as above (per-sample from calibration)
+        per = {"shade": calib["shade_state_bytes"],
+               "extend": nodes * NODE_BYTES + prims * PRIM_BYTES + calib["extend_queue_bytes"],
+               "extend_queue_only": calib["extend_queue_bytes"],
+               "shadow": (calib["shadow_nodes_visited"] * NODE_BYTES + calib["shadow_prims_tested"] * PRIM_BYTES
+                          + calib["shadow_queue_bytes"])}
+        roof["stage_gbs"] = {}
+        for k, b in per.items():
+            t = st["kernel_ms_" + k.split("_")[0]]
+            if t > 0:
+                roof["stage_gbs"][k] = round(b / paths * st["samples"] / (t * 1e-3) / 1e9, 1)
     return roof
 
 

@@ -205,6 +205,9 @@ typedef struct nh_render_stats {
     /* wavefront mode: the any-hit kernel's share of ray_queries / nodes_visited / boxes_tested /
        prims_tested (the rest is the extend kernel's) */
     uint64_t shadow_queries, shadow_nodes_visited, shadow_boxes_tested, shadow_prims_tested;
+    /* wavefront mode, always counted (host side, from the queue counts): path-state bytes the
+       shade kernels load + store, and the queue bytes of the extend / any-hit kernels */
+    uint64_t shade_state_bytes, extend_queue_bytes, shadow_queue_bytes, paths_shaded;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;

@@ -497,15 +497,8 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
             for (int i = 0; i < 4; ++i) (void)hipEventDestroy(e[i]);
         }
     } guard{ev};
-    HIP_TRY(c, hipEventRecord(ev[0], c->stream));
-    nh::launch_wf_generate(c->d_scene, L, c->stream);
+    nh::launch_wf_generate(c->d_scene, L, c->stream);  // timed with the whole chunk (kernel_ms_path)
     HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipEventRecord(ev[1], c->stream));
-    HIP_TRY(c, hipEventSynchronize(ev[1]));
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
-    c->stats.kernel_ms_shade += ms;
-    c->stats.launches_shade++;
     L.n_ext = P.n_paths;
     L.n_sh = 0;
     L.in_q = 0;
@@ -517,6 +510,7 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         L.pre_sh[s] = 0;
     }
     const size_t count_bytes = 2 * kQueueShards * kCountStride * sizeof(unsigned);
+    bool first = true;
     while (L.n_ext > 0) {
         HIP_TRY(c, hipMemsetAsync(c->wf.counts, 0, count_bytes, c->stream));
         HIP_TRY(c, hipEventRecord(ev[0], c->stream));
@@ -553,6 +547,16 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         L.pre_ext[kQueueShards] = (int)ne;
         L.pre_sh[kQueueShards] = (int)ns;
         if (ne > (size_t)P.n_paths) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
+        // bytes by construction (nh_wavefront.hip): shade loads 96 B per path (ray, hit, Li, throughput,
+        // rng, flags, pid), +16 pending BSDF sample after the first bounce, +17 (pending NEE + occlusion)
+        // per queued shadow ray; stores 116 B per survivor, 36 per new shadow ray, 12 per finished path
+        const uint64_t shaded = (uint64_t)L.n_ext, pend = first ? 0 : shaded;
+        c->stats.paths_shaded += shaded;
+        c->stats.shade_state_bytes += shaded * 96 + pend * 16 + (uint64_t)L.n_sh * 17 + ne * 116 + ns * 36 +
+                                      (shaded - ne) * 12;
+        c->stats.extend_queue_bytes += shaded * 48;        // ray in (32 B), hit out (16 B)
+        c->stats.shadow_queue_bytes += (uint64_t)L.n_sh * 37;  // ray in, path slot, occlusion byte out
+        first = false;
         L.n_ext = (int)ne;
         L.n_sh = (int)ns;
         L.in_q ^= 1;

@@ -223,11 +223,13 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
             const F3 bsdf_col = xyz(pc);
             F3 li_ems = f3(0, 0, 0);
             float pdfems = 0.f, pdfems_mats = 0.f;
-            if ((flags & F_NEE) && !B.occl[s]) {  // unoccluded light sample (an unqueued one is all zero)
+            if (flags & F_NEE) {  // a queued light sample counts unless occluded (an unqueued one is all zero)
                 const float4 pe = B.pend_ems[s];
-                li_ems = xyz(pe);
-                pdfems = pe.w;
-                pdfems_mats = pc.w;
+                if (!B.occl[s]) {
+                    li_ems = xyz(pe);
+                    pdfems = pe.w;
+                    pdfems_mats = pc.w;
+                }
             }
             if ((pdfems_mats + pdfems) > kEps) w_ems = pdfems / (pdfems_mats + pdfems);
             if (!is_zero(bsdf_col) && found) {

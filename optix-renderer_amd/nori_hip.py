@@ -108,7 +108,9 @@ class nh_render_stats(C.Structure):
                 ("nodes_visited", C.c_uint64), ("boxes_tested", C.c_uint64), ("prims_tested", C.c_uint64),
                 ("invalid_samples", C.c_uint64), ("shadow_queries", C.c_uint64),
                 ("shadow_nodes_visited", C.c_uint64), ("shadow_boxes_tested", C.c_uint64),
-                ("shadow_prims_tested", C.c_uint64)]
+                ("shadow_prims_tested", C.c_uint64), ("shade_state_bytes", C.c_uint64),
+                ("extend_queue_bytes", C.c_uint64), ("shadow_queue_bytes", C.c_uint64),
+                ("paths_shaded", C.c_uint64)]
 
 
 def _sig(name, res, *args):
