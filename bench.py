@@ -92,8 +92,8 @@ def roofline(args, calib, st, W, H, R):
     kernel's summed HIP-event duration over the timed region on the context's stream.
       megakernel: nh_path_kernel -- BVH nodes x 64 B + primitive tests x 48 B (closest, probe and
                   shadow queries) + 20 B sample record per path
-      wavefront:  wf_extend -- the closest-hit share of nodes/prims + 52 B per query (queue index
-                  4 B, ray 32 B in, hit 16 B out)"""
+      wavefront:  the dominant stage -- wf_shade: path-state bytes; wf_extend: the closest-hit
+                  share of nodes/prims + 48 B per query (ray 32 B in, hit 16 B out)"""
     paths = calib["samples"]
     if args.mode == "wavefront":
         # dominant stage by measured time
@@ -110,6 +110,9 @@ def roofline(args, calib, st, W, H, R):
                            + calib["shadow_queue_bytes"])
         launches, ms, kernel = max(st[f"launches_{stage}"], 1), st[f"kernel_ms_{stage}"], f"wf_{stage}"
     else:
+        q, nodes, prims = calib["ray_queries"], calib["nodes_visited"], calib["prims_tested"]
+        bytes_calib = nodes * NODE_BYTES + prims * PRIM_BYTES + paths * RECORD_BYTES
+        launches, ms, kernel = max(st["launches_path"], 1), st["kernel_ms_path"], "nh_path_kernel"
     bytes_per_sample = bytes_calib / paths
     avg_ms = ms / launches
     bytes_per_launch = bytes_per_sample * st["samples"] / launches
