@@ -1,0 +1,29 @@
+"""Record HBM bytes per launch of one kernel from a scripts/pmc.sh run into profiles/pmc_traffic.json.
+
+usage: python scripts/pmc_traffic.py gpurun_out/pmc_TAG WORKLOAD_KEY KERNEL_SUBSTRING
+FETCH_SIZE (KB) is doubled (gfx950 reports half the bytes of wide coalesced reads,
+MI355X_MICROARCH.md HBM section); WRITE_SIZE (KB) is taken as is. Both are averaged over the
+kernel's dispatches, like the bench's achieved bytes per launch.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+root, key, pat = sys.argv[1:4]
+vals = defaultdict(list)
+for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        if pat in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"]) * 2 * 1024
+write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"]) * 1024
+out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+data = json.load(open(out)) if os.path.exists(out) else {}
+data[key] = {"kernel": pat, "hbm_bytes_per_launch": int(fetch + write), "read_bytes_per_launch": int(fetch),
+             "write_bytes_per_launch": int(write), "dispatches": len(vals["FETCH_SIZE"]),
+             "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {os.path.basename(root)}"}
+json.dump(data, open(out, "w"), indent=1, sort_keys=True)
+print(key, data[key])
