@@ -20,7 +20,8 @@ HIP_FLAGS  := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) $(FP_FLAGS) \
               -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero \
               -Iinclude -I$(PKG)/csrc -Wno-unused-result
 
-HOST_SRC := $(PKG)/host/xml_lite.cpp $(PKG)/host/scene_loader.cpp $(PKG)/host/bvh_build.cpp $(PKG)/host/image_io.cpp
+HOST_SRC := $(PKG)/host/xml_lite.cpp $(PKG)/host/scene_loader.cpp $(PKG)/host/bvh_build.cpp $(PKG)/host/image_io.cpp \
+            $(PKG)/host/png_decode.cpp
 HIP_SRC  := $(PKG)/csrc/nh_kernels.hip $(PKG)/csrc/nh_wavefront.hip $(PKG)/csrc/nh_api.hip
 HOST_OBJ := $(patsubst $(PKG)/host/%.cpp,$(OBJDIR)/host_%.o,$(HOST_SRC))
 HIP_OBJ  := $(patsubst $(PKG)/csrc/%.hip,$(OBJDIR)/hip_%.o,$(HIP_SRC))
@@ -44,12 +45,12 @@ $(OBJDIR)/hip_%.o: $(PKG)/csrc/%.hip $(HIP_DEPS)
 # product library: host ingestion + HIP kernels + C ABI
 $(LIB): $(HOST_OBJ) $(HIP_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -L/opt/rocm/lib -lrccl -lz -Wl,-rpath,/opt/rocm/lib
 
 # host-only subset (scene loader, BVH builder, image I/O): usable without a GPU runtime
 $(HOSTLIB): $(HOST_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(CXX) -shared -fPIC -pthread -o $@ $^
+	$(CXX) -shared -fPIC -pthread -o $@ $^ -lz
 
 $(CLI): $(PKG)/host/nori_hip_main.cpp $(LIB)
 	$(CXX) $(HOST_FLAGS) -o $@ $< -L$(LIBDIR) -lnori_hip -Wl,-rpath,'$$ORIGIN'

@@ -111,6 +111,21 @@ typedef struct nh_filter {
     float table[33];         /* NORI_FILTER_RESOLUTION + 1 entries, last = 0 */
 } nh_filter;
 
+/* EnvMap emitter (src/emitters/environmentmap.cpp) with its albedo texture: a png_texture
+ * (src/textures/PNGTexture.cpp, sRGB-decoded RGBA floats, PNG row 0 first) or the constant 0.5
+ * fallback as a 1x1 texture. */
+typedef struct nh_envmap {
+    int32_t width, height;        /* texture size (getWidth/getHeight); 1x1 for constant textures */
+    const float *rgba;            /* width*height*4 floats (PNGTexture::data) */
+    float radiance[3];            /* EnvMap radiance multiplier */
+    float scale_u, scale_v;       /* PNGTexture scaleU/scaleV */
+    float offset_u, offset_v;     /* PNGTexture offsetU/offsetV (non-spherical lookups) */
+    int32_t spherical;            /* PNGTexture sphericalTexture */
+    int32_t constant;             /* ConstantTexture: eval ignores uv */
+    const float *cdf;             /* EnvMap::calculateProbs DiscretePDF: width*height+1 CDF entries */
+    float normalization;          /* DiscretePDF::getNormalization() */
+} nh_envmap;
+
 typedef struct nh_scene_desc {
     nh_camera camera;
     nh_filter filter;
@@ -134,6 +149,7 @@ typedef struct nh_scene_desc {
     const uint32_t *F;            /* 3 per face, local to the owning shape */
     uint32_t n_area_cdf;
     const float *area_cdf;        /* concatenated per-mesh area CDFs */
+    nh_envmap env;                /* valid when envmap >= 0 */
 } nh_scene_desc;
 
 /* ---- BVH in the reference's own layout (include/nori/bvh.h:127-165) ---- */
@@ -235,6 +251,9 @@ void nh_bvh_free(nh_bvh *bvh);
 int nh_framebuffer_to_rgb(const float *rgbw, int32_t width, int32_t height, int32_t border, float *rgb);
 /* Bitmap::save equivalents: PFM (always available) and uncompressed OpenEXR */
 int nh_write_pfm(const char *path, const float *rgb, int32_t width, int32_t height);
+/* PNG decode as PNGTexture::loadFromFile's lodepng call (8-bit RGBA, row 0 first); rgba may be
+   NULL (or cap too small) to query the size */
+int nh_image_load_png(const char *path, uint8_t *rgba, size_t cap, int32_t *width, int32_t *height);
 int nh_write_exr(const char *path, const float *rgb, int32_t width, int32_t height);
 
 /* device side */

@@ -183,7 +183,12 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     if (d->camera.width <= 0 || d->camera.height <= 0) return fail(c, "invalid camera resolution"), NH_ERR_INVALID;
     if (d->camera.lens_radius > 1e-4f)
         return fail(c, "depth of field is not supported (reference uses a shared static sampler)"), NH_ERR_UNSUPPORTED;
-    if (d->envmap >= 0) return fail(c, "environment maps are not supported yet"), NH_ERR_UNSUPPORTED;
+    if (d->envmap >= 0) {
+        const nh_envmap &e = d->env;
+        if ((uint32_t)d->envmap >= d->n_emitters || d->emitters[d->envmap].type != NH_EMITTER_ENVMAP)
+            return fail(c, "envmap index does not name an envmap emitter"), NH_ERR_INVALID;
+        if (e.width <= 0 || e.height <= 0 || !e.rgba || !e.cdf) return fail(c, "invalid envmap texture"), NH_ERR_INVALID;
+    }
     free_all(c->scene_bufs);
     free_all(c->bvh_bufs);
     c->has_scene = c->has_bvh = false;
@@ -221,7 +226,8 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     std::vector<DEmitter> de(d->n_emitters);
     for (uint32_t i = 0; i < d->n_emitters; ++i) {
         const nh_emitter &e = d->emitters[i];
-        if (e.type == NH_EMITTER_ENVMAP) return fail(c, "environment maps are not supported yet"), NH_ERR_UNSUPPORTED;
+        if (e.type == NH_EMITTER_ENVMAP && (int32_t)i != d->envmap)
+            return fail(c, "only one environment map per scene is supported"), NH_ERR_UNSUPPORTED;
         DEmitter &o = de[i];
         std::memset(&o, 0, sizeof(o));
         o.type = e.type;
@@ -244,6 +250,27 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     if ((rc = upload(c, c->scene_bufs, d->BT, 3 * nv, &S.BT))) return rc;
     if ((rc = upload(c, c->scene_bufs, d->F, 3 * (size_t)d->n_faces, &S.F))) return rc;
     if ((rc = upload(c, c->scene_bufs, d->area_cdf, (size_t)d->n_area_cdf, &S.area_cdf))) return rc;
+    S.envmap = d->envmap;
+    if (d->envmap >= 0) {
+        const nh_envmap &e = d->env;
+        const size_t texels = (size_t)e.width * (size_t)e.height;
+        const float *rgba = nullptr;
+        if ((rc = upload(c, c->scene_bufs, e.rgba, 4 * texels, &rgba))) return rc;
+        S.env_rgba = reinterpret_cast<const float4 *>(rgba);
+        if ((rc = upload(c, c->scene_bufs, e.cdf, texels + 1, &S.env_cdf))) return rc;
+        S.env_w = e.width;
+        S.env_h = e.height;
+        S.env_spherical = e.spherical;
+        S.env_constant = e.constant;
+        S.env_norm = e.normalization;
+        S.env_su = e.scale_u;
+        S.env_sv = e.scale_v;
+        S.env_ou = e.offset_u;
+        S.env_ov = e.offset_v;
+        S.env_r = e.radiance[0];
+        S.env_g = e.radiance[1];
+        S.env_b = e.radiance[2];
+    }
     S.n_emitters = (int)d->n_emitters;
     S.integrator = d->integrator == NH_INTEGRATOR_PATH_MATS ? 1 : 0;
     std::memcpy(S.s2c, d->camera.sample_to_camera, sizeof(S.s2c));

@@ -123,7 +123,7 @@ NHD Rng path_rng(uint64_t seed, uint64_t pixel, uint64_t sample) {
 // ---- scene records -----------------------------------------------------------
 enum : int { SHAPE_MESH = 0, SHAPE_SPHERE = 1 };
 enum : int { BSDF_DIFFUSE = 0, BSDF_MIRROR = 1, BSDF_DIELECTRIC = 2, BSDF_MICROFACET = 3 };
-enum : int { EMITTER_AREA = 0, EMITTER_POINT = 1 };
+enum : int { EMITTER_AREA = 0, EMITTER_POINT = 1, EMITTER_ENVMAP = 2 };
 enum : int { M_UNKNOWN = 0, M_SOLID_ANGLE = 1, M_DISCRETE = 2 };
 
 struct alignas(16) DShape {
@@ -170,6 +170,13 @@ struct DScene {
     float filter_radius, lookup;
     int border;
     float table[33];
+    // EnvMap (environmentmap.cpp) and its albedo texture (PNGTexture.cpp / ConstantTexture)
+    int envmap;  // emitter index, or -1
+    const float4 *env_rgba;
+    const float *env_cdf;  // env_w * env_h + 1 entries
+    int env_w, env_h, env_spherical, env_constant;
+    float env_norm, env_su, env_sv, env_ou, env_ov;
+    float env_r, env_g, env_b;
 };
 
 NHD F3 ldv(const float *a, uint32_t i) { return f3(a[3 * i], a[3 * i + 1], a[3 * i + 2]); }

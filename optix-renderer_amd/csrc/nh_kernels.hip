@@ -46,7 +46,11 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
     Hit h;
     if (STATS) queries++;
     bool found = trace<DEPTH, ORDERED, false, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st);
-    while (found) {
+    for (;;) {
+        if (!found) {  // path_mis.cpp:32-44: escaped rays see the environment map, no MIS weight
+            if (S.envmap >= 0) li = add(li, mulc(t, env_eval(S, d)));
+            break;
+        }
         Its its;
         hit_info(S, tv, h, o, d, its);
         const DShape shape = S.shapes[its.shape];
@@ -147,7 +151,10 @@ __device__ F3 li_path_mats(const DScene &S, const Traversal &tv, Rng &rng, F3 o,
             if (STATS) queries++;
             found = closest<DEPTH, ORDERED, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st);
         }
-        if (!found) break;
+        if (!found) {  // path_mats.cpp:26-35
+            if (S.envmap >= 0) li = add(li, mulc(t, env_eval(S, d)));
+            break;
+        }
         Its its;
         hit_info(S, tv, h, o, d, its);
         const DShape shape = S.shapes[its.shape];

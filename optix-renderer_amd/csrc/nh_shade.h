@@ -58,8 +58,62 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
     }
 }
 
-// AreaEmitter / PointLight (src/emitters/arealight.cpp:58-125, pointlight.cpp:47-78)
+
+// ---- EnvMap (environmentmap.cpp:73-169) + PNGTexture::eval (PNGTexture.cpp:125-160) ------------
+// Nori's M_PI is a float constant (common.h:61), so all angle arithmetic is fp32.
+__device__ __forceinline__ F3 spherical_direction(float theta, float phi) {  // common.cpp:270-281
+    float st, ct, sp, cp;
+    f_sincos(theta, st, ct);
+    f_sincos(phi, sp, cp);
+    return f3(st * cp, st * sp, ct);
+}
+__device__ __forceinline__ void spherical_coordinates(F3 v, float &theta, float &phi) {  // common.cpp:283-291
+    theta = f_acos(v.z);
+    phi = f_atan2(v.y, v.x);
+    if (phi < 0) phi += 2 * kPi;
+}
+__device__ __forceinline__ F3 env_tex(const DScene &S, float u, float v) {
+    if (S.env_constant) {
+        const float4 c = S.env_rgba[0];
+        return f3(c.x, c.y, c.z);
+    }
+    if (S.env_spherical) {
+        F3 wi = spherical_direction(v * kPi, u * 2.f * kPi);
+        // Eigen rotation (identity for eulerAngles = 0) times wi, keeping the signed zeros it produces
+        wi = f3(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
+                0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+        float th, ph;
+        spherical_coordinates(wi, th, ph);
+        u = ph / (2.f * kPi);
+        v = th / kPi;
+    } else {
+        u += S.env_ou;
+        v += S.env_ov;
+    }
+    const unsigned W = (unsigned)S.env_w, H = (unsigned)S.env_h;
+    const float fu = u * S.env_su * (float)W, fv = v * S.env_sv * (float)H;
+    const unsigned w = fu > 0.f ? (unsigned)fu : 0u, hh = fv > 0.f ? (unsigned)fv : 0u;
+    const unsigned h = H - hh;
+    const float4 c = S.env_rgba[(h * W + w) % (W * H)];
+    return f3(c.x, c.y, c.z);
+}
+__device__ __forceinline__ F3 env_eval(const DScene &S, F3 wi) {  // EnvMap::eval
+    float th, ph;
+    spherical_coordinates(wi, th, ph);
+    const F3 c = env_tex(S, ph / (2.f * kPi), th / kPi);
+    return f3(c.x * S.env_r, c.y * S.env_g, c.z * S.env_b);
+}
+__device__ __forceinline__ float env_pdf(const DScene &S, F3 wi) {  // EnvMap::pdf
+    const float sphere_pdf = 0.25f / kPi;  // squareToUniformSpherePdf((1,0,0))
+    if (S.env_w == 1 && S.env_h == 1) return sphere_pdf;
+    const F3 c = env_eval(S, wi);
+    const float lum = c.x * 0.212671f + c.y * 0.715160f + c.z * 0.072169f;
+    return lum * S.env_norm / sphere_pdf * (float)(unsigned)S.env_h * (float)(unsigned)S.env_w;
+}
+
+// AreaEmitter / PointLight / EnvMap (src/emitters/arealight.cpp:58-125, pointlight.cpp:47-78)
 __device__ __forceinline__ float emitter_pdf(const DScene &S, const DEmitter &e, F3 ref, F3 p, F3 n, F3 wi) {
+    if (e.type == EMITTER_ENVMAP) return env_pdf(S, wi);
     if (e.type == EMITTER_POINT) return 1.f;
     if (dot(n, neg(wi)) < 0.f) return 0.f;
     const DShape sh = S.shapes[e.shape];
@@ -87,6 +141,24 @@ struct ESample {
 
 __device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e, F3 ref, float sx, float sy,
                                              ESample &es) {
+    if (e.type == EMITTER_ENVMAP) {  // EnvMap::sample (environmentmap.cpp:73-101)
+        const unsigned W = (unsigned)S.env_w, H = (unsigned)S.env_h;
+        const unsigned elem = (unsigned)dpdf_sample(S.env_cdf, (int)(W * H), sx);
+        const float i = (int)(elem / W) / (float)H, j = (int)(elem % W) / (float)W;
+        const F3 v = (W == 1 && H == 1) ? uniform_sphere(sx, sy) : spherical_direction(j * kPi, i * 2.0f * kPi);
+        es.p = f3(v.x * 1.f / kEps, v.y * 1.f / kEps, v.z * 1.f / kEps);
+        es.n = neg(v);
+        const F3 pr = sub(es.p, ref);
+        es.wi = normalized(pr);
+        es.so = es.p;
+        es.sd = neg(es.wi);
+        es.smint = kEps;
+        es.smaxt = f_sqrt(dot(pr, pr)) - kEps;
+        const float pdf = env_pdf(S, es.wi);
+        if (pdf < kEps) return f3(0, 0, 0);
+        const F3 ev = env_eval(S, es.wi);
+        return f3(ev.x / pdf, ev.y / pdf, ev.z / pdf);
+    }
     if (e.type == EMITTER_POINT) {
         F3 pos = f3(e.px, e.py, e.pz);
         F3 rp = sub(ref, pos);

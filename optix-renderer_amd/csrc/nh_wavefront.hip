@@ -188,7 +188,8 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
     bool alive = true;
     if (S.integrator == 1) {  // ---------------- path_mats (path_mats.cpp:16-78)
         if (!(flags & F_FIRST)) t = mulc(t, xyz(B.pend_col[s]));
-        if (!found) {
+        if (!found) {  // path_mats.cpp:26-35
+            if (S.envmap >= 0) li = add(li, mulc(t, env_eval(S, d)));
             alive = false;
         } else {
             hit_info(S, tv, h, org, d, its);
@@ -250,7 +251,8 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
             li = add(li, mulc(scl(w_ems, t), li_ems));
             t = mulc(t, bsdf_col);
         }
-        if (!found) {
+        if (!found) {  // path_mis.cpp:32-44: escaped rays see the environment map, no MIS weight
+            if (S.envmap >= 0) li = add(li, mulc(t, env_eval(S, d)));
             alive = false;
         } else {
             if (!have_its) hit_info(S, tv, h, org, d, its);

@@ -232,6 +232,8 @@ struct PropList {
         return p->v;
     }
     M4 get_transform(const std::string &n, const M4 &def) const { auto p = get(n, Prop::Transform); return p ? p->t : def; }
+    bool get_bool(const std::string &n, bool def) const { auto p = get(n, Prop::Bool); return p ? p->b : def; }
+    V3 get_vector(const std::string &n, V3 def) const { auto p = get(n, Prop::Vector); return p ? p->v : def; }
 };
 
 // ---------------------------------------------------------------------------
@@ -261,6 +263,8 @@ struct SceneData {
     std::vector<float> V, N, UV, T, BT;
     std::vector<uint32_t> F;
     std::vector<float> area_cdf;
+    nh_envmap env{};
+    std::vector<float> env_rgba, env_cdf;
     // camera parameters kept for re-projection on resize
     float fov = 30.f, near_clip = 1e-4f, far_clip = 1e4f, focal = 10.f, fstop = 0.f, lens = 0.f;
     M4 to_world = M4::identity();
@@ -674,6 +678,121 @@ nh_bsdf default_diffuse() {
     return b;
 }
 
+
+// ---------------------------------------------------------------------------
+// EnvMap + albedo texture (src/emitters/environmentmap.cpp, src/textures/PNGTexture.cpp,
+// src/textures/consttexture.cpp). M_PI is Nori's float constant (common.h:59-61), so every
+// angle expression is fp32; sincosf/acosf/atan2f/powf are evaluated in fp64 and rounded.
+// ---------------------------------------------------------------------------
+constexpr float kPiF = 3.14159265358979323846f;
+
+V3 spherical_direction(float theta, float phi) {  // common.cpp:270-281
+    const float st = (float)std::sin((double)theta), ct = (float)std::cos((double)theta);
+    const float sp = (float)std::sin((double)phi), cp = (float)std::cos((double)phi);
+    return v3(st * cp, st * sp, ct);
+}
+void spherical_coordinates(V3 v, float &theta, float &phi) {  // common.cpp:283-291
+    theta = (float)std::acos((double)v.z);
+    phi = (float)std::atan2((double)v.y, (double)v.x);
+    if (phi < 0) phi += 2 * kPiF;
+}
+float inverse_gamma(float x) {  // PNGTexture.cpp:442-447
+    if (x <= 0.04045f) return x * 1.f / 12.92f;
+    return (float)std::pow((double)((x + 0.055f) * 1.f / 1.055f), (double)2.4f);
+}
+
+// PNGTexture::eval (PNGTexture.cpp:125-160) / ConstantTexture::eval; eulerAngles = 0 only
+V3 env_tex_eval(const nh_envmap &e, const float *rgba, float u, float v) {
+    if (e.constant) return v3(rgba[0], rgba[1], rgba[2]);
+    if (e.spherical) {
+        V3 wi = spherical_direction(v * kPiF, u * 2.f * kPiF);
+        // rot * wi with rot = identity from the Euler-angle quaternions (fp32, signed zeros kept)
+        wi = v3(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
+                0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+        float th, ph;
+        spherical_coordinates(wi, th, ph);
+        u = ph / (2.f * kPiF);
+        v = th / kPiF;
+    } else {
+        u += e.offset_u;
+        v += e.offset_v;
+    }
+    const unsigned W = (unsigned)e.width, H = (unsigned)e.height;
+    const float fu = u * e.scale_u * (float)W, fv = v * e.scale_v * (float)H;
+    const unsigned w = fu > 0.f ? (unsigned)fu : 0u, hh = fv > 0.f ? (unsigned)fv : 0u;
+    const unsigned h = H - hh;
+    const unsigned index = (h * W + w) % (W * H);
+    return v3(rgba[4 * (size_t)index], rgba[4 * (size_t)index + 1], rgba[4 * (size_t)index + 2]);
+}
+
+void build_envmap(const Obj &o, const std::string &base_dir, SceneData &sd, nh_emitter &em) {
+    em.type = NH_EMITTER_ENVMAP;
+    V3 rad = o.props.get_color("radiance", v3(1, 1, 1));
+    em.radiance[0] = rad.x; em.radiance[1] = rad.y; em.radiance[2] = rad.z;
+    nh_envmap &e = sd.env;
+    e = nh_envmap{};
+    e.radiance[0] = rad.x; e.radiance[1] = rad.y; e.radiance[2] = rad.z;
+    e.scale_u = e.scale_v = 1.f;
+    const Obj *tex = nullptr;
+    for (auto &ch : o.children) {
+        if (ch->tag != "texture") throw SceneError("EnvMap::addChild(<" + ch->tag + ">) is not supported!");
+        if (ch->props.get_string("name", "") != "albedo")
+            throw SceneError("The name of this texture does not match any field!");
+        if (tex) throw SceneError("There is already an albedo defined!");
+        tex = ch.get();
+    }
+    if (!tex || tex->type == "constant_color") {  // EnvMap::cloneAndInit fallback: constant 0.5
+        V3 c = tex ? tex->props.get_color("value", v3(0, 0, 0)) : v3(0.5f, 0.5f, 0.5f);
+        e.width = e.height = 1;
+        e.constant = 1;
+        sd.env_rgba = {c.x, c.y, c.z, 1.f};
+    } else if (tex->type == "png_texture") {
+        const PropList &p = tex->props;
+        const std::string fn = join_path(base_dir, p.get_string("filename"));
+        if (!p.get_bool("sRGB", true)) throw SceneError("png_texture: normal-map (sRGB=false) lookups are not supported");
+        V3 eul = p.get_vector("eulerAngles", v3(0, 0, 0));
+        if (eul.x != 0 || eul.y != 0 || eul.z != 0) throw SceneError("png_texture: eulerAngles are not supported");
+        if (p.get_float("intensity", 1.f) != 1.f) { /* only used by normal maps */ }
+        e.scale_u = p.get_float("scaleU", 1.f);
+        e.scale_v = p.get_float("scaleV", 1.f);
+        e.offset_u = p.get_float("offsetU", 0.f);
+        e.offset_v = p.get_float("offsetV", 0.f);
+        e.spherical = p.get_bool("sphericalTexture", false) ? 1 : 0;
+        const auto dot = fn.find_last_of('.');
+        if (dot == std::string::npos || fn.substr(dot) != ".png")
+            throw SceneError("PNGTexture: file extension " + (dot == std::string::npos ? std::string() : fn.substr(dot)) +
+                             " unknown.");
+        std::vector<uint8_t> px;
+        unsigned w = 0, h = 0;
+        std::string err;
+        if (!png_decode_rgba8(fn, px, w, h, err)) throw SceneError("PNGTexture: " + err);
+        e.width = (int32_t)w;
+        e.height = (int32_t)h;
+        sd.env_rgba.resize(px.size());
+        for (size_t i = 0; i < px.size(); ++i) sd.env_rgba[i] = inverse_gamma(static_cast<float>(px[i]) / 255.f);
+    } else {
+        throw SceneError("texture \"" + tex->type + "\" is not supported for environment maps");
+    }
+    // EnvMap::calculateProbs (environmentmap.cpp:155-169): note the (row, col) -> (u, v) swap
+    const unsigned W = (unsigned)e.width, H = (unsigned)e.height;
+    sd.env_cdf.assign(1, 0.0f);
+    sd.env_cdf.reserve((size_t)W * H + 1);
+    for (unsigned i = 0; i < H; ++i)
+        for (unsigned j = 0; j < W; ++j) {
+            V3 c = env_tex_eval(e, sd.env_rgba.data(), i / (float)H, j / (float)W);
+            float lum = c.x * 0.212671f + c.y * 0.715160f + c.z * 0.072169f;
+            sd.env_cdf.push_back(sd.env_cdf.back() + std::fabs(lum));
+        }
+    const float sum = sd.env_cdf.back();
+    if (sum > 0) {
+        e.normalization = 1.0f / sum;
+        for (size_t i = 1; i < sd.env_cdf.size(); ++i) sd.env_cdf[i] *= e.normalization;
+        sd.env_cdf.back() = 1.0f;
+    } else {
+        e.normalization = 0.0f;
+    }
+}
+
 void build_scene(const Obj &scene, const std::string &base_dir, SceneData &sd) {
     bool have_camera = false, have_integrator = false, have_sampler = false;
     set_filter(sd.filter, 0, 2.0f, 0.5f, 1.0f / 3.0f, 1.0f / 3.0f);
@@ -782,6 +901,10 @@ void build_scene(const Obj &scene, const std::string &base_dir, SceneData &sd) {
                 // PointLight::update: m_radiance = m_power / (4 * M_PI)
                 float d = 4 * 3.14159265358979323846f;
                 em.radiance[0] = pw.x / d; em.radiance[1] = pw.y / d; em.radiance[2] = pw.z / d;
+            } else if (ch.type == "envmap") {
+                if (sd.envmap >= 0) throw SceneError("only one environment map per scene is supported");
+                build_envmap(ch, base_dir, sd, em);
+                sd.envmap = (int32_t)sd.emitters.size();
             } else {
                 throw SceneError("emitter \"" + ch.type + "\" is not supported yet");
             }
@@ -868,6 +991,11 @@ void fill_desc(const SceneData &sd, nh_scene_desc *d) {
     d->F = sd.F.data();
     d->n_area_cdf = (uint32_t)sd.area_cdf.size();
     d->area_cdf = sd.area_cdf.data();
+    if (sd.envmap >= 0) {
+        d->env = sd.env;
+        d->env.rgba = sd.env_rgba.data();
+        d->env.cdf = sd.env_cdf.data();
+    }
 }
 
 }  // namespace nh

@@ -66,13 +66,19 @@ class nh_filter(C.Structure):
     _fields_ = [("radius", _f), ("border", _i32), ("lookup_factor", _f), ("table", _f * 33)]
 
 
+class nh_envmap(C.Structure):
+    _fields_ = [("width", _i32), ("height", _i32), ("rgba", _fp), ("radiance", _f * 3), ("scale_u", _f),
+                ("scale_v", _f), ("offset_u", _f), ("offset_v", _f), ("spherical", _i32), ("constant", _i32),
+                ("cdf", _fp), ("normalization", _f)]
+
+
 class nh_scene_desc(C.Structure):
     _fields_ = [("camera", nh_camera), ("filter", nh_filter), ("integrator", _i32), ("sample_count", _i32),
                 ("n_shapes", _u32), ("shapes", C.POINTER(nh_shape)), ("n_bsdfs", _u32),
                 ("bsdfs", C.POINTER(nh_bsdf)), ("n_emitters", _u32), ("emitters", C.POINTER(nh_emitter)),
                 ("emitter_cdf", _fp), ("envmap", _i32), ("n_vertices", _u32), ("V", _fp), ("N", _fp),
                 ("UV", _fp), ("T", _fp), ("BT", _fp), ("n_faces", _u32), ("F", _u32p), ("n_area_cdf", _u32),
-                ("area_cdf", _fp)]
+                ("area_cdf", _fp), ("env", nh_envmap)]
 
 
 class nh_bvh_node(C.Structure):
@@ -135,6 +141,7 @@ _sig("nh_bvh_get_desc", _i32, _vp, C.POINTER(nh_bvh_desc))
 _sig("nh_bvh_free", None, _vp)
 _sig("nh_framebuffer_to_rgb", _i32, _fp, _i32, _i32, _i32, _fp)
 _sig("nh_write_pfm", _i32, C.c_char_p, _fp, _i32, _i32)
+_sig("nh_image_load_png", _i32, C.c_char_p, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(_i32), C.POINTER(_i32))
 _sig("nh_write_exr", _i32, C.c_char_p, _fp, _i32, _i32)
 _sig("nh_get_device_count", _i32, C.POINTER(C.c_int))
 _sig("nh_create", _i32, C.c_int, C.POINTER(_vp))
@@ -377,3 +384,13 @@ def write_exr(path: str, rgb: np.ndarray):
 def write_pfm(path: str, rgb: np.ndarray):
     rgb = np.ascontiguousarray(rgb, dtype=np.float32)
     _host_check(_lib.nh_write_pfm(path.encode(), _fptr(rgb), rgb.shape[1], rgb.shape[0]), "write_pfm")
+
+
+def load_png(path: str) -> np.ndarray:
+    """PNG -> (H, W, 4) uint8 through the library's decoder (nh_image_load_png)."""
+    w, h = _i32(), _i32()
+    _host_check(_lib.nh_image_load_png(path.encode(), None, 0, C.byref(w), C.byref(h)), "load_png")
+    out = np.zeros((h.value, w.value, 4), np.uint8)
+    _host_check(_lib.nh_image_load_png(path.encode(), out.ctypes.data_as(C.POINTER(C.c_uint8)), out.nbytes,
+                                       C.byref(w), C.byref(h)), "load_png")
+    return out

@@ -130,3 +130,133 @@ def test_references(xml_path: str) -> list[float]:
         if s.get("name") == "references":
             return [float(x) for x in s.get("value").replace(",", " ").split()]
     return []
+
+
+# ---------------------------------------------------------------------------------------
+# Environment-map scenes (C5's envmap). The reference's probe image
+# (scenes/project/res/rooitou_park.png) is not shipped to the GPU box, so the sky is a
+# deterministic synthetic PNG: a vertical gradient, a bright "sun" disc and a seeded noise
+# texture, written with every PNG scanline filter type so the decoder is exercised.
+
+def _png_filter_row(kind: int, row: np.ndarray, prev: np.ndarray, bpp: int) -> bytes:
+    r = row.astype(np.int32)
+    p = prev.astype(np.int32)
+    left = np.concatenate([np.zeros(bpp, np.int32), r[:-bpp]])
+    upleft = np.concatenate([np.zeros(bpp, np.int32), p[:-bpp]])
+    if kind == 0:
+        out = r
+    elif kind == 1:
+        out = r - left
+    elif kind == 2:
+        out = r - p
+    elif kind == 3:
+        out = r - ((left + p) >> 1)
+    else:
+        pa = np.abs(p - upleft)
+        pb = np.abs(left - upleft)
+        pc = np.abs(left + p - 2 * upleft)
+        pred = np.where((pa <= pb) & (pa <= pc), left, np.where(pb <= pc, p, upleft))
+        out = r - pred
+    return bytes([kind]) + (out & 0xFF).astype(np.uint8).tobytes()
+
+
+def write_png(path: str, img: np.ndarray) -> None:
+    """8-bit RGB (H, W, 3) or RGBA (H, W, 4) PNG; scanline filter type = row index mod 5."""
+    import struct
+    import zlib
+    h, w, ch = img.shape
+    ctype = {3: 2, 4: 6}[ch]
+    raw = bytearray()
+    prev = np.zeros(w * ch, np.uint8)
+    for y in range(h):
+        row = img[y].reshape(-1)
+        raw += _png_filter_row(y % 5, row, prev, ch)
+        prev = row
+
+    def chunk(tag: bytes, data: bytes) -> bytes:
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n")
+        f.write(chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, ctype, 0, 0, 0)))
+        f.write(chunk(b"IDAT", zlib.compress(bytes(raw), 6)))
+        f.write(chunk(b"IEND", b""))
+
+
+def sky_image(width: int, height: int, seed: int = 7) -> np.ndarray:
+    """Synthetic lat-long sky (rows = polar angle), uint8 RGB."""
+    rng = np.random.default_rng(seed)
+    v = (np.arange(height) + 0.5) / height
+    u = (np.arange(width) + 0.5) / width
+    V, U = np.meshgrid(v, u, indexing="ij")
+    sky = np.stack([0.35 + 0.4 * V, 0.5 + 0.3 * V, 0.9 - 0.2 * V], -1)
+    ground = np.stack([0.25 + 0 * V, 0.2 + 0 * V, 0.15 + 0 * V], -1)
+    img = np.where((V > 0.5)[..., None], ground, sky)
+    d2 = ((U - 0.3) * 2) ** 2 + (V - 0.25) ** 2
+    img = img + 4.0 * np.exp(-d2 / (2 * 0.02 ** 2))[..., None] * np.array([1.0, 0.9, 0.7])
+    img = img * (0.9 + 0.2 * rng.random((height, width, 1)))
+    return np.clip(img * 200, 0, 255).astype(np.uint8)
+
+
+def envmap_xml(out_dir: str, width: int = 64, height: int = 48, spp: int = 16, texture: str = "png",
+               tex_size=(96, 48), spherical: bool = True, area_light: bool = True, integrator: str = "path_mis",
+               mesh: str | None = None) -> str:
+    """Open scene lit by an envmap (+ optionally a small area light): a ground quad, a diffuse
+    and a microfacet sphere, a mirror sphere. texture: png | constant | none (EnvMap's 0.5
+    fallback). mesh: optional OBJ path added with a diffuse BSDF."""
+    os.makedirs(out_dir, exist_ok=True)
+    tex_xml = ""
+    if texture == "png":
+        png = os.path.join(out_dir, f"sky_{tex_size[0]}x{tex_size[1]}.png")
+        if not os.path.exists(png):
+            write_png(png, sky_image(*tex_size))
+        tex_xml = f"""<texture type="png_texture" name="albedo">
+      <string name="filename" value="{os.path.basename(png)}"/>
+      <boolean name="sphericalTexture" value="{'true' if spherical else 'false'}"/>
+    </texture>"""
+    elif texture == "constant":
+        tex_xml = '<texture type="constant_color" name="albedo"><color name="value" value="0.8 0.7 0.6"/></texture>'
+    quad = os.path.join(out_dir, "ground.obj")
+    with open(quad, "w") as f:
+        f.write("v -4 0 -4\nv 4 0 -4\nv 4 0 4\nv -4 0 4\nvt 0 0\nvt 1 0\nvt 1 1\nvt 0 1\nf 1/1 4/4 3/3 2/2\n")
+    light = ""
+    if area_light:
+        lq = os.path.join(out_dir, "lightquad.obj")
+        with open(lq, "w") as f:
+            f.write("v -0.3 2.5 -0.3\nv 0.3 2.5 -0.3\nv 0.3 2.5 0.3\nv -0.3 2.5 0.3\nf 1 2 3 4\n")
+        light = f"""<shape type="obj"><string name="filename" value="lightquad.obj"/>
+    <emitter type="area"><color name="radiance" value="6 6 6"/></emitter></shape>"""
+    extra = ""
+    if mesh:
+        extra = f"""<shape type="obj"><string name="filename" value="{os.path.relpath(mesh, out_dir)}"/>
+    <bsdf type="diffuse"><color name="albedo" value="0.6 0.6 0.6"/></bsdf></shape>"""
+    text = f"""<?xml version="1.0" encoding="utf-8"?>
+<scene>
+  <integrator type="{integrator}"/>
+  <sampler type="independent"><integer name="sampleCount" value="{spp}"/></sampler>
+  <camera type="perspective">
+    <transform name="toWorld"><lookat target="0, 0.4, 0" origin="0, 1.2, 3.2" up="0, 1, 0"/></transform>
+    <float name="fov" value="40"/>
+    <integer name="width" value="{width}"/><integer name="height" value="{height}"/>
+  </camera>
+  <emitter type="envmap">
+    <color name="radiance" value="1.5 1.5 1.5"/>
+    {tex_xml}
+  </emitter>
+  {light}
+  <shape type="obj"><string name="filename" value="ground.obj"/>
+    <bsdf type="diffuse"><color name="albedo" value="0.5 0.5 0.45"/></bsdf></shape>
+  <shape type="sphere"><point name="center" value="-0.7 0.4 0"/><float name="radius" value="0.4"/>
+    <bsdf type="diffuse"><color name="albedo" value="0.7 0.3 0.2"/></bsdf></shape>
+  <shape type="sphere"><point name="center" value="0.1 0.35 0.3"/><float name="radius" value="0.35"/>
+    <bsdf type="microfacet"><float name="alpha" value="0.15"/><color name="kd" value="0.2 0.3 0.5"/></bsdf></shape>
+  <shape type="sphere"><point name="center" value="0.8 0.3 -0.3"/><float name="radius" value="0.3"/>
+    <bsdf type="mirror"/></shape>
+  {extra}
+</scene>
+"""
+    key = repr((width, height, spp, texture, tex_size, spherical, area_light, integrator, mesh)).encode()
+    dst = os.path.join(out_dir, f"envmap_{hashlib.sha1(key).hexdigest()[:10]}.xml")
+    with open(dst, "w") as f:
+        f.write(text)
+    return dst

@@ -405,6 +405,10 @@ struct no_scene {
     std::vector<float> UV;
     std::vector<uint32_t> F;
     std::vector<float> area_cdf;
+    int envmap = -1;              // emitter index of the EnvMap, or -1
+    nh_envmap env{};              // scalar parameters (pointers below)
+    std::vector<float> env_rgba;  // PNGTexture::data
+    std::vector<float> env_cdf;   // EnvMap::calculateProbs, recomputed here (no_env_cdf)
     std::vector<uint32_t> shape_offset;
     std::vector<BNode> nodes;
     std::vector<uint32_t> indices;
@@ -605,6 +609,54 @@ inline ERec erec(V3 ref, V3 p, V3 n) {
     return r;
 }
 
+
+// ---- EnvMap (environmentmap.cpp:73-169) + PNGTexture::eval (PNGTexture.cpp:125-160) ----------
+// M_PI is Nori's float constant (common.h:61): every angle expression is fp32.
+V3 spherical_direction(float theta, float phi) {  // common.cpp:270-281 (sincosf)
+    float st = f_sin(theta), ct = f_cos(theta), sp = f_sin(phi), cp = f_cos(phi);
+    return mk(st * cp, st * sp, ct);
+}
+void spherical_coordinates(V3 v, float &theta, float &phi) {  // common.cpp:283-291
+    theta = f_acos(v.z);
+    phi = f_atan2(v.y, v.x);
+    if (phi < 0) phi += 2 * kPi;
+}
+V3 env_tex_eval(const no_scene &s, float u, float v) {
+    const float *d = s.env_rgba.data();
+    if (s.env.constant) return mk(d[0], d[1], d[2]);  // ConstantTexture::eval
+    if (s.env.spherical) {
+        V3 wi = spherical_direction(v * kPi, u * 2.f * kPi);
+        // Eigen rotation (identity for eulerAngles = 0) times wi, signed zeros as Eigen produces them
+        wi = mk(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
+                0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+        float th, ph;
+        spherical_coordinates(wi, th, ph);
+        u = ph / (2.f * kPi);
+        v = th / kPi;
+    } else {
+        u += s.env.offset_u;
+        v += s.env.offset_v;
+    }
+    const unsigned W = (unsigned)s.env.width, H = (unsigned)s.env.height;
+    const float fu = u * s.env.scale_u * (float)W, fv = v * s.env.scale_v * (float)H;
+    const unsigned w = fu > 0.f ? (unsigned)fu : 0u, hh = fv > 0.f ? (unsigned)fv : 0u;
+    const unsigned h = H - hh;
+    const unsigned index = (h * W + w) % (W * H);
+    return mk(d[4 * (size_t)index], d[4 * (size_t)index + 1], d[4 * (size_t)index + 2]);
+}
+V3 env_eval(const no_scene &s, V3 wi) {  // EnvMap::eval
+    float th, ph;
+    spherical_coordinates(wi, th, ph);
+    const float u = ph / (2.f * kPi), v = th / kPi;
+    return cmul(env_tex_eval(s, u, v), mk(s.env.radiance[0], s.env.radiance[1], s.env.radiance[2]));
+}
+float env_pdf(const no_scene &s, V3 wi) {  // EnvMap::pdf
+    const float sphere_pdf = 0.25f / kPi;  // squareToUniformSpherePdf((1,0,0))
+    if (s.env.width == 1 && s.env.height == 1) return sphere_pdf;
+    return luminance(env_eval(s, wi)) * s.env.normalization / sphere_pdf * (float)(unsigned)s.env.height *
+           (float)(unsigned)s.env.width;
+}
+
 size_t dpdf_sample(const float *cdf, size_t n_cdf, float x) {  // dpdf.h:124-130
     const float *e = std::lower_bound(cdf, cdf + n_cdf, x);
     size_t index = (size_t)std::max((ptrdiff_t)0, (e - cdf) - 1);
@@ -624,6 +676,7 @@ V3 emitter_eval(const no_scene &s, const nh_emitter &e, const ERec &r) {
     return mk(0, 0, 0);
 }
 float emitter_pdf(const no_scene &s, const nh_emitter &e, const ERec &r) {
+    if (e.type == NH_EMITTER_ENVMAP) return env_pdf(s, r.wi);
     if (e.type == NH_EMITTER_AREA) {  // arealight.cpp:107-125
         if (dot(r.n, -r.wi) < 0.f) return 0.f;
         float prob = s.shapes[e.shape].type == NH_SHAPE_MESH
@@ -634,6 +687,20 @@ float emitter_pdf(const no_scene &s, const nh_emitter &e, const ERec &r) {
     return 1.f;  // point light
 }
 V3 emitter_sample(const no_scene &s, const nh_emitter &e, ERec &r, float sx, float sy) {
+    if (e.type == NH_EMITTER_ENVMAP) {  // EnvMap::sample (environmentmap.cpp:73-101)
+        const unsigned W = (unsigned)s.env.width, H = (unsigned)s.env.height;
+        const size_t elem = dpdf_sample(s.env_cdf.data(), s.env_cdf.size(), sx);
+        const float i = (int)(elem / W) / (float)H, j = (int)(elem % W) / (float)W;
+        V3 v = (W == 1 && H == 1) ? square_to_uniform_sphere(sx, sy) : spherical_direction(j * kPi, i * 2.0f * kPi);
+        V3 v_inf = mk(v.x * 1.f / kEps, v.y * 1.f / kEps, v.z * 1.f / kEps);
+        r.n = -v;
+        r.p = v_inf;
+        r.wi = normalized(r.p - r.ref);
+        r.shadow = make_ray(r.p, -r.wi, kEps, norm(r.p - r.ref) - kEps);
+        r.pdf = env_pdf(s, r.wi);
+        if (r.pdf < kEps) return mk(0, 0, 0);
+        return env_eval(s, r.wi) / r.pdf;
+    }
     if (e.type == NH_EMITTER_POINT) {  // pointlight.cpp:47-66
         V3 pos = mk(e.position[0], e.position[1], e.position[2]);
         r.shadow = make_ray(pos, normalized(r.ref - pos), kEps, norm(r.ref - pos) - kEps);
@@ -682,7 +749,7 @@ V3 li_path_mis(const no_scene &s, Sampler &smp, const Ray &ray) {  // path_mis.c
         float pdfems = 0.f, pdfmat = 0.f, pdfems_mats = 0.f, pdfmat_ems = 0.f;
         Its its;
         if (!bvh_intersect(s, trace, its, false)) {
-            // environment maps are not supported by the loader yet (no envmap -> nothing added)
+            if (s.envmap >= 0) li = li + cmul(t, env_eval(s, trace.d));  // path_mis.cpp:32-43
             break;
         }
         const nh_shape &shape = s.shapes[its.shape];
@@ -756,7 +823,10 @@ V3 li_path_mats(const no_scene &s, Sampler &smp, const Ray &ray) {  // path_mats
     int counter = 0;
     while (true) {
         Its its;
-        if (!bvh_intersect(s, trace, its, false)) break;
+        if (!bvh_intersect(s, trace, its, false)) {
+            if (s.envmap >= 0) li = li + cmul(t, env_eval(s, trace.d));  // path_mats.cpp:26-35
+            break;
+        }
         const nh_shape &shape = s.shapes[its.shape];
         const nh_bsdf &bsdf = s.bsdfs[shape.bsdf];
         if (shape.emitter >= 0) {
@@ -877,6 +947,14 @@ std::vector<std::pair<int, int>> spiral_blocks(int w, int h, int bs) {
 
 extern "C" {
 
+int no_env_cdf(const no_scene *s, const float **cdf, uint32_t *n, float *normalization) {
+    if (!s || s->envmap < 0) return NH_ERR_INVALID;
+    *cdf = s->env_cdf.data();
+    *n = (uint32_t)s->env_cdf.size();
+    *normalization = s->env.normalization;
+    return NH_OK;
+}
+
 int no_scene_create(const nh_scene_desc *d, no_scene **out) {
     if (!d || !out) return NH_ERR_INVALID;
     auto s = std::make_unique<no_scene>();
@@ -896,6 +974,28 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
     s->UV.assign(d->UV, d->UV + 2 * (size_t)d->n_vertices);
     s->F.assign(d->F, d->F + 3 * (size_t)d->n_faces);
     s->area_cdf.assign(d->area_cdf, d->area_cdf + d->n_area_cdf);
+    s->envmap = d->envmap;
+    if (d->envmap >= 0) {
+        s->env = d->env;
+        s->env_rgba.assign(d->env.rgba, d->env.rgba + 4 * (size_t)d->env.width * d->env.height);
+        s->env.rgba = nullptr;
+        s->env.cdf = nullptr;
+        // EnvMap::calculateProbs (environmentmap.cpp:155-169) + DiscretePDF append/normalize
+        // (dpdf.h:48-115), restated: texture evaluated at (row / H, col / W)
+        const unsigned W = (unsigned)d->env.width, H = (unsigned)d->env.height;
+        s->env_cdf.assign(1, 0.0f);
+        for (unsigned i = 0; i < H; ++i)
+            for (unsigned j = 0; j < W; ++j)
+                s->env_cdf.push_back(s->env_cdf.back() + std::fabs(luminance(env_tex_eval(*s, i / (float)H, j / (float)W))));
+        const float sum = s->env_cdf.back();
+        if (sum > 0) {
+            s->env.normalization = 1.0f / sum;
+            for (size_t i = 1; i < s->env_cdf.size(); ++i) s->env_cdf[i] *= s->env.normalization;
+            s->env_cdf.back() = 1.0f;
+        } else {
+            s->env.normalization = 0.0f;
+        }
+    }
 
     // ---- BVH::addShape / BVH::build, serial restatement (bvh.cpp:236-380) ----
     s->shape_offset.push_back(0u);

@@ -35,6 +35,8 @@ int no_scene_create(const nh_scene_desc *desc, no_scene **out);
 void no_scene_free(no_scene *s);
 /* export the oracle's BVH (reference layout) for comparison with the product builder */
 int no_bvh_info(const no_scene *s, uint32_t *n_nodes, uint32_t *n_indices);
+/* the oracle's own EnvMap::calculateProbs CDF (W*H+1 entries) and normalization */
+int no_env_cdf(const no_scene *s, const float **cdf, uint32_t *n, float *normalization);
 int no_bvh_export(const no_scene *s, nh_bvh_node *nodes, uint32_t *indices);
 
 /* BVH::rayIntersect over a ray batch (closest or any hit) */

@@ -36,6 +36,7 @@ def _sig(name, res, *args):
 _sig("no_scene_create", _i32, C.POINTER(nh.nh_scene_desc), C.POINTER(_vp))
 _sig("no_scene_free", None, _vp)
 _sig("no_bvh_info", _i32, _vp, C.POINTER(_u32), C.POINTER(_u32))
+_sig("no_env_cdf", _i32, _vp, C.POINTER(_fp), C.POINTER(_u32), C.POINTER(C.c_float))
 _sig("no_bvh_export", _i32, _vp, C.POINTER(nh.nh_bvh_node), C.POINTER(_u32))
 _sig("no_trace_rays", _i32, _vp, C.POINTER(nh.nh_ray_soa), _i32, _i32, C.POINTER(nh.nh_hit_soa))
 _sig("no_pcg32_seed", None, _u64p, _u64p, _u64, _u64)
@@ -101,6 +102,13 @@ class OracleScene:
         _lib.no_bvh_export(self._h, nodes, idx.ctypes.data_as(C.POINTER(_u32)))
         raw = np.ctypeslib.as_array(C.cast(nodes, C.POINTER(C.c_uint32)), shape=(max(nn.value, 1) * 8,))
         return raw.reshape(-1, 8)[: nn.value].copy(), idx
+
+    def env_cdf(self):
+        """The oracle's own EnvMap::calculateProbs CDF and normalization (None without an envmap)."""
+        p, n, norm = _fp(), _u32(), C.c_float()
+        if _lib.no_env_cdf(self._h, C.byref(p), C.byref(n), C.byref(norm)) != 0:
+            return None
+        return np.ctypeslib.as_array(p, shape=(n.value,)).copy(), norm.value
 
     def trace(self, o, d, mint, maxt, any_hit=False):
         n = len(o)

@@ -195,3 +195,17 @@ def test_wavefront_matches_megakernel(gpu, tmp_path, monkeypatch):
                blocks=[0, 2, 3, 5, 7, 8, 11])
     np.testing.assert_array_equal(out[0][0], ctx.framebuffer())
     assert ctx.stats()["launches_splat"] > 1
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("texture,integrator", [("png", nh.INTEGRATOR_PATH_MIS), ("png", nh.INTEGRATOR_PATH_MATS),
+                                                ("constant", nh.INTEGRATOR_PATH_MIS),
+                                                ("none", nh.INTEGRATOR_PATH_MIS)])
+def test_render_parity_envmap(gpu, tmp_path, texture, integrator, mode):
+    """EnvMap emitter (NEE by luminance CDF, escaped-ray term) + png_texture lookups, GPU vs oracle."""
+    xml = scenegen.envmap_xml(str(tmp_path), texture=texture, tex_size=(96, 48))
+    g, r, s = render_pair(xml, 64, 48, 8, integrator=integrator, mode=mode, traversal=nh.TRAVERSAL_ORDERED)
+    e = rel_l2(g, r)
+    print(f"envmap {texture} integrator={integrator} mode={mode}: rel-L2 {e:.3e}, max|d| {np.abs(g - r).max():.3e}")
+    assert e < TOL_REL_L2
+    assert nh.to_rgb(r, s.border).mean() > 0.05
