@@ -489,7 +489,7 @@ static int ensure_wf(nh_ctx *c, size_t n) {
              alloc(B.li, nq) && alloc(B.thr, nq) && alloc(B.pend_ems, nq) && alloc(B.pend_col, nq) &&
              alloc(B.pdfmat, nq) && alloc(B.flags, nq) && alloc(B.pid, nq) && alloc(B.occl, nq);
     ok = ok && alloc(W.sh_o, nq) && alloc(W.sh_d, nq) && alloc(W.sh_slot, nq) &&
-         alloc(W.counts, 2 * kQueueShards * kCountStride);
+         alloc(W.counts, 4 * kQueueShards * kCountStride);
     if (!ok) {
         free_all(c->wf_bufs);
         c->wf = WfState{};
@@ -536,10 +536,12 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         L.pre_ext[s] = s == 0 ? 0 : L.n_ext;  // generate wrote a dense queue
         L.pre_sh[s] = 0;
     }
+    // [0, 2) x 8 shards: shade's append counters (read back); [2, 4) x 8: the persistent
+    // extend / any-hit kernels' fetch counters
     const size_t count_bytes = 2 * kQueueShards * kCountStride * sizeof(unsigned);
     bool first = true;
     while (L.n_ext > 0) {
-        HIP_TRY(c, hipMemsetAsync(c->wf.counts, 0, count_bytes, c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->wf.counts, 0, 2 * count_bytes, c->stream));
         HIP_TRY(c, hipEventRecord(ev[0], c->stream));
         nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[1], c->stream));

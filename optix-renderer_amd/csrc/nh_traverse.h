@@ -216,4 +216,126 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
     return ANY ? false : found;
 }
 
+
+// Resumable form of trace(): identical visits, box/primitive tests and order (hence identical
+// results and counters), but one unit of work per step() -- one inner node, one primitive, or
+// one stack pop -- so a persistent wave can hand finished lanes new rays between steps instead
+// of idling until its slowest lane is done (nh_wavefront.hip wf_trace_pt).
+template <bool ORDERED, bool ANY, bool STATS>
+struct Tracer {
+    F3 o, d, r;
+    float mint, maxt;
+    int cur;      // inner node to visit next, or -1
+    int k, kend;  // primitive range of the leaf under test
+    int sp;
+    bool found, done;
+    Hit best;
+
+    NHD void begin(const DScene &S, const Traversal &tv, F3 o_, F3 d_, float mint_, float maxt_, TravStats &st) {
+        o = o_;
+        d = d_;
+        mint = mint_;
+        maxt = maxt_;
+        // adaptive ray epsilon (bvh.cpp:407-410)
+        if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));
+        best.k = -1;
+        best.t = INFINITY;
+        found = false;
+        done = true;
+        sp = 0;
+        cur = -1;
+        k = kend = 0;
+        if (S.root_kind == 0 || maxt < mint) return;
+        r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        float near_t;
+        if (STATS) st.boxes++;
+        if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d,
+                      r, mint, maxt, near_t))
+            return;
+        done = false;
+        if (S.root_kind == 2) {
+            const int2 lf = tv.leaves[0];
+            k = lf.x;
+            kend = lf.x + lf.y;
+        } else {
+            cur = 0;
+        }
+    }
+
+    NHD void step(const Traversal &tv, uint32_t *stk, int stride, TravStats &st) {
+        if (k < kend) {  // one primitive of the current leaf
+            const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
+            if (STATS) st.prims++;
+            float t, u = 0.f, v = 0.f;
+            const bool hit = (__float_as_int(c.w) == 0) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
+                                                        : sphere_test(a, o, d, mint, maxt, t);
+            if (hit) {
+                if (ANY) {
+                    found = true;
+                    done = true;
+                    return;
+                }
+                if (t < maxt || k > best.k) {
+                    found = true;
+                    maxt = t;
+                    best.t = t;
+                    best.u = u;
+                    best.v = v;
+                    best.k = k;
+                }
+            }
+            ++k;
+            return;
+        }
+        if (cur >= 0) {  // one inner node: test both child boxes
+            const float4 n0 = tv.nodes[4 * cur], n1 = tv.nodes[4 * cur + 1], n2 = tv.nodes[4 * cur + 2];
+            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * cur + 3]);
+            if (STATS) { st.nodes++; st.boxes += 2; }
+            float nl, nr;
+            const bool hl = box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, nl);
+            const bool hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
+            int next;
+            if (hl && hr) {
+                const bool right_first = ORDERED && nr < nl;
+                stk[sp * stride] = ((uint32_t)cur << 1) | (right_first ? 0u : 1u);
+                ++sp;
+                next = right_first ? n3.y : n3.x;
+            } else if (hl) {
+                next = n3.x;
+            } else if (hr) {
+                next = n3.y;
+            } else {
+                cur = -1;
+                return;
+            }
+            enter(tv, next);
+            return;
+        }
+        if (sp > 0) {  // one deferred child: re-test its box against the current maxt
+            --sp;
+            const uint32_t e = stk[sp * stride];
+            const int parent = (int)(e >> 1), side = (int)(e & 1u);
+            const float4 n0 = tv.nodes[4 * parent], n1 = tv.nodes[4 * parent + 1], n2 = tv.nodes[4 * parent + 2];
+            if (STATS) st.boxes++;
+            float near_t;
+            if (!child_box_test(n0, n1, n2, side, o, d, r, mint, maxt, near_t)) return;
+            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * parent + 3]);
+            enter(tv, side ? n3.y : n3.x);
+            return;
+        }
+        done = true;
+    }
+
+    NHD void enter(const Traversal &tv, int ref) {
+        if (ref >= 0) {
+            cur = ref;
+        } else {
+            const int2 lf = tv.leaves[~ref];
+            k = lf.x;
+            kend = lf.x + lf.y;
+            cur = -1;
+        }
+    }
+};
+
 }  // namespace nhd

@@ -28,6 +28,7 @@
 #include "nh_internal.h"
 #include "nh_shade.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 using namespace nhd;
@@ -157,6 +158,89 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
             unsigned long long x = v[j];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
             if ((threadIdx.x & 63) == 0) atomicAdd(&L.counters[8 + j], x);
+        }
+    }
+}
+
+
+// Persistent traversal: a fixed grid of waves pulls rays in batches of kFetchBatch from eight
+// fetch segments (segment f = [f*n/8, (f+1)*n/8) of the dense queue index; a wave starts on the
+// segment of its XCD, blockIdx % 8, and moves on when it runs dry), and refills every lane whose
+// traversal finished before the next Tracer step. A wave thus stays busy until the pool is empty
+// instead of waiting for its slowest ray (the 64-lane divergence that made one wave execute
+// ~10x the instructions of an average ray on the 1M-triangle scene).
+constexpr int kFetchBatch = 64;
+template <int DEPTH, bool ORDERED, bool ANY, bool STATS>
+__global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+    __shared__ uint32_t stk[DEPTH * 128];
+    const DScene &S = *Sp;
+    const int n = ANY ? L.n_sh : L.n_ext;
+    const int *pre = ANY ? L.pre_sh : L.pre_ext;
+    unsigned *fetch = L.st.counts + (ANY ? 3 : 2) * kQueueShards * kCountStride;
+    const WfBuf &B = L.st.buf[L.in_q];
+    const int lane = threadIdx.x & 63;
+    uint32_t *my_stk = stk + threadIdx.x;
+    int seg = blockIdx.x & (kQueueShards - 1), tried = 0;
+    int batch_next = 0, batch_end = 0;  // wave-uniform
+    int slot = -1;                      // this lane's ray (queue slot), -1 = idle
+    Tracer<ORDERED, ANY, STATS> tr;
+    TravStats st{0, 0, 0};
+    unsigned long long queries = 0;
+    for (;;) {
+        const bool idle = slot < 0;
+        const unsigned long long im = __ballot(idle);
+        if (im) {
+            while (batch_next >= batch_end && tried < kQueueShards) {  // wave-uniform refill
+                const int lo = (int)((long long)seg * n / kQueueShards);
+                const int hi = (int)((long long)(seg + 1) * n / kQueueShards);
+                unsigned base = 0;
+                if (lane == 0) base = atomicAdd(&fetch[seg * kCountStride], (unsigned)kFetchBatch);
+                base = __shfl(base, 0, 64);
+                if ((long long)lo + base < hi) {
+                    batch_next = lo + (int)base;
+                    batch_end = min(batch_next + kFetchBatch, hi);
+                } else {
+                    seg = (seg + 1) & (kQueueShards - 1);
+                    ++tried;
+                }
+            }
+            const int rank = __popcll(im & ((1ull << lane) - 1ull));
+            if (idle && batch_next + rank < batch_end) {
+                const int q = batch_next + rank;
+                slot = queue_slot(pre, L.seg_cap, q);
+                float4 ro, rd;
+                if (ANY) {
+                    ro = L.st.sh_o[slot];
+                    rd = L.st.sh_d[slot];
+                } else {
+                    ro = B.ray_o[slot];
+                    rd = B.ray_d[slot];
+                }
+                // a zero BSDF direction (maxt = -inf) misses every primitive without a traversal
+                if (STATS && (ANY || rd.w >= ro.w)) ++queries;
+                tr.begin(S, tv, xyz(ro), xyz(rd), ro.w, rd.w, st);
+            }
+            batch_next = min(batch_next + __popcll(im), batch_end);
+        }
+        if (!__any(slot >= 0)) break;
+        if (slot >= 0) {
+            if (!tr.done) tr.step(tv, my_stk, 128, st);
+            if (tr.done) {
+                if (ANY) {
+                    B.occl[L.st.sh_slot[slot]] = tr.found ? 1 : 0;
+                } else {
+                    B.hit[slot] = make_float4(tr.best.t, tr.best.u, tr.best.v, __int_as_float(tr.found ? tr.best.k : -1));
+                }
+                slot = -1;
+            }
+        }
+    }
+    if (STATS) {
+        unsigned long long v[4] = {queries, st.nodes, st.boxes, st.prims};
+        for (int j = 0; j < 4; ++j) {
+            unsigned long long x = v[j];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            if (lane == 0) atomicAdd(&L.counters[(ANY ? 8 : 0) + j], x);
         }
     }
 }
@@ -354,11 +438,34 @@ __global__ __launch_bounds__(256, 4) void wf_shade(const DScene *__restrict__ Sp
 
 namespace nh {
 
+static bool persistent_traversal() {
+    static const bool on = [] {
+        const char *e = std::getenv("NH_PERSISTENT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <int DEPTH>
 static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                               bool shadow, hipStream_t st) {
     const int n = shadow ? L.n_sh : L.n_ext;
     if (n <= 0) return;
+    if (persistent_traversal()) {
+        // enough resident waves to fill the chip (LDS-limited at DEPTH 32: 10 workgroups per CU)
+        const int blocks = std::min((n + 127) / 128, 256 * 8);
+        const dim3 grid(blocks);
+#define NH_PT(A, O, T) hipLaunchKernelGGL((wf_trace_pt<DEPTH, O, A, T>), grid, dim3(128), 0, st, S, tv, L)
+        if (shadow) {
+            if (ordered) { if (stats) NH_PT(true, true, true); else NH_PT(true, true, false); }
+            else { if (stats) NH_PT(true, false, true); else NH_PT(true, false, false); }
+        } else {
+            if (ordered) { if (stats) NH_PT(false, true, true); else NH_PT(false, true, false); }
+            else { if (stats) NH_PT(false, false, true); else NH_PT(false, false, false); }
+        }
+#undef NH_PT
+        return;
+    }
     dim3 grid((n + 127) / 128);
 #define NH_WF(K, O, T) hipLaunchKernelGGL((K<DEPTH, O, T>), grid, dim3(128), 0, st, S, tv, L)
     if (shadow) {
