@@ -61,7 +61,9 @@ struct nh_ctx {
     WfState wf{};
     std::vector<void *> wf_bufs;
     size_t wf_cap = 0;
-    unsigned *h_counts = nullptr;  // pinned host mirror of wf.counts
+    unsigned *h_counts = nullptr;  // pinned: kRing bounce-count copies + one initial count slot
+    std::vector<hipEvent_t> wf_events;  // 4 per bounce, reused across chunks
+    hipEvent_t wf_copy_ev[4] = {};
 };
 
 namespace {
@@ -172,6 +174,9 @@ void nh_destroy(nh_ctx *c) {
     (void)hipFree(c->d_scene);
     free_all(c->wf_bufs);
     if (c->h_counts) (void)hipHostFree(c->h_counts);
+    for (hipEvent_t e : c->wf_events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->wf_copy_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -466,6 +471,7 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
 }
 
 
+constexpr int kRing = 4;  // bounce-count copies in flight
 constexpr size_t kWfBytesPerPath = 2 * (16 * 7 + 8 + 4 + 4 + 4 + 1) + 36;  // two buffers + shadow queue
 
 static int ensure_wf(nh_ctx *c, size_t n) {
@@ -489,21 +495,27 @@ static int ensure_wf(nh_ctx *c, size_t n) {
              alloc(B.li, nq) && alloc(B.thr, nq) && alloc(B.pend_ems, nq) && alloc(B.pend_col, nq) &&
              alloc(B.pdfmat, nq) && alloc(B.flags, nq) && alloc(B.pid, nq) && alloc(B.occl, nq);
     ok = ok && alloc(W.sh_o, nq) && alloc(W.sh_d, nq) && alloc(W.sh_slot, nq) &&
-         alloc(W.counts, 4 * kQueueShards * kCountStride);
+         alloc(W.counts, 2 * kCountSlot);
     if (!ok) {
         free_all(c->wf_bufs);
         c->wf = WfState{};
         return fail(c, "hipMalloc failed for wavefront path state"), NH_ERR_DEVICE;
     }
-    if (!c->h_counts && hipHostMalloc(reinterpret_cast<void **>(&c->h_counts), 2 * kQueueShards * kCountStride * sizeof(unsigned)) != hipSuccess)
-        return fail(c, "hipHostMalloc failed"), NH_ERR_DEVICE;
+    if (!c->h_counts) {
+        if (hipHostMalloc(reinterpret_cast<void **>(&c->h_counts),
+                          (kRing * 2 * kCountGroup + kCountSlot) * sizeof(unsigned)) != hipSuccess)
+            return fail(c, "hipHostMalloc failed"), NH_ERR_DEVICE;
+        for (hipEvent_t &e : c->wf_copy_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     c->wf_cap = n;
     return NH_OK;
 }
 
-// One chunk of rounds through generate -> {extend, shadow} -> shade until no path is alive.
-// The live counts come back through pinned memory once per bounce (the host needs them to size
-// the next grids); the kernel times are summed per stage.
+// One chunk of rounds through generate -> {extend, any-hit, shade} per bounce until no path is
+// alive. Queue lengths stay on the device (nh_internal.h count slots); the host enqueues bounce
+// i+1 before it waits for bounce i's counts (2 KB into pinned memory), so the GPU never idles
+// on a host round trip and exactly one empty bounce is enqueued at the end. Kernel times come
+// from per-launch events read once the chunk has finished.
 static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch &P) {
     WfLaunch L{};
     L.st = c->wf;
@@ -516,79 +528,91 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     L.rec_jy = P.rec_jy;
     L.counters = P.counters;
     const bool ordered = q->traversal == NH_TRAVERSAL_ORDERED, stats = q->collect_stats != 0;
-    hipEvent_t ev[4];
-    for (auto &e : ev) HIP_TRY(c, hipEventCreate(&e));
-    struct Guard {
-        hipEvent_t *e;
-        ~Guard() {
-            for (int i = 0; i < 4; ++i) (void)hipEventDestroy(e[i]);
-        }
-    } guard{ev};
+    const int per_chunk = 256;  // wf_shade's chunk
+    const int max_chunks = (P.n_paths + per_chunk - 1) / per_chunk;
+    L.seg_cap = (max_chunks + kQueueShards - 1) / kQueueShards * per_chunk;
+    // persistent traversal pays off on deep BVHs (long, divergent traversals); cbox-like scenes
+    // traverse faster with one ray per lane
+    bool persistent = c->depth > 20;
+    if (const char *e = std::getenv("NH_PERSISTENT")) persistent = e[0] == '1';
+    unsigned *slot[2] = {c->wf.counts, c->wf.counts + kCountSlot};
+    // bounce 0 reads the dense queue written by generate: shard 0 holds all n_paths
+    unsigned *h_init = c->h_counts + kRing * 2 * kCountGroup;
+    std::memset(h_init, 0, kCountSlot * sizeof(unsigned));
+    h_init[0] = (unsigned)P.n_paths;
+    HIP_TRY(c, hipMemcpyAsync(slot[0], h_init, kCountSlot * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
     nh::launch_wf_generate(c->d_scene, L, c->stream);  // timed with the whole chunk (kernel_ms_path)
     HIP_TRY(c, hipGetLastError());
-    L.n_ext = P.n_paths;
-    L.n_sh = 0;
-    L.in_q = 0;
-    const int per_block = 256;
-    const int max_blocks = (P.n_paths + per_block - 1) / per_block;
-    L.seg_cap = (max_blocks + kQueueShards - 1) / kQueueShards * per_block;
-    for (int s = 0; s <= kQueueShards; ++s) {
-        L.pre_ext[s] = s == 0 ? 0 : L.n_ext;  // generate wrote a dense queue
-        L.pre_sh[s] = 0;
-    }
-    // [0, 2) x 8 shards: shade's append counters (read back); [2, 4) x 8: the persistent
-    // extend / any-hit kernels' fetch counters
-    const size_t count_bytes = 2 * kQueueShards * kCountStride * sizeof(unsigned);
-    bool first = true;
-    while (L.n_ext > 0) {
-        HIP_TRY(c, hipMemsetAsync(c->wf.counts, 0, 2 * count_bytes, c->stream));
+    const size_t append_bytes = 2 * kCountGroup * sizeof(unsigned);
+    // per-bounce totals: in_e / in_s = live paths / shadow rays entering the bounce
+    std::vector<uint64_t> in_e{(uint64_t)P.n_paths}, in_s{0};
+    int it = 0;
+    for (;; ++it) {
+        const int in = it & 1;
+        L.in_q = in;
+        L.cnt_in = slot[in];
+        L.cnt_out = slot[in ^ 1];
+        if ((size_t)(it + 1) * 4 > c->wf_events.size()) {
+            for (int k = 0; k < 64; ++k) {
+                hipEvent_t e;
+                HIP_TRY(c, hipEventCreate(&e));
+                c->wf_events.push_back(e);
+            }
+        }
+        hipEvent_t *ev = &c->wf_events[(size_t)it * 4];
+        HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), c->stream));
         HIP_TRY(c, hipEventRecord(ev[0], c->stream));
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, c->depth, c->stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, persistent, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[1], c->stream));
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, c->depth, c->stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, persistent, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[2], c->stream));
         nh::launch_wf_shade(c->d_scene, c->tv, L, c->stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], c->stream));
-        HIP_TRY(c, hipMemcpyAsync(c->h_counts, c->wf.counts, count_bytes, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        float a = 0.f, b = 0.f, d = 0.f;
-        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
-        (void)hipEventElapsedTime(&b, ev[1], ev[2]);
-        (void)hipEventElapsedTime(&d, ev[2], ev[3]);
-        c->stats.kernel_ms_extend += a;
-        c->stats.launches_extend++;
-        if (L.n_sh > 0) {
-            c->stats.kernel_ms_shadow += b;
-            c->stats.launches_shadow++;
-        }
-        c->stats.kernel_ms_shade += d;
-        c->stats.launches_shade++;
-        size_t ne = 0, ns = 0;
+        unsigned *h = c->h_counts + (size_t)(it % kRing) * 2 * kCountGroup;
+        HIP_TRY(c, hipMemcpyAsync(h, slot[in ^ 1], append_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipEventRecord(c->wf_copy_ev[it % kRing], c->stream));
+        if (it == 0) continue;
+        // counts of bounce it-1 (its copy was enqueued before bounce it, which keeps the GPU busy)
+        HIP_TRY(c, hipEventSynchronize(c->wf_copy_ev[(it - 1) % kRing]));
+        const unsigned *hp = c->h_counts + (size_t)((it - 1) % kRing) * 2 * kCountGroup;
+        uint64_t ne = 0, ns = 0;
         for (int s = 0; s < kQueueShards; ++s) {
-            const unsigned ce = c->h_counts[s * kCountStride], cs = c->h_counts[(kQueueShards + s) * kCountStride];
+            const unsigned ce = hp[s * kCountStride], cs = hp[kCountGroup + s * kCountStride];
             if (ce > (unsigned)L.seg_cap || cs > ce) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
-            L.pre_ext[s] = (int)ne;
-            L.pre_sh[s] = (int)ns;
             ne += ce;
             ns += cs;
         }
-        L.pre_ext[kQueueShards] = (int)ne;
-        L.pre_sh[kQueueShards] = (int)ns;
-        if (ne > (size_t)P.n_paths) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
-        // bytes by construction (nh_wavefront.hip): shade loads 96 B per path (ray, hit, Li, throughput,
-        // rng, flags, pid), +16 pending BSDF sample after the first bounce, +17 (pending NEE + occlusion)
-        // per queued shadow ray; stores 116 B per survivor, 36 per new shadow ray, 12 per finished path
-        const uint64_t shaded = (uint64_t)L.n_ext, pend = first ? 0 : shaded;
+        if (ne > (uint64_t)P.n_paths) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
+        in_e.push_back(ne);
+        in_s.push_back(ns);
+        if (ne == 0) break;  // bounce `it` was enqueued empty: the chunk is done
+        if (it > 100000) return fail(c, "wavefront did not terminate"), NH_ERR_DEVICE;
+    }
+    HIP_TRY(c, hipEventSynchronize(c->wf_events[(size_t)it * 4 + 3]));
+    for (int b = 0; b <= it; ++b) {
+        hipEvent_t *ev = &c->wf_events[(size_t)b * 4];
+        float a = 0.f, sh = 0.f, d = 0.f;
+        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+        (void)hipEventElapsedTime(&sh, ev[1], ev[2]);
+        (void)hipEventElapsedTime(&d, ev[2], ev[3]);
+        c->stats.kernel_ms_extend += a;
+        c->stats.kernel_ms_shadow += sh;
+        c->stats.kernel_ms_shade += d;
+        c->stats.launches_extend++;
+        c->stats.launches_shadow++;
+        c->stats.launches_shade++;
+    }
+    // bytes by construction (nh_wavefront.hip): shade loads 96 B per path (ray, hit, Li, throughput,
+    // rng, flags, pid), +16 pending BSDF sample after the first bounce, +17 (pending NEE + occlusion)
+    // per queued shadow ray; stores 116 B per survivor, 36 per new shadow ray, 12 per finished path
+    for (size_t b = 0; b + 1 < in_e.size(); ++b) {
+        const uint64_t shaded = in_e[b], nsh = in_s[b], ne = in_e[b + 1], ns = in_s[b + 1];
+        const uint64_t pend = b == 0 ? 0 : shaded;
         c->stats.paths_shaded += shaded;
-        c->stats.shade_state_bytes += shaded * 96 + pend * 16 + (uint64_t)L.n_sh * 17 + ne * 116 + ns * 36 +
-                                      (shaded - ne) * 12;
-        c->stats.extend_queue_bytes += shaded * 48;        // ray in (32 B), hit out (16 B)
-        c->stats.shadow_queue_bytes += (uint64_t)L.n_sh * 37;  // ray in, path slot, occlusion byte out
-        first = false;
-        L.n_ext = (int)ne;
-        L.n_sh = (int)ns;
-        L.in_q ^= 1;
+        c->stats.shade_state_bytes += shaded * 96 + pend * 16 + nsh * 17 + ne * 116 + ns * 36 + (shaded - ne) * 12;
+        c->stats.extend_queue_bytes += shaded * 48;  // ray in (32 B), hit out (16 B)
+        c->stats.shadow_queue_bytes += nsh * 37;     // ray in, path slot, occlusion byte out
     }
     return NH_OK;
 }

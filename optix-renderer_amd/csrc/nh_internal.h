@@ -75,6 +75,14 @@ struct WfState {
     unsigned *counts;        // per-shard append counters, one 128-B line each:
                              // [s * kCountStride] paths, [(kQueueShards + s) * kCountStride] shadow rays
 };
+// Queue counts live on the device: the shade kernel of bounce i appends into count slot
+// (i+1)&1, the kernels of bounce i+1 read it (8 shard counts -> dense prefix) -- the host never
+// sizes a grid from them, it only reads them back (one bounce behind) to know when to stop.
+// A count slot holds 4 groups of kQueueShards counters, each on its own 128-B line:
+//   group 0 path appends, 1 shadow-ray appends, 2 / 3 persistent extend / any-hit fetch cursors.
+constexpr int kCountGroup = kQueueShards * kCountStride;
+constexpr int kCountSlot = 4 * kCountGroup;
+
 struct WfLaunch {
     WfState st;
     int n_paths, n_list, s0;
@@ -82,16 +90,15 @@ struct WfLaunch {
     const int *pixel_list;
     float4 *rec_rgbx;
     float *rec_jy;
-    int n_ext, n_sh, in_q;
-    // queue entry q lives at slot s * seg_cap + (q - pre[s]) for the shard s with
-    // pre[s] <= q < pre[s + 1] (a dense queue is pre = {0, n, n, ...})
-    int seg_cap;
-    int pre_ext[kQueueShards + 1], pre_sh[kQueueShards + 1];
+    int in_q;               // buffer (and count slot) read by this bounce
+    unsigned *cnt_in;       // count slot of this bounce's input queues
+    unsigned *cnt_out;      // count slot the shade kernel appends into
+    int seg_cap;            // entries per shard segment of every queue / buffer
     unsigned long long *counters;
 };
 namespace nh {
 void launch_wf_generate(const nhd::DScene *S, const WfLaunch &L, hipStream_t st);
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                     bool shadow, int depth, hipStream_t st);
+                     bool shadow, bool persistent, int depth, hipStream_t st);
 void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, hipStream_t st);
 }  // namespace nh

@@ -59,6 +59,30 @@ __device__ __forceinline__ int queue_slot(const int *pre, int seg_cap, int q) {
     return slot;
 }
 
+// dense prefix over the 8 shard counts of one count group
+struct QView {
+    int n;
+    int pre[kQueueShards + 1];
+};
+__device__ __forceinline__ QView queue_view(const unsigned *group) {
+    QView v;
+    v.pre[0] = 0;
+#pragma unroll
+    for (int s = 0; s < kQueueShards; ++s) v.pre[s + 1] = v.pre[s] + (int)group[s * kCountStride];
+    v.n = v.pre[kQueueShards];
+    return v;
+}
+
+__device__ __forceinline__ void flush_trav_stats(unsigned long long *dst, unsigned long long queries,
+                                                 const TravStats &st) {
+    unsigned long long v[4] = {queries, st.nodes, st.boxes, st.prims};
+    for (int j = 0; j < 4; ++j) {
+        unsigned long long x = v[j];
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&dst[j], x);
+    }
+}
+
 // the state one shade step produces for a surviving path
 struct PState {
     float4 ro, rd;   // next ray (origin, mint), (direction, maxt)
@@ -110,58 +134,47 @@ __global__ __launch_bounds__(256) void wf_generate(const DScene *__restrict__ Sp
     L.rec_jy[p] = jy;
 }
 
+// Grid-stride over the live queue (its length is read from the device count slot).
 template <int DEPTH, bool ORDERED, bool STATS>
 __global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
     const DScene &S = *Sp;
-    const int q = blockIdx.x * 128 + threadIdx.x;
+    const QView qv = queue_view(L.cnt_in);
+    const WfBuf &B = L.st.buf[L.in_q];
     TravStats st{0, 0, 0};
-    bool live = false;
-    if (q < L.n_ext) {
-        const WfBuf &B = L.st.buf[L.in_q];
-        const int s = queue_slot(L.pre_ext, L.seg_cap, q);
+    unsigned long long queries = 0;
+    for (int q = blockIdx.x * 128 + threadIdx.x; q < qv.n; q += gridDim.x * 128) {
+        const int s = queue_slot(qv.pre, L.seg_cap, q);
         const float4 ro = B.ray_o[s], rd = B.ray_d[s];
         Hit h;
         // a zero BSDF direction (maxt = -inf) misses every primitive: not traversed, as in the megakernel
-        live = rd.w >= ro.w;
+        const bool live = rd.w >= ro.w;
+        queries += live ? 1 : 0;
         const bool found = live && trace<DEPTH, ORDERED, false, STATS>(tv, S, xyz(ro), xyz(rd), ro.w, rd.w, h,
                                                                        stk + threadIdx.x, 128, st);
         B.hit[s] = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
     }
-    if (STATS) {
-        unsigned long long v[4] = {live ? 1ull : 0ull, st.nodes, st.boxes, st.prims};
-        for (int j = 0; j < 4; ++j) {
-            unsigned long long x = v[j];
-            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-            if ((threadIdx.x & 63) == 0) atomicAdd(&L.counters[j], x);
-        }
-    }
+    if (STATS) flush_trav_stats(L.counters, queries, st);
 }
 
 template <int DEPTH, bool ORDERED, bool STATS>
 __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
     const DScene &S = *Sp;
-    const int q = blockIdx.x * 128 + threadIdx.x;
+    const QView qv = queue_view(L.cnt_in + kCountGroup);
     TravStats st{0, 0, 0};
-    if (q < L.n_sh) {
-        const int s = queue_slot(L.pre_sh, L.seg_cap, q);
+    unsigned long long queries = 0;
+    for (int q = blockIdx.x * 128 + threadIdx.x; q < qv.n; q += gridDim.x * 128) {
+        const int s = queue_slot(qv.pre, L.seg_cap, q);
         const float4 so = L.st.sh_o[s], sd = L.st.sh_d[s];
         Hit h;
+        ++queries;
         const bool occ = trace<DEPTH, ORDERED, true, STATS>(tv, S, xyz(so), xyz(sd), so.w, sd.w, h,
                                                             stk + threadIdx.x, 128, st);
         L.st.buf[L.in_q].occl[L.st.sh_slot[s]] = occ ? 1 : 0;
     }
-    if (STATS) {
-        unsigned long long v[4] = {q < L.n_sh ? 1ull : 0ull, st.nodes, st.boxes, st.prims};
-        for (int j = 0; j < 4; ++j) {
-            unsigned long long x = v[j];
-            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-            if ((threadIdx.x & 63) == 0) atomicAdd(&L.counters[8 + j], x);
-        }
-    }
+    if (STATS) flush_trav_stats(L.counters + 8, queries, st);
 }
-
 
 // Persistent traversal: a fixed grid of waves pulls rays in batches of kFetchBatch from eight
 // fetch segments (segment f = [f*n/8, (f+1)*n/8) of the dense queue index; a wave starts on the
@@ -170,13 +183,15 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
 // instead of waiting for its slowest ray (the 64-lane divergence that made one wave execute
 // ~10x the instructions of an average ray on the 1M-triangle scene).
 constexpr int kFetchBatch = 64;
+constexpr int kTraceBlocks = 256 * 10, kTraceBlocksPersistent = 256 * 8, kShadeBlocks = 256 * 8;
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS>
 __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
     const DScene &S = *Sp;
-    const int n = ANY ? L.n_sh : L.n_ext;
-    const int *pre = ANY ? L.pre_sh : L.pre_ext;
-    unsigned *fetch = L.st.counts + (ANY ? 3 : 2) * kQueueShards * kCountStride;
+    const QView qv = queue_view(L.cnt_in + (ANY ? kCountGroup : 0));
+    const int n = qv.n;
+    const int *pre = qv.pre;
+    unsigned *fetch = L.cnt_in + (ANY ? 3 : 2) * kCountGroup;
     const WfBuf &B = L.st.buf[L.in_q];
     const int lane = threadIdx.x & 63;
     uint32_t *my_stk = stk + threadIdx.x;
@@ -235,14 +250,7 @@ __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp
             }
         }
     }
-    if (STATS) {
-        unsigned long long v[4] = {queries, st.nodes, st.boxes, st.prims};
-        for (int j = 0; j < 4; ++j) {
-            unsigned long long x = v[j];
-            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-            if (lane == 0) atomicAdd(&L.counters[(ANY ? 8 : 0) + j], x);
-        }
-    }
+    if (STATS) flush_trav_stats(L.counters + (ANY ? 8 : 0), queries, st);
 }
 
 // One shade step of the path in slot s of buffer B. Returns whether the path continues (its
@@ -407,54 +415,50 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
 __global__ __launch_bounds__(256, 4) void wf_shade(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ unsigned s_n[2], s_base[2];
     const DScene &S = *Sp;
-    if (threadIdx.x < 2) s_n[threadIdx.x] = 0u;
-    __syncthreads();
-    const int q = blockIdx.x * 256 + (int)threadIdx.x;
-    bool cont = false, nee = false;
-    PState o;
-    float4 so, sd;
-    if (q < L.n_ext)
-        cont = shade_path(S, tv, L, L.st.buf[L.in_q], queue_slot(L.pre_ext, L.seg_cap, q), o, nee, so, sd);
-    const int le = wave_append(&s_n[0], cont);
-    const int ls = wave_append(&s_n[1], cont && nee);
-    __syncthreads();
+    const QView qv = queue_view(L.cnt_in);
+    // gridDim.x is a multiple of kQueueShards, so the 256-entry chunks a shard receives are those
+    // with chunk index = shard (mod 8): at most seg_cap entries (nh_api.hip sizes seg_cap so)
     const int shard = blockIdx.x & (kQueueShards - 1);
-    if (threadIdx.x == 0) {
-        s_base[0] = s_n[0] ? atomicAdd(&L.st.counts[shard * kCountStride], s_n[0]) : 0u;
-        s_base[1] = s_n[1] ? atomicAdd(&L.st.counts[(kQueueShards + shard) * kCountStride], s_n[1]) : 0u;
-    }
-    __syncthreads();
-    if (cont) {
-        const int slot = shard * L.seg_cap + (int)s_base[0] + le;
-        store_state(L.st.buf[1 - L.in_q], slot, o);
-        if (nee) {
-            const int ss = shard * L.seg_cap + (int)s_base[1] + ls;
-            L.st.sh_o[ss] = so;
-            L.st.sh_d[ss] = sd;
-            L.st.sh_slot[ss] = slot;
+    for (int base = blockIdx.x * 256; base < qv.n; base += gridDim.x * 256) {
+        if (threadIdx.x < 2) s_n[threadIdx.x] = 0u;
+        __syncthreads();
+        const int q = base + (int)threadIdx.x;
+        bool cont = false, nee = false;
+        PState o;
+        float4 so, sd;
+        if (q < qv.n)
+            cont = shade_path(S, tv, L, L.st.buf[L.in_q], queue_slot(qv.pre, L.seg_cap, q), o, nee, so, sd);
+        const int le = wave_append(&s_n[0], cont);
+        const int ls = wave_append(&s_n[1], cont && nee);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s_base[0] = s_n[0] ? atomicAdd(&L.cnt_out[shard * kCountStride], s_n[0]) : 0u;
+            s_base[1] = s_n[1] ? atomicAdd(&L.cnt_out[kCountGroup + shard * kCountStride], s_n[1]) : 0u;
         }
+        __syncthreads();
+        if (cont) {
+            const int slot = shard * L.seg_cap + (int)s_base[0] + le;
+            store_state(L.st.buf[1 - L.in_q], slot, o);
+            if (nee) {
+                const int ss = shard * L.seg_cap + (int)s_base[1] + ls;
+                L.st.sh_o[ss] = so;
+                L.st.sh_d[ss] = sd;
+                L.st.sh_slot[ss] = slot;
+            }
+        }
+        __syncthreads();  // s_n / s_base are reused by the next chunk
     }
 }
 
 namespace nh {
 
-static bool persistent_traversal() {
-    static const bool on = [] {
-        const char *e = std::getenv("NH_PERSISTENT");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 
 template <int DEPTH>
 static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                              bool shadow, hipStream_t st) {
-    const int n = shadow ? L.n_sh : L.n_ext;
-    if (n <= 0) return;
-    if (persistent_traversal()) {
-        // enough resident waves to fill the chip (LDS-limited at DEPTH 32: 10 workgroups per CU)
-        const int blocks = std::min((n + 127) / 128, 256 * 8);
-        const dim3 grid(blocks);
+                              bool shadow, bool persistent, hipStream_t st) {
+    // fixed grids: the queue length is only known on the device
+    const dim3 grid(persistent ? kTraceBlocksPersistent : kTraceBlocks);
+    if (persistent) {
 #define NH_PT(A, O, T) hipLaunchKernelGGL((wf_trace_pt<DEPTH, O, A, T>), grid, dim3(128), 0, st, S, tv, L)
         if (shadow) {
             if (ordered) { if (stats) NH_PT(true, true, true); else NH_PT(true, true, false); }
@@ -466,7 +470,6 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
 #undef NH_PT
         return;
     }
-    dim3 grid((n + 127) / 128);
 #define NH_WF(K, O, T) hipLaunchKernelGGL((K<DEPTH, O, T>), grid, dim3(128), 0, st, S, tv, L)
     if (shadow) {
         if (ordered) { if (stats) NH_WF(wf_shadow, true, true); else NH_WF(wf_shadow, true, false); }
@@ -479,11 +482,11 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
 }
 
 void launch_wf_trace(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool shadow,
-                     int depth, hipStream_t st) {
-    if (depth <= 16) launch_wf_trace_d<16>(S, tv, L, ordered, stats, shadow, st);
-    else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, st);
-    else if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, st);
-    else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, st);
+                     bool persistent, int depth, hipStream_t st) {
+    if (depth <= 16) launch_wf_trace_d<16>(S, tv, L, ordered, stats, shadow, persistent, st);
+    else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, persistent, st);
+    else if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, persistent, st);
+    else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, persistent, st);
 }
 
 void launch_wf_generate(const DScene *S, const WfLaunch &L, hipStream_t st) {
@@ -491,8 +494,7 @@ void launch_wf_generate(const DScene *S, const WfLaunch &L, hipStream_t st) {
 }
 
 void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, hipStream_t st) {
-    if (L.n_ext <= 0) return;
-    hipLaunchKernelGGL(wf_shade, dim3((L.n_ext + 255) / 256), dim3(256), 0, st, S, tv, L);
+    hipLaunchKernelGGL(wf_shade, dim3(kShadeBlocks), dim3(256), 0, st, S, tv, L);
 }
 
 }  // namespace nh
