@@ -560,13 +560,16 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
             }
         }
         hipEvent_t *ev = &c->wf_events[(size_t)it * 4];
+        // upper bound of this bounce's live paths: the input of the previous bounce (known: the
+        // host has read the counts up to bounce it-2)
+        const int bound = (int)in_e[it == 0 ? 0 : it - 1];
         HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), c->stream));
         HIP_TRY(c, hipEventRecord(ev[0], c->stream));
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, persistent, c->depth, c->stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, persistent, bound, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[1], c->stream));
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, persistent, c->depth, c->stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, persistent, bound, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[2], c->stream));
-        nh::launch_wf_shade(c->d_scene, c->tv, L, c->stream);
+        nh::launch_wf_shade(c->d_scene, c->tv, L, bound, c->stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], c->stream));
         unsigned *h = c->h_counts + (size_t)(it % kRing) * 2 * kCountGroup;

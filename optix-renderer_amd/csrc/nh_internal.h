@@ -99,6 +99,6 @@ struct WfLaunch {
 namespace nh {
 void launch_wf_generate(const nhd::DScene *S, const WfLaunch &L, hipStream_t st);
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                     bool shadow, bool persistent, int depth, hipStream_t st);
-void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, hipStream_t st);
+                     bool shadow, bool persistent, int bound, int depth, hipStream_t st);
+void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, int bound, hipStream_t st);
 }  // namespace nh

@@ -183,7 +183,7 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
 // instead of waiting for its slowest ray (the 64-lane divergence that made one wave execute
 // ~10x the instructions of an average ray on the 1M-triangle scene).
 constexpr int kFetchBatch = 64;
-constexpr int kTraceBlocks = 256 * 10, kTraceBlocksPersistent = 256 * 8, kShadeBlocks = 256 * 8;
+constexpr int kTraceBlocksMax = 1 << 20, kTraceBlocksPersistent = 256 * 8;
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS>
 __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
@@ -455,9 +455,11 @@ namespace nh {
 
 template <int DEPTH>
 static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                              bool shadow, bool persistent, hipStream_t st) {
-    // fixed grids: the queue length is only known on the device
-    const dim3 grid(persistent ? kTraceBlocksPersistent : kTraceBlocks);
+                              bool shadow, bool persistent, int bound, hipStream_t st) {
+    // the queue length is only known on the device: size the grid from the host's upper bound
+    // (the kernels stride over whatever the device count says)
+    const int want = std::max(1, (bound + 127) / 128);
+    const dim3 grid(std::min(want, persistent ? kTraceBlocksPersistent : kTraceBlocksMax));
     if (persistent) {
 #define NH_PT(A, O, T) hipLaunchKernelGGL((wf_trace_pt<DEPTH, O, A, T>), grid, dim3(128), 0, st, S, tv, L)
         if (shadow) {
@@ -482,19 +484,22 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
 }
 
 void launch_wf_trace(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool shadow,
-                     bool persistent, int depth, hipStream_t st) {
-    if (depth <= 16) launch_wf_trace_d<16>(S, tv, L, ordered, stats, shadow, persistent, st);
-    else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, persistent, st);
-    else if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, persistent, st);
-    else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, persistent, st);
+                     bool persistent, int bound, int depth, hipStream_t st) {
+    if (depth <= 16) launch_wf_trace_d<16>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
+    else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
+    else if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
+    else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
 }
 
 void launch_wf_generate(const DScene *S, const WfLaunch &L, hipStream_t st) {
     hipLaunchKernelGGL(wf_generate, dim3((L.n_paths + 255) / 256), dim3(256), 0, st, S, L);
 }
 
-void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, hipStream_t st) {
-    hipLaunchKernelGGL(wf_shade, dim3(kShadeBlocks), dim3(256), 0, st, S, tv, L);
+void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, int bound, hipStream_t st) {
+    // one 256-entry chunk per workgroup up to the bound; a multiple of kQueueShards (see wf_shade)
+    int blocks = std::max(1, (bound + 255) / 256);
+    blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
+    hipLaunchKernelGGL(wf_shade, dim3(blocks), dim3(256), 0, st, S, tv, L);
 }
 
 }  // namespace nh
