@@ -416,37 +416,36 @@ __global__ __launch_bounds__(256, 4) void wf_shade(const DScene *__restrict__ Sp
     __shared__ unsigned s_n[2], s_base[2];
     const DScene &S = *Sp;
     const QView qv = queue_view(L.cnt_in);
-    // gridDim.x is a multiple of kQueueShards, so the 256-entry chunks a shard receives are those
-    // with chunk index = shard (mod 8): at most seg_cap entries (nh_api.hip sizes seg_cap so)
+    // one 256-entry chunk per workgroup: the grid covers the host's upper bound of qv.n
+    const int base = blockIdx.x * 256;
+    if (base >= qv.n) return;  // whole workgroup
+    // gridDim.x is a multiple of kQueueShards, so shard s receives the chunks c = s (mod 8):
+    // at most seg_cap entries (nh_api.hip sizes seg_cap so)
     const int shard = blockIdx.x & (kQueueShards - 1);
-    for (int base = blockIdx.x * 256; base < qv.n; base += gridDim.x * 256) {
-        if (threadIdx.x < 2) s_n[threadIdx.x] = 0u;
-        __syncthreads();
-        const int q = base + (int)threadIdx.x;
-        bool cont = false, nee = false;
-        PState o;
-        float4 so, sd;
-        if (q < qv.n)
-            cont = shade_path(S, tv, L, L.st.buf[L.in_q], queue_slot(qv.pre, L.seg_cap, q), o, nee, so, sd);
-        const int le = wave_append(&s_n[0], cont);
-        const int ls = wave_append(&s_n[1], cont && nee);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            s_base[0] = s_n[0] ? atomicAdd(&L.cnt_out[shard * kCountStride], s_n[0]) : 0u;
-            s_base[1] = s_n[1] ? atomicAdd(&L.cnt_out[kCountGroup + shard * kCountStride], s_n[1]) : 0u;
+    if (threadIdx.x < 2) s_n[threadIdx.x] = 0u;
+    __syncthreads();
+    const int q = base + (int)threadIdx.x;
+    bool cont = false, nee = false;
+    PState o;
+    float4 so, sd;
+    if (q < qv.n) cont = shade_path(S, tv, L, L.st.buf[L.in_q], queue_slot(qv.pre, L.seg_cap, q), o, nee, so, sd);
+    const int le = wave_append(&s_n[0], cont);
+    const int ls = wave_append(&s_n[1], cont && nee);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_base[0] = s_n[0] ? atomicAdd(&L.cnt_out[shard * kCountStride], s_n[0]) : 0u;
+        s_base[1] = s_n[1] ? atomicAdd(&L.cnt_out[kCountGroup + shard * kCountStride], s_n[1]) : 0u;
+    }
+    __syncthreads();
+    if (cont) {
+        const int slot = shard * L.seg_cap + (int)s_base[0] + le;
+        store_state(L.st.buf[1 - L.in_q], slot, o);
+        if (nee) {
+            const int ss = shard * L.seg_cap + (int)s_base[1] + ls;
+            L.st.sh_o[ss] = so;
+            L.st.sh_d[ss] = sd;
+            L.st.sh_slot[ss] = slot;
         }
-        __syncthreads();
-        if (cont) {
-            const int slot = shard * L.seg_cap + (int)s_base[0] + le;
-            store_state(L.st.buf[1 - L.in_q], slot, o);
-            if (nee) {
-                const int ss = shard * L.seg_cap + (int)s_base[1] + ls;
-                L.st.sh_o[ss] = so;
-                L.st.sh_d[ss] = sd;
-                L.st.sh_slot[ss] = slot;
-            }
-        }
-        __syncthreads();  // s_n / s_base are reused by the next chunk
     }
 }
 
