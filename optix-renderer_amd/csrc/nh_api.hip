@@ -41,6 +41,7 @@ struct nh_ctx {
     std::vector<void *> scene_bufs, bvh_bufs;
     bool has_scene = false, has_bvh = false;
     int depth = 0;
+    int n_node_f4 = 0, n_leaves = 0, n_prim_f4 = 0;  // GPU BVH sizes (float4 / int2 entries)
     std::vector<uint32_t> bvh_indices, shape_offset;
     float *fb = nullptr;
     size_t fb_floats = 0;
@@ -408,6 +409,9 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
         }
     }
     int rc;
+    c->n_node_f4 = (int)nodes.size();
+    c->n_leaves = (int)leaves.size();
+    c->n_prim_f4 = (int)prims.size();
     if ((rc = upload(c, c->bvh_bufs, nodes.data(), nodes.size(), &c->tv.nodes))) return rc;
     if ((rc = upload(c, c->bvh_bufs, leaves.data(), leaves.size(), &c->tv.leaves))) return rc;
     if ((rc = upload(c, c->bvh_bufs, prims.data(), prims.size(), &c->tv.prims))) return rc;
@@ -527,6 +531,15 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     L.rec_rgbx = P.rec_rgbx;
     L.rec_jy = P.rec_jy;
     L.counters = P.counters;
+    // scenes whose BVH fits in a few KB (the Cornell box: < 1 KB) are traversed from an LDS copy
+    const size_t scene_bytes = 16 * (size_t)(c->n_node_f4 + c->n_prim_f4) + 8 * (size_t)c->n_leaves;
+    bool small = scene_bytes <= kSmallSceneBytes;
+    if (const char *e = std::getenv("NH_LDS_SCENE")) small = small && e[0] != '0';
+    if (small) {
+        L.small_nodes = c->n_node_f4;
+        L.small_leaves = c->n_leaves;
+        L.small_prims = c->n_prim_f4;
+    }
     const bool ordered = q->traversal == NH_TRAVERSAL_ORDERED, stats = q->collect_stats != 0;
     const int per_chunk = 256;  // wf_shade's chunk
     const int max_chunks = (P.n_paths + per_chunk - 1) / per_chunk;

@@ -94,8 +94,12 @@ struct WfLaunch {
     unsigned *cnt_in;       // count slot of this bounce's input queues
     unsigned *cnt_out;      // count slot the shade kernel appends into
     int seg_cap;            // entries per shard segment of every queue / buffer
+    // small scenes: float4 / int2 counts of the BVH arrays staged into LDS by the traversal
+    // kernels (0 = traverse from HBM)
+    int small_nodes, small_leaves, small_prims;
     unsigned long long *counters;
 };
+constexpr size_t kSmallSceneBytes = 16384;
 namespace nh {
 void launch_wf_generate(const nhd::DScene *S, const WfLaunch &L, hipStream_t st);
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,

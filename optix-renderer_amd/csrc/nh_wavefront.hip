@@ -134,11 +134,31 @@ __global__ __launch_bounds__(256) void wf_generate(const DScene *__restrict__ Sp
     L.rec_jy[p] = jy;
 }
 
+
+// Stage a small BVH (nodes, leaf table, primitives) into dynamic LDS; returns the traversal view
+// to use. Called by all threads of the workgroup (contains a barrier).
+__device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, const WfLaunch &L, float4 *lds) {
+    if (L.small_nodes + L.small_prims == 0) return tv;
+    float4 *nodes = lds, *prims = lds + L.small_nodes;
+    int2 *leaves = reinterpret_cast<int2 *>(prims + L.small_prims);
+    for (int i = threadIdx.x; i < L.small_nodes; i += blockDim.x) nodes[i] = tv.nodes[i];
+    for (int i = threadIdx.x; i < L.small_prims; i += blockDim.x) prims[i] = tv.prims[i];
+    for (int i = threadIdx.x; i < L.small_leaves; i += blockDim.x) leaves[i] = tv.leaves[i];
+    __syncthreads();
+    Traversal t;
+    t.nodes = nodes;
+    t.prims = prims;
+    t.leaves = leaves;
+    return t;
+}
+
 // Grid-stride over the live queue (its length is read from the device count slot).
 template <int DEPTH, bool ORDERED, bool STATS>
-__global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+__global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
+    extern __shared__ float4 lds_scene[];
     const DScene &S = *Sp;
+    const Traversal tv = stage_small_scene(tv_g, L, lds_scene);
     const QView qv = queue_view(L.cnt_in);
     const WfBuf &B = L.st.buf[L.in_q];
     TravStats st{0, 0, 0};
@@ -158,9 +178,11 @@ __global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, 
 }
 
 template <int DEPTH, bool ORDERED, bool STATS>
-__global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+__global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
+    extern __shared__ float4 lds_scene[];
     const DScene &S = *Sp;
+    const Traversal tv = stage_small_scene(tv_g, L, lds_scene);
     const QView qv = queue_view(L.cnt_in + kCountGroup);
     TravStats st{0, 0, 0};
     unsigned long long queries = 0;
@@ -471,7 +493,8 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
 #undef NH_PT
         return;
     }
-#define NH_WF(K, O, T) hipLaunchKernelGGL((K<DEPTH, O, T>), grid, dim3(128), 0, st, S, tv, L)
+    const size_t lds = 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves;
+#define NH_WF(K, O, T) hipLaunchKernelGGL((K<DEPTH, O, T>), grid, dim3(128), lds, st, S, tv, L)
     if (shadow) {
         if (ordered) { if (stats) NH_WF(wf_shadow, true, true); else NH_WF(wf_shadow, true, false); }
         else { if (stats) NH_WF(wf_shadow, false, true); else NH_WF(wf_shadow, false, false); }
