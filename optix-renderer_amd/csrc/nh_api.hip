@@ -404,8 +404,8 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
             float fl;
             std::memcpy(&fl, &li, 4);
             p[0] = make_float4(p0[0], p0[1], p0[2], fl);
-            p[1] = make_float4(p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2], fs);
-            p[2] = make_float4(p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2], f0);
+            p[1] = make_float4(p1[0], p1[1], p1[2], fs);
+            p[2] = make_float4(p2[0], p2[1], p2[2], f0);
         }
     }
     int rc;

@@ -32,14 +32,19 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
         its.sh.n = n;
         return;
     }
-    const int local = __float_as_int(a.w);
-    const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + local);
-    const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
     const float bx = 1 - (h.u + h.v), by = h.u, bz = h.v;
-    const F3 p0 = ldv(S.V, i0), p1 = ldv(S.V, i1), p2 = ldv(S.V, i2);
+    const float4 c = tv.prims[3 * h.k + 2];
+    const F3 p0 = f3(a.x, a.y, a.z), p1 = f3(b.x, b.y, b.z), p2 = f3(c.x, c.y, c.z);  // the mesh's vertices
     its.p = add(add(scl(bx, p0), scl(by, p1)), scl(bz, p2));
     its.u = h.u;
     its.v = h.v;
+    if (!sh.has_uv && !sh.has_n) {
+        its.sh = frame_from_n(normalized(cross(sub(p1, p0), sub(p2, p0))));
+        return;
+    }
+    const int local = __float_as_int(a.w);
+    const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + local);
+    const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
     if (sh.has_uv) {
         its.u = bx * S.UV[2 * i0] + by * S.UV[2 * i1] + bz * S.UV[2 * i2];
         its.v = bx * S.UV[2 * i0 + 1] + by * S.UV[2 * i1 + 1] + bz * S.UV[2 * i2 + 1];

@@ -7,7 +7,8 @@
 //     n3 = (int L.ref, int R.ref, 0, 0)   ref >= 0: inner node, ref < 0: leaf ~ref
 //   leaf table: int2 (start, count) into the primitive array
 //   primitive (48 B, in the reference's m_indices order) = 3 x float4:
-//     triangle: (p0, local face) (p1-p0, shape) (p2-p0, 0)
+//     triangle: (p0, local face) (p1, shape) (p2, 0) -- the vertices themselves, so
+//               setHitInformation needs no index/vertex fetches for the hit point
 //     sphere:   (center, radius) (0, shape) (0, 1)
 // Child boxes live in the parent, so one 64-B fetch tests both children; the
 // reference tests a node's own box when it is visited, which is the same set of
@@ -70,9 +71,9 @@ NHD bool box_test(float mnx, float mny, float mnz, float mxx, float mxy, float m
     return mint <= far_t && near_t <= maxt;
 }
 
-// Mesh::rayIntersect (mesh.cpp:101-139) on precomputed edges
+// Mesh::rayIntersect (mesh.cpp:101-139): edges from the vertices, as the reference computes them
 NHD bool tri_test(float4 a, float4 b, float4 c, F3 o, F3 d, float mint, float maxt, float &t, float &u, float &v) {
-    F3 p0 = f3(a.x, a.y, a.z), e1 = f3(b.x, b.y, b.z), e2 = f3(c.x, c.y, c.z);
+    const F3 p0 = f3(a.x, a.y, a.z), e1 = sub(f3(b.x, b.y, b.z), p0), e2 = sub(f3(c.x, c.y, c.z), p0);
     F3 pvec = cross(d, e2);
     float det = dot(e1, pvec);
     if (det > -1e-8f && det < 1e-8f) return false;
