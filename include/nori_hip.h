@@ -224,6 +224,9 @@ typedef struct nh_render_stats {
     /* wavefront mode, always counted (host side, from the queue counts): path-state bytes the
        shade kernels load + store, and the queue bytes of the extend / any-hit kernels */
     uint64_t shade_state_bytes, extend_queue_bytes, shadow_queue_bytes, paths_shaded;
+    /* wavefront mode: the tail kernel that finishes the last few live paths of a chunk in place */
+    double kernel_ms_tail;
+    uint64_t launches_tail;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;

@@ -559,6 +559,10 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     const size_t append_bytes = 2 * kCountGroup * sizeof(unsigned);
     // per-bounce totals: in_e / in_s = live paths / shadow rays entering the bounce
     std::vector<uint64_t> in_e{(uint64_t)P.n_paths}, in_s{0};
+    // below this many live paths the rest of the chunk runs in one wf_tail launch
+    int64_t tail_at = std::max<int64_t>(P.n_paths / 64, 8192);
+    if (const char *e = std::getenv("NH_TAIL")) tail_at = std::atoll(e);
+    bool tail = false;
     int it = 0;
     for (;; ++it) {
         const int in = it & 1;
@@ -582,6 +586,23 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         HIP_TRY(c, hipEventRecord(ev[1], c->stream));
         nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, persistent, bound, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[2], c->stream));
+        tail = it > 0 && (int64_t)bound <= tail_at;
+        if (tail) {
+            nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, bound, c->depth, c->stream);
+            HIP_TRY(c, hipGetLastError());
+            HIP_TRY(c, hipEventRecord(ev[3], c->stream));
+            // the last regular bounce's output counts, for the byte accounting below
+            HIP_TRY(c, hipEventSynchronize(c->wf_copy_ev[(it - 1) % kRing]));
+            const unsigned *hp = c->h_counts + (size_t)((it - 1) % kRing) * 2 * kCountGroup;
+            uint64_t ne = 0, ns = 0;
+            for (int s = 0; s < kQueueShards; ++s) {
+                ne += hp[s * kCountStride];
+                ns += hp[kCountGroup + s * kCountStride];
+            }
+            in_e.push_back(ne);
+            in_s.push_back(ns);
+            break;
+        }
         nh::launch_wf_shade(c->d_scene, c->tv, L, bound, c->stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], c->stream));
@@ -614,14 +635,20 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         (void)hipEventElapsedTime(&d, ev[2], ev[3]);
         c->stats.kernel_ms_extend += a;
         c->stats.kernel_ms_shadow += sh;
-        c->stats.kernel_ms_shade += d;
         c->stats.launches_extend++;
         c->stats.launches_shadow++;
-        c->stats.launches_shade++;
+        if (tail && b == it) {
+            c->stats.kernel_ms_tail += d;
+            c->stats.launches_tail++;
+        } else {
+            c->stats.kernel_ms_shade += d;
+            c->stats.launches_shade++;
+        }
     }
     // bytes by construction (nh_wavefront.hip): shade loads 96 B per path (ray, hit, Li, throughput,
     // rng, flags, pid), +16 pending BSDF sample after the first bounce, +17 (pending NEE + occlusion)
     // per queued shadow ray; stores 116 B per survivor, 36 per new shadow ray, 12 per finished path
+    // (bounces shaded by wf_shade only; the tail kernel's work is not part of this account)
     for (size_t b = 0; b + 1 < in_e.size(); ++b) {
         const uint64_t shaded = in_e[b], nsh = in_s[b], ne = in_e[b + 1], ns = in_s[b + 1];
         const uint64_t pend = b == 0 ? 0 : shaded;

@@ -105,4 +105,6 @@ void launch_wf_generate(const nhd::DScene *S, const WfLaunch &L, hipStream_t st)
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                      bool shadow, bool persistent, int bound, int depth, hipStream_t st);
 void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, int bound, hipStream_t st);
+void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
+                    int bound, int depth, hipStream_t st);
 }  // namespace nh

@@ -471,6 +471,51 @@ __global__ __launch_bounds__(256, 4) void wf_shade(const DScene *__restrict__ Sp
     }
 }
 
+// Tail of a chunk: once few paths are alive, per-bounce launches cost more than the work they
+// carry (three kernels + count traffic for a few thousand paths). wf_tail takes the live queue
+// of a bounce whose extend / any-hit traversals are done and finishes every path in place, one
+// thread per path: shade, then its next closest-hit and shadow traversals, until it terminates --
+// the same operations in the same order as further wavefront bounces.
+template <int DEPTH, bool ORDERED, bool STATS>
+__global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
+    __shared__ uint32_t stk[DEPTH * 128];
+    extern __shared__ float4 lds_scene[];
+    const DScene &S = *Sp;
+    const Traversal tv = stage_small_scene(tv_g, L, lds_scene);
+    const QView qv = queue_view(L.cnt_in);
+    const WfBuf &B = L.st.buf[L.in_q];
+    TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
+    unsigned long long q_e = 0, q_s = 0;
+    for (int q = blockIdx.x * 128 + threadIdx.x; q < qv.n; q += gridDim.x * 128) {
+        const int s = queue_slot(qv.pre, L.seg_cap, q);
+        for (;;) {
+            PState o;
+            bool nee = false;
+            float4 so, sd;
+            if (!shade_path(S, tv, L, B, s, o, nee, so, sd)) break;
+            store_state(B, s, o);
+            Hit h;
+            const bool live = o.rd.w >= o.ro.w;
+            q_e += live ? 1 : 0;
+            const bool found = live && trace<DEPTH, ORDERED, false, STATS>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w,
+                                                                           o.rd.w, h, stk + threadIdx.x, 128, st_e);
+            B.hit[s] = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
+            if (nee) {
+                ++q_s;
+                Hit hs;
+                B.occl[s] = trace<DEPTH, ORDERED, true, STATS>(tv, S, xyz(so), xyz(sd), so.w, sd.w, hs,
+                                                               stk + threadIdx.x, 128, st_s)
+                                ? 1
+                                : 0;
+            }
+        }
+    }
+    if (STATS) {
+        flush_trav_stats(L.counters, q_e, st_e);
+        flush_trav_stats(L.counters + 8, q_s, st_s);
+    }
+}
+
 namespace nh {
 
 
@@ -511,6 +556,25 @@ void launch_wf_trace(const DScene *S, const Traversal &tv, const WfLaunch &L, bo
     else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
     else if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
     else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
+}
+
+template <int DEPTH>
+static void launch_wf_tail_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
+                             int bound, hipStream_t st) {
+    const dim3 grid(std::max(1, (bound + 127) / 128));
+    const size_t lds = 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves;
+#define NH_TL(O, T) hipLaunchKernelGGL((wf_tail<DEPTH, O, T>), grid, dim3(128), lds, st, S, tv, L)
+    if (ordered) { if (stats) NH_TL(true, true); else NH_TL(true, false); }
+    else { if (stats) NH_TL(false, true); else NH_TL(false, false); }
+#undef NH_TL
+}
+
+void launch_wf_tail(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
+                    int depth, hipStream_t st) {
+    if (depth <= 16) launch_wf_tail_d<16>(S, tv, L, ordered, stats, bound, st);
+    else if (depth <= 32) launch_wf_tail_d<32>(S, tv, L, ordered, stats, bound, st);
+    else if (depth <= 64) launch_wf_tail_d<64>(S, tv, L, ordered, stats, bound, st);
+    else launch_wf_tail_d<128>(S, tv, L, ordered, stats, bound, st);
 }
 
 void launch_wf_generate(const DScene *S, const WfLaunch &L, hipStream_t st) {

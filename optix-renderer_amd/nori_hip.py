@@ -116,7 +116,7 @@ class nh_render_stats(C.Structure):
                 ("shadow_nodes_visited", C.c_uint64), ("shadow_boxes_tested", C.c_uint64),
                 ("shadow_prims_tested", C.c_uint64), ("shade_state_bytes", C.c_uint64),
                 ("extend_queue_bytes", C.c_uint64), ("shadow_queue_bytes", C.c_uint64),
-                ("paths_shaded", C.c_uint64)]
+                ("paths_shaded", C.c_uint64), ("kernel_ms_tail", C.c_double), ("launches_tail", C.c_uint64)]
 
 
 def _sig(name, res, *args):

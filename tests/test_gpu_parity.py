@@ -209,3 +209,26 @@ def test_render_parity_envmap(gpu, tmp_path, texture, integrator, mode):
     print(f"envmap {texture} integrator={integrator} mode={mode}: rel-L2 {e:.3e}, max|d| {np.abs(g - r).max():.3e}")
     assert e < TOL_REL_L2
     assert nh.to_rgb(r, s.border).mean() > 0.05
+
+
+@pytest.mark.parametrize("knob", ["NH_PERSISTENT=1", "NH_PERSISTENT=0", "NH_LDS_SCENE=0", "NH_TAIL=0", "NH_TAIL=1000000"])
+def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
+    """The traversal variants the wavefront picks per scene (persistent ray-fetching traversal for
+    deep BVHs, per-lane traversal, LDS-staged small BVHs) all give the megakernel's framebuffer
+    bit for bit, on a microfacet mesh (deep BVH) and on the Cornell box (LDS-sized BVH)."""
+    name, val = knob.split("=")
+    for xml in (scenegen.bumpy_cbox_xml(str(tmp_path), 160, 80)[0], scenegen.cbox_xml(str(tmp_path), "c1")):
+        s = nh.Scene(xml)
+        s.set_resolution(48, 40)
+        b = nh.Bvh(s)
+        ref = nh.Context(0)
+        ref.upload(s, b)
+        ref.render(0, 6, seed=11, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_MEGAKERNEL, stats=True)
+        monkeypatch.setenv(name, val)
+        ctx = nh.Context(0)
+        ctx.upload(s, b)
+        ctx.render(0, 6, seed=11, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT, stats=True)
+        monkeypatch.delenv(name)
+        np.testing.assert_array_equal(ref.framebuffer(), ctx.framebuffer())
+        for k in ("ray_queries", "nodes_visited", "prims_tested"):
+            assert ref.stats()[k] == ctx.stats()[k], (xml, k)
