@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--steps", type=int, default=16)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--rounds", type=int, default=16, help="sample rounds per step")
-    p.add_argument("--config", default="c2", choices=["c1", "c2", "c4", "bumpy1m"])
+    p.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "bumpy1m"])
     p.add_argument("--width", type=int, default=None)
     p.add_argument("--height", type=int, default=None)
     p.add_argument("--traversal", default="ordered", choices=["ordered", "reference"])
@@ -60,16 +60,23 @@ def parse():
 
 
 def build_scene(args, tmp):
+    """SURVEY.md 8(d) configurations. Returns (xml, W, H, description, default spp per step count)."""
     import scenegen
     if args.config in ("c1", "c2", "c4"):
         w = args.width or (2048 if args.config == "c4" else 1024)
         h = args.height or w
         xml = scenegen.cbox_xml(tmp, "c2" if args.config == "c2" else "c1", width=w, height=h)
         desc = f"Cornell box ({'diffuse-only' if args.config == 'c2' else 'mirror+dielectric'}) {w}x{h}"
+    elif args.config == "c5":
+        w = args.width or 4096
+        h = args.height or w
+        xml, ntri = scenegen.c5_xml(tmp, width=w, height=h)
+        desc = f"C5: 10 flattened bumpy meshes ({ntri} tris) + png envmap + area light {w}x{h}"
     else:
         w = args.width or 1024
         h = args.height or w
-        xml, ntri = scenegen.bumpy_cbox_xml(tmp, 2000, 250, width=w, height=h)
+        n_phi = 1000 if args.config == "c3" else 2000
+        xml, ntri = scenegen.bumpy_cbox_xml(tmp, n_phi, 250, width=w, height=h)
         desc = f"cbox + synthetic bumpy sphere ({ntri} tris, Beckmann microfacet) {w}x{h}"
     return xml, w, h, desc
 

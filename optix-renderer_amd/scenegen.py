@@ -260,3 +260,64 @@ def envmap_xml(out_dir: str, width: int = 64, height: int = 48, spp: int = 16, t
     with open(dst, "w") as f:
         f.write(text)
     return dst
+
+
+def c5_xml(out_dir: str, n_copies: int = 10, n_phi: int = 2000, n_theta: int = 250, width: int = 4096,
+           height: int = 4096, spp: int = 16, sky=(1500, 750)) -> tuple[str, int]:
+    """C5: n_copies bumpy meshes with distinct affine transforms, flattened
+    (Nori bakes toWorld, obj.cpp:107-121; no instancing), lit by an envmap png_texture with
+    sphericalTexture=true (a synthetic sky of the size of scenes/project/res/rooitou_park.png,
+    which does not travel to the GPU box) and a small area light. Returns (xml, triangle count)."""
+    os.makedirs(out_dir, exist_ok=True)
+    mesh = os.path.join(out_dir, f"bumpy_{n_phi}x{n_theta}_c0.obj")
+    ntri = bumpy_sphere_obj(mesh, n_phi, n_theta, center=(0.0, 0.0, 0.0), radius=1.0)
+    rng = np.random.default_rng(5)
+    shapes = []
+    for i in range(n_copies):
+        ang = i * 360.0 / n_copies
+        x, z = 2.2 * np.cos(np.radians(ang)), 2.2 * np.sin(np.radians(ang))
+        sc = 0.45 + 0.2 * rng.random()
+        rot = 360.0 * rng.random()
+        kd = rng.random(3) * 0.5 + 0.2
+        bsdf = (f'<bsdf type="microfacet"><float name="alpha" value="{0.1 + 0.3 * rng.random():.3f}"/>'
+                f'<color name="kd" value="{kd[0]:.3f} {kd[1]:.3f} {kd[2]:.3f}"/></bsdf>' if i % 2 == 0 else
+                f'<bsdf type="diffuse"><color name="albedo" value="{kd[0]:.3f} {kd[1]:.3f} {kd[2]:.3f}"/></bsdf>')
+        shapes.append(f"""  <shape type="obj"><string name="filename" value="{os.path.basename(mesh)}"/>
+    <transform name="toWorld"><scale value="{sc:.3f},{sc * 1.1:.3f},{sc:.3f}"/><rotate axis="0,1,0" angle="{rot:.2f}"/>
+      <translate value="{x:.3f},{sc * 1.1:.3f},{z:.3f}"/></transform>
+    {bsdf}</shape>""")
+    png = os.path.join(out_dir, f"sky_{sky[0]}x{sky[1]}.png")
+    if not os.path.exists(png):
+        write_png(png, sky_image(*sky))
+    quad = os.path.join(out_dir, "c5_ground.obj")
+    with open(quad, "w") as f:
+        f.write("v -8 0 -8\nv 8 0 -8\nv 8 0 8\nv -8 0 8\nf 1 4 3 2\n")
+    lq = os.path.join(out_dir, "c5_light.obj")
+    with open(lq, "w") as f:
+        f.write("v -0.5 4 -0.5\nv 0.5 4 -0.5\nv 0.5 4 0.5\nv -0.5 4 0.5\nf 1 2 3 4\n")
+    text = f"""<?xml version="1.0" encoding="utf-8"?>
+<scene>
+  <integrator type="path_mis"/>
+  <sampler type="independent"><integer name="sampleCount" value="{spp}"/></sampler>
+  <camera type="perspective">
+    <transform name="toWorld"><lookat target="0, 0.5, 0" origin="0, 3.5, 7.5" up="0, 1, 0"/></transform>
+    <float name="fov" value="45"/>
+    <integer name="width" value="{width}"/><integer name="height" value="{height}"/>
+  </camera>
+  <emitter type="envmap">
+    <texture type="png_texture" name="albedo">
+      <string name="filename" value="{os.path.basename(png)}"/>
+      <boolean name="sphericalTexture" value="true"/>
+    </texture>
+  </emitter>
+  <shape type="obj"><string name="filename" value="c5_light.obj"/>
+    <emitter type="area"><color name="radiance" value="8 8 8"/></emitter></shape>
+  <shape type="obj"><string name="filename" value="c5_ground.obj"/>
+    <bsdf type="diffuse"><color name="albedo" value="0.4 0.4 0.4"/></bsdf></shape>
+{chr(10).join(shapes)}
+</scene>
+"""
+    dst = os.path.join(out_dir, f"c5_{n_copies}x{n_phi}x{n_theta}_{width}x{height}_{spp}.xml")
+    with open(dst, "w") as f:
+        f.write(text)
+    return dst, ntri * n_copies + 4

@@ -232,3 +232,16 @@ def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
         np.testing.assert_array_equal(ref.framebuffer(), ctx.framebuffer())
         for k in ("ray_queries", "nodes_visited", "prims_tested"):
             assert ref.stats()[k] == ctx.stats()[k], (xml, k)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_render_parity_c5_small(gpu, tmp_path, mode):
+    """C5-shaped scene at test size: flattened transformed bumpy meshes (microfacet + diffuse),
+    png envmap (sphericalTexture) + area light."""
+    xml, ntri = scenegen.c5_xml(str(tmp_path), n_copies=4, n_phi=240, n_theta=60, width=48, height=40, spp=4,
+                                sky=(120, 60))
+    assert ntri > 50000
+    g, r, s = render_pair(xml, 48, 40, 4, mode=mode, traversal=nh.TRAVERSAL_ORDERED)
+    e = rel_l2(g, r)
+    print(f"c5-small mode={mode}: rel-L2 {e:.3e}")
+    assert e < TOL_REL_L2
