@@ -135,7 +135,7 @@ def roofline(args, calib, st, W, H, R):
             "prims_per_query": round(prims / max(q, 1), 3),
             "splat_ms_per_launch": round(st["kernel_ms_splat"] / max(st["launches_splat"], 1), 4)}
     if args.mode == "wavefront":
-        roof["stage_ms"] = {k: round(st[f"kernel_ms_{k}"], 3) for k in ("extend", "shadow", "shade", "splat")}
+        roof["stage_ms"] = {k: round(st[f"kernel_ms_{k}"], 3) for k in ("extend", "shadow", "shade", "tail", "splat")}
         # every traversal/shade stage against HBM, algorithmic bytes as above (per-sample from calibration)
         per = {"shade": calib["shade_state_bytes"],
                "extend": nodes * NODE_BYTES + prims * PRIM_BYTES + calib["extend_queue_bytes"],

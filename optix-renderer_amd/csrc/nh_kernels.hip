@@ -435,8 +435,13 @@ static void launch_path_d(const DScene *S, const Traversal &tv, const PathLaunch
                           hipStream_t st) {
     // 4 waves/SIMD measured best (13.7 / 13.8 / 9.8 / 8.3 ms per 16M C2 samples at 1 / 2 / 3 / 4);
     // the 2-wave build stays selectable (NH_PATH_WAVES=2) for register-heavy experiments
-    if (path_min_waves() == 2) launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, st);
-    else launch_path_w<BLOCK, DEPTH, 4>(S, tv, L, ordered, stats, st);
+    // deep stacks (DEPTH > 32) are LDS-limited below 4 waves anyway: build them for 2
+    if constexpr (DEPTH > 32) {
+        launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, st);
+    } else {
+        if (path_min_waves() == 2) launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, st);
+        else launch_path_w<BLOCK, DEPTH, 4>(S, tv, L, ordered, stats, st);
+    }
 }
 
 void launch_path(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats, int depth,
