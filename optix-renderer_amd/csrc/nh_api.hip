@@ -147,11 +147,11 @@ int nh_create(int device, nh_ctx **out) {
     auto *c = new nh_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->counters, 16 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->counters, kStatShards * kStatStride * sizeof(unsigned long long)) != hipSuccess) {
         delete c;
         return NH_ERR_DEVICE;
     }
-    (void)hipMemset(c->counters, 0, 16 * sizeof(unsigned long long));
+    (void)hipMemset(c->counters, 0, kStatShards * kStatStride * sizeof(unsigned long long));
     *out = c;
     return NH_OK;
 }
@@ -750,7 +750,8 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         rc = ensure_wf(c, (size_t)chunk * per_round);
         if (rc) return rc;
     }
-    if (q->collect_stats) HIP_TRY(c, hipMemsetAsync(c->counters, 0, 16 * sizeof(unsigned long long), c->stream));
+    if (q->collect_stats)
+        HIP_TRY(c, hipMemsetAsync(c->counters, 0, kStatShards * kStatStride * sizeof(unsigned long long), c->stream));
     struct Ev {
         hipEvent_t a, b, d;
     };
@@ -800,7 +801,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         }
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev.b, c->stream));
-        if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters + 4, c->stream);
+        if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters, c->stream);
         nh::launch_splat(P, c->stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev.d, c->stream));
@@ -821,8 +822,10 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     }
     c->stats.samples += (uint64_t)rounds * (uint64_t)c->n_list;
     if (q->collect_stats) {
-        unsigned long long h[16];
-        HIP_TRY(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost));
+        unsigned long long hs[kStatShards * kStatStride], h[16] = {};
+        HIP_TRY(c, hipMemcpy(hs, c->counters, sizeof(hs), hipMemcpyDeviceToHost));
+        for (int sh = 0; sh < kStatShards; ++sh)
+            for (int j = 0; j < 16; ++j) h[j] += hs[sh * kStatStride + j];
         c->stats.ray_queries += h[0] + h[8];
         c->stats.nodes_visited += h[1] + h[9];
         c->stats.boxes_tested += h[2] + h[10];

@@ -40,6 +40,14 @@ struct SplatLaunch {
     float4 *staging;
 };
 
+// In-kernel work counters (collect_stats): kStatShards copies of [0-3] queries, nodes, boxes, prims,
+// [4] invalid samples, [8-11] the any-hit share, one copy per XCD (workgroup b adds to copy b % 8)
+// so the per-wave atomics of concurrent workgroups do not serialise on one address.
+constexpr int kStatShards = 8, kStatStride = 32;
+__device__ __forceinline__ unsigned long long *stat_shard(unsigned long long *c) {
+    return c + (blockIdx.x & (kStatShards - 1)) * kStatStride;
+}
+
 namespace nh {
 void launch_trace(const nhd::DScene *S, const nhd::Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n,
                   bool any, bool ordered, bool stats, int depth, unsigned long long *ctr, hipStream_t st);

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(BLOCK) void nh_trace_kernel(const DScene *__restric
             hb.k[i] = hit ? h.k : -1;
         }
     }
-    if (STATS) flush_stats(st, i < n ? 1u : 0u, counters);
+    if (STATS) flush_stats(st, i < n ? 1u : 0u, stat_shard(counters));
 }
 
 template <int BLOCK, int DEPTH, bool ORDERED, bool STATS, int MINW>
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
         L.rec_rgbx[r] = make_float4(li.x, li.y, li.z, jx);
         L.rec_jy[r] = jy;
     }
-    if (STATS) flush_stats(st, queries, L.counters);
+    if (STATS) flush_stats(st, queries, stat_shard(L.counters));
 }
 
 // ImageBlock::put(pos, value) into the per-block ImageBlock of one (round, block)
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(256) void nh_count_invalid_kernel(const float4 *rec
         c = is_valid(f3(v.x, v.y, v.z)) ? 0 : 1;
     }
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(stat_shard(out) + 4, c);
 }
 
 // ---------------------------------------------------------------------------

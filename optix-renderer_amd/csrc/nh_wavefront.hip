@@ -174,7 +174,7 @@ __global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, 
                                                                        stk + threadIdx.x, 128, st);
         B.hit[s] = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
     }
-    if (STATS) flush_trav_stats(L.counters, queries, st);
+    if (STATS) flush_trav_stats(stat_shard(L.counters), queries, st);
 }
 
 template <int DEPTH, bool ORDERED, bool STATS>
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
                                                             stk + threadIdx.x, 128, st);
         L.st.buf[L.in_q].occl[L.st.sh_slot[s]] = occ ? 1 : 0;
     }
-    if (STATS) flush_trav_stats(L.counters + 8, queries, st);
+    if (STATS) flush_trav_stats(stat_shard(L.counters) + 8, queries, st);
 }
 
 // Persistent traversal: a fixed grid of waves pulls rays in batches of kFetchBatch from eight
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp
             }
         }
     }
-    if (STATS) flush_trav_stats(L.counters + (ANY ? 8 : 0), queries, st);
+    if (STATS) flush_trav_stats(stat_shard(L.counters) + (ANY ? 8 : 0), queries, st);
 }
 
 // One shade step of the path in slot s of buffer B. Returns whether the path continues (its
@@ -511,8 +511,8 @@ __global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Tr
         }
     }
     if (STATS) {
-        flush_trav_stats(L.counters, q_e, st_e);
-        flush_trav_stats(L.counters + 8, q_s, st_s);
+        flush_trav_stats(stat_shard(L.counters), q_e, st_e);
+        flush_trav_stats(stat_shard(L.counters) + 8, q_s, st_s);
     }
 }
 
