@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "bumpy1m"])
     p.add_argument("--width", type=int, default=None)
     p.add_argument("--height", type=int, default=None)
-    p.add_argument("--traversal", default="sah", choices=["sah", "ordered", "reference"])
+    p.add_argument("--traversal", default="ordered", choices=["ordered", "reference"])
     p.add_argument("--mode", default="wavefront", choices=["megakernel", "wavefront"])
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
@@ -195,7 +195,7 @@ def main():
     ctx.upload(scene, bvh)
     upload_s = time.perf_counter() - t0
     blocks = nh.tile_shard(W, H, world, rank) if world > 1 else None
-    trav = {"sah": nh.TRAVERSAL_SAH, "ordered": nh.TRAVERSAL_ORDERED, "reference": nh.TRAVERSAL_REFERENCE}[args.traversal]
+    trav = nh.TRAVERSAL_ORDERED if args.traversal == "ordered" else nh.TRAVERSAL_REFERENCE
     mode = nh.MODE_WAVEFRONT if args.mode == "wavefront" else nh.MODE_MEGAKERNEL
     R = args.rounds
 

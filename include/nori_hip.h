@@ -191,12 +191,7 @@ typedef struct nh_hit_soa {
 /* ---- rendering ------------------------------------------------------------ */
 
 enum { NH_MODE_MEGAKERNEL = 0, NH_MODE_WAVEFRONT = 1 };
-/* Which tree and order answer the ray queries (all three give the reference's closest hit:
- * smallest t, ties to the largest reference leaf-order position):
- *   REFERENCE  the reference BVH (BVH::build), left child first -- the reference's own traversal
- *   ORDERED    the reference BVH, nearer child first
- *   SAH        a binned-SAH tree built for the GPU at nh_upload_bvh (host/gpu_bvh.cpp), nearer first */
-enum { NH_TRAVERSAL_REFERENCE = 0, NH_TRAVERSAL_ORDERED = 1, NH_TRAVERSAL_SAH = 2 };
+enum { NH_TRAVERSAL_REFERENCE = 0, NH_TRAVERSAL_ORDERED = 1 };
 
 typedef struct nh_render_req {
     int32_t sample_begin;         /* sample rounds [sample_begin, sample_end) */

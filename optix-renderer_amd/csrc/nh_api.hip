@@ -19,7 +19,6 @@
 #include <vector>
 
 #include "nh_internal.h"
-#include "../host/gpu_bvh.h"
 #include "nori_hip.h"
 
 using nhd::DBsdf;
@@ -42,11 +41,7 @@ struct nh_ctx {
     std::vector<void *> scene_bufs, bvh_bufs;
     bool has_scene = false, has_bvh = false;
     int depth = 0;
-    struct TreeInfo {
-        int n_node_f4 = 0, n_leaves = 0, n_prim_f4 = 0;  // float4 / int2 entries
-        int depth = 0;                                   // stack entries needed
-    } tree[2];                                           // [0] reference layout, [1] SAH tree
-    nhd::Traversal tv2{};                                // the SAH tree (NH_TRAVERSAL_SAH)
+    int n_node_f4 = 0, n_leaves = 0, n_prim_f4 = 0;  // GPU BVH sizes (float4 / int2 entries)
     std::vector<uint32_t> bvh_indices, shape_offset;
     float *fb = nullptr;
     size_t fb_floats = 0;
@@ -392,15 +387,15 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
         uint32_t local = g - off[s];
         const nh_shape &sh = c->shapes[s];
         float4 *p = &prims[3 * (size_t)k];
-        int si = (int)s, nsi = ~(int)s, ki = (int)k;
-        float fs, fns, fk;
+        int si = (int)s, one = 1, zero = 0;
+        float fs, f1, f0;
         std::memcpy(&fs, &si, 4);
-        std::memcpy(&fns, &nsi, 4);
-        std::memcpy(&fk, &ki, 4);
+        std::memcpy(&f1, &one, 4);
+        std::memcpy(&f0, &zero, 4);
         if (sh.type == NH_SHAPE_SPHERE) {
             p[0] = make_float4(sh.center[0], sh.center[1], sh.center[2], sh.radius);
-            p[1] = make_float4(0, 0, 0, fns);
-            p[2] = make_float4(0, 0, 0, fk);
+            p[1] = make_float4(0, 0, 0, fs);
+            p[2] = make_float4(0, 0, 0, f1);
         } else {
             const uint32_t *f = &c->F[3 * ((size_t)sh.f_offset + local)];
             const float *p0 = &c->V[3 * ((size_t)sh.v_offset + f[0])], *p1 = &c->V[3 * ((size_t)sh.v_offset + f[1])],
@@ -410,64 +405,21 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
             std::memcpy(&fl, &li, 4);
             p[0] = make_float4(p0[0], p0[1], p0[2], fl);
             p[1] = make_float4(p1[0], p1[1], p1[2], fs);
-            p[2] = make_float4(p2[0], p2[1], p2[2], fk);
+            p[2] = make_float4(p2[0], p2[1], p2[2], f0);
         }
     }
     int rc;
-    c->tree[0].n_node_f4 = (int)nodes.size();
-    c->tree[0].n_leaves = (int)leaves.size();
-    c->tree[0].n_prim_f4 = (int)prims.size();
-    c->tree[0].depth = (int)b->max_depth + 2;
-    c->tv.root_kind = S.root_kind;
+    c->n_node_f4 = (int)nodes.size();
+    c->n_leaves = (int)leaves.size();
+    c->n_prim_f4 = (int)prims.size();
     if ((rc = upload(c, c->bvh_bufs, nodes.data(), nodes.size(), &c->tv.nodes))) return rc;
     if ((rc = upload(c, c->bvh_bufs, leaves.data(), leaves.size(), &c->tv.leaves))) return rc;
     if ((rc = upload(c, c->bvh_bufs, prims.data(), prims.size(), &c->tv.prims))) return rc;
-    // NH_TRAVERSAL_SAH tree (host/gpu_bvh.cpp) over the same primitive records
-    {
-        const uint32_t n = b->n_indices;
-        std::vector<float> boxes(6 * (size_t)n), cent(3 * (size_t)n);
-        for (uint32_t k = 0; k < n; ++k) {
-            const float4 *p = &prims[3 * (size_t)k];
-            float *bx = &boxes[6 * (size_t)k];
-            int tag;
-            std::memcpy(&tag, &p[1].w, 4);
-            if (tag < 0) {  // sphere
-                const float cc[3] = {p[0].x, p[0].y, p[0].z};
-                for (int i = 0; i < 3; ++i) {
-                    bx[i] = cc[i] - p[0].w;
-                    bx[3 + i] = cc[i] + p[0].w;
-                }
-            } else {
-                const float v[3][3] = {{p[0].x, p[0].y, p[0].z}, {p[1].x, p[1].y, p[1].z}, {p[2].x, p[2].y, p[2].z}};
-                for (int i = 0; i < 3; ++i) {
-                    bx[i] = std::min(v[0][i], std::min(v[1][i], v[2][i]));
-                    bx[3 + i] = std::max(v[0][i], std::max(v[1][i], v[2][i]));
-                }
-            }
-            for (int i = 0; i < 3; ++i) cent[3 * (size_t)k + i] = 0.5f * (bx[i] + bx[3 + i]);
-        }
-        nh::GpuBvh g;
-        nh::build_gpu_bvh(boxes.data(), cent.data(), n, g);
-        std::vector<float4> prims2(3 * (size_t)n);
-        for (uint32_t j = 0; j < n; ++j)
-            for (int w = 0; w < 3; ++w) prims2[3 * (size_t)j + w] = prims[3 * (size_t)g.order[j] + w];
-        std::vector<int2> leaves2(g.leaves.size());
-        for (size_t i = 0; i < g.leaves.size(); ++i) leaves2[i] = make_int2(g.leaves[i].start, g.leaves[i].count);
-        const float4 *nodes2 = reinterpret_cast<const float4 *>(g.nodes.data());
-        c->tree[1].n_node_f4 = (int)(g.nodes.size() / 4);
-        c->tree[1].n_leaves = (int)leaves2.size();
-        c->tree[1].n_prim_f4 = (int)prims2.size();
-        c->tree[1].depth = g.depth + 2;
-        c->tv2.root_kind = n == 0 ? 0 : g.root_kind;
-        if ((rc = upload(c, c->bvh_bufs, nodes2, g.nodes.size() / 4, &c->tv2.nodes))) return rc;
-        if ((rc = upload(c, c->bvh_bufs, leaves2.data(), leaves2.size(), &c->tv2.leaves))) return rc;
-        if ((rc = upload(c, c->bvh_bufs, prims2.data(), prims2.size(), &c->tv2.prims))) return rc;
-    }
     S.nodes = c->tv.nodes;
     S.prims = c->tv.prims;
     c->bvh_indices.assign(b->indices, b->indices + b->n_indices);
     c->shape_offset = off;
-    c->depth = std::max(c->tree[0].depth, c->tree[1].depth);  // one stack depth for either tree
+    c->depth = (int)b->max_depth + 2;
     if (!c->d_scene) HIP_TRY(c, hipMalloc(&c->d_scene, sizeof(nhd::DScene)));
     HIP_TRY(c, hipMemcpyAsync(c->d_scene, &c->S, sizeof(nhd::DScene), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -495,8 +447,7 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
     HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.u = (float *)p;
     HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.v = (float *)p;
     HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.k = (int *)p;
-    nh::launch_trace(c->d_scene, traversal == NH_TRAVERSAL_SAH ? c->tv2 : c->tv, rb, hb, n, any_hit != 0,
-                     traversal != NH_TRAVERSAL_REFERENCE, false, c->depth,
+    nh::launch_trace(c->d_scene, c->tv, rb, hb, n, any_hit != 0, traversal == NH_TRAVERSAL_ORDERED, false, c->depth,
                      c->counters, c->stream);
     HIP_TRY(c, hipGetLastError());
     std::vector<int> k(nn);
@@ -581,24 +532,21 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     L.rec_jy = P.rec_jy;
     L.counters = P.counters;
     // scenes whose BVH fits in a few KB (the Cornell box: < 1 KB) are traversed from an LDS copy
-    const bool sah = q->traversal == NH_TRAVERSAL_SAH;
-    const nhd::Traversal &tv = sah ? c->tv2 : c->tv;
-    const nh_ctx::TreeInfo &tree = c->tree[sah ? 1 : 0];
-    const size_t scene_bytes = 16 * (size_t)(tree.n_node_f4 + tree.n_prim_f4) + 8 * (size_t)tree.n_leaves;
+    const size_t scene_bytes = 16 * (size_t)(c->n_node_f4 + c->n_prim_f4) + 8 * (size_t)c->n_leaves;
     bool small = scene_bytes <= kSmallSceneBytes;
     if (const char *e = std::getenv("NH_LDS_SCENE")) small = small && e[0] != '0';
     if (small) {
-        L.small_nodes = tree.n_node_f4;
-        L.small_leaves = tree.n_leaves;
-        L.small_prims = tree.n_prim_f4;
+        L.small_nodes = c->n_node_f4;
+        L.small_leaves = c->n_leaves;
+        L.small_prims = c->n_prim_f4;
     }
-    const bool ordered = q->traversal != NH_TRAVERSAL_REFERENCE, stats = q->collect_stats != 0;
+    const bool ordered = q->traversal == NH_TRAVERSAL_ORDERED, stats = q->collect_stats != 0;
     const int per_chunk = 256;  // wf_shade's chunk
     const int max_chunks = (P.n_paths + per_chunk - 1) / per_chunk;
     L.seg_cap = (max_chunks + kQueueShards - 1) / kQueueShards * per_chunk;
     // persistent traversal pays off on deep BVHs (long, divergent traversals); cbox-like scenes
     // traverse faster with one ray per lane
-    bool persistent = tree.depth > 20;
+    bool persistent = c->depth > 20;
     if (const char *e = std::getenv("NH_PERSISTENT")) persistent = e[0] == '1';
     unsigned *slot[2] = {c->wf.counts, c->wf.counts + kCountSlot};
     // bounce 0 reads the dense queue written by generate: shard 0 holds all n_paths
@@ -634,13 +582,13 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         const int bound = (int)in_e[it == 0 ? 0 : it - 1];
         HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), c->stream));
         HIP_TRY(c, hipEventRecord(ev[0], c->stream));
-        nh::launch_wf_trace(c->d_scene, tv, L, ordered, stats, false, persistent, bound, c->depth, c->stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, persistent, bound, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[1], c->stream));
-        nh::launch_wf_trace(c->d_scene, tv, L, ordered, stats, true, persistent, bound, c->depth, c->stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, persistent, bound, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[2], c->stream));
         tail = it > 0 && (int64_t)bound <= tail_at;
         if (tail) {
-            nh::launch_wf_tail(c->d_scene, tv, L, ordered, stats, bound, c->depth, c->stream);
+            nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, bound, c->depth, c->stream);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev[3], c->stream));
             // the last regular bounce's output counts, for the byte accounting below
@@ -655,7 +603,7 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
             in_s.push_back(ns);
             break;
         }
-        nh::launch_wf_shade(c->d_scene, tv, L, bound, c->stream);
+        nh::launch_wf_shade(c->d_scene, c->tv, L, bound, c->stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], c->stream));
         unsigned *h = c->h_counts + (size_t)(it % kRing) * 2 * kCountGroup;
@@ -848,8 +796,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
             rc = render_wavefront(c, q, L);
             if (rc) return rc;
         } else {
-            nh::launch_path(c->d_scene, q->traversal == NH_TRAVERSAL_SAH ? c->tv2 : c->tv, L,
-                            q->traversal != NH_TRAVERSAL_REFERENCE, q->collect_stats != 0, c->depth,
+            nh::launch_path(c->d_scene, c->tv, L, q->traversal == NH_TRAVERSAL_ORDERED, q->collect_stats != 0, c->depth,
                             c->stream);
         }
         HIP_TRY(c, hipGetLastError());

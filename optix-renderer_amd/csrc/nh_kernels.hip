@@ -113,7 +113,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
             found = trace<DEPTH, ORDERED, false, STATS>(tv, S, no, nd, kEps, INFINITY, h, stk, stride, st);
         }
         if (!is_zero(bsdf_col) && found) {
-            const int hs_shape = prim_shape(tv.prims[3 * h.k + 1]);
+            const int hs_shape = __float_as_int(tv.prims[3 * h.k + 1].w);
             const int hem = S.shapes[hs_shape].emitter;
             if (hem >= 0) {
                 Its its_s;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(BLOCK) void nh_trace_kernel(const DScene *__restric
             hb.t[i] = hit ? h.t : INFINITY;
             hb.u[i] = hit ? h.u : 0.f;
             hb.v[i] = hit ? h.v : 0.f;
-            hb.k[i] = hit ? h.rk : -1;  // reference leaf-order position
+            hb.k[i] = hit ? h.k : -1;
         }
     }
     if (STATS) flush_stats(st, i < n ? 1u : 0u, stat_shard(counters));

@@ -15,7 +15,7 @@ struct Its {  // Intersection (include/nori/shape.h:41-79); geoFrame only where 
 // Mesh::setHitInformation (mesh.cpp:141-196) / Sphere::setHitInformation (sphere.cpp:96-124)
 __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, const Hit &h, F3 o, F3 d, Its &its) {
     const float4 a = tv.prims[3 * h.k], b = tv.prims[3 * h.k + 1];
-    const int shape = prim_shape(b);
+    const int shape = __float_as_int(b.w);
     const DShape sh = S.shapes[shape];
     its.shape = shape;
     if (sh.type == SHAPE_SPHERE) {

@@ -6,12 +6,10 @@
 //     n0 = (L.min.xyz, L.max.x)  n1 = (L.max.yz, R.min.xy)  n2 = (R.min.z, R.max.xyz)
 //     n3 = (int L.ref, int R.ref, 0, 0)   ref >= 0: inner node, ref < 0: leaf ~ref
 //   leaf table: int2 (start, count) into the primitive array
-//   primitive (48 B, in the tree's leaf order) = 3 x float4:
-//     triangle: (p0, local face) (p1, shape) (p2, k) -- the vertices themselves, so
+//   primitive (48 B, in the reference's m_indices order) = 3 x float4:
+//     triangle: (p0, local face) (p1, shape) (p2, 0) -- the vertices themselves, so
 //               setHitInformation needs no index/vertex fetches for the hit point
-//     sphere:   (center, radius) (0, ~shape) (0, k)
-//   k = the primitive's position in the reference BVH's m_indices order (the tie-break key);
-//   in the reference-layout tree it equals the array position.
+//     sphere:   (center, radius) (0, shape) (0, 1)
 // Child boxes live in the parent, so one 64-B fetch tests both children; the
 // reference tests a node's own box when it is visited, which is the same set of
 // tests. Deferred children carry their slab entry distance and are re-checked against
@@ -31,8 +29,7 @@ namespace nhd {
 
 struct Hit {
     float t, u, v;
-    int k;   // position in the traversed tree's primitive array
-    int rk;  // reference leaf-order position (tie-break key)
+    int k;  // leaf-order primitive position
 };
 
 struct TravStats {
@@ -110,14 +107,7 @@ struct Traversal {
     const float4 *nodes;
     const int2 *leaves;
     const float4 *prims;
-    int root_kind;  // 0 = empty scene, 1 = root inner node 0, 2 = root is leaf 0
 };
-
-NHD bool prim_is_sphere(float4 b) { return __float_as_int(b.w) < 0; }
-NHD int prim_shape(float4 b) {
-    const int s = __float_as_int(b.w);
-    return s < 0 ? ~s : s;
-}
 
 // Test the primitives of one leaf. Returns true when an any-hit query is answered.
 template <bool ANY, bool STATS>
@@ -128,19 +118,17 @@ NHD bool leaf_test(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float 
         const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
         if (STATS) st.prims++;
         float t, u = 0.f, v = 0.f;
-        bool hit = !prim_is_sphere(b) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
-                                      : sphere_test(a, o, d, mint, maxt, t);
+        bool hit = (__float_as_int(c.w) == 0) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
+                                              : sphere_test(a, o, d, mint, maxt, t);
         if (!hit) continue;
         if (ANY) return true;
-        const int rk = __float_as_int(c.w);
-        if (t < maxt || rk > best.rk) {
+        if (t < maxt || k > best.k) {
             found = true;
             maxt = t;
             best.t = t;
             best.u = u;
             best.v = v;
             best.k = k;
-            best.rk = rk;
         }
     }
     return false;
@@ -163,9 +151,8 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
     // adaptive ray epsilon (bvh.cpp:407-410)
     if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));
     best.k = -1;
-    best.rk = -1;
     best.t = INFINITY;
-    if (tv.root_kind == 0 || maxt < mint) return false;
+    if (S.root_kind == 0 || maxt < mint) return false;
     const F3 r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     bool found = false;
     float near_t;
@@ -173,7 +160,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
     if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d, r,
                   mint, maxt, near_t))
         return false;
-    if (tv.root_kind == 2) {
+    if (S.root_kind == 2) {
         bool any = leaf_test<ANY, STATS>(tv, 0, o, d, mint, maxt, best, found, st);
         return ANY ? any : found;
     }
@@ -253,14 +240,13 @@ struct Tracer {
         // adaptive ray epsilon (bvh.cpp:407-410)
         if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));
         best.k = -1;
-        best.rk = -1;
         best.t = INFINITY;
         found = false;
         done = true;
         sp = 0;
         cur = -1;
         k = kend = 0;
-        if (tv.root_kind == 0 || maxt < mint) return;
+        if (S.root_kind == 0 || maxt < mint) return;
         r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
         float near_t;
         if (STATS) st.boxes++;
@@ -268,7 +254,7 @@ struct Tracer {
                       r, mint, maxt, near_t))
             return;
         done = false;
-        if (tv.root_kind == 2) {
+        if (S.root_kind == 2) {
             const int2 lf = tv.leaves[0];
             k = lf.x;
             kend = lf.x + lf.y;
@@ -282,23 +268,21 @@ struct Tracer {
             const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
             if (STATS) st.prims++;
             float t, u = 0.f, v = 0.f;
-            const bool hit = !prim_is_sphere(b) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
-                                                : sphere_test(a, o, d, mint, maxt, t);
+            const bool hit = (__float_as_int(c.w) == 0) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
+                                                        : sphere_test(a, o, d, mint, maxt, t);
             if (hit) {
                 if (ANY) {
                     found = true;
                     done = true;
                     return;
                 }
-                const int rk = __float_as_int(c.w);
-                if (t < maxt || rk > best.rk) {
+                if (t < maxt || k > best.k) {
                     found = true;
                     maxt = t;
                     best.t = t;
                     best.u = u;
                     best.v = v;
                     best.k = k;
-                    best.rk = rk;
                 }
             }
             ++k;

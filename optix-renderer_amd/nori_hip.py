@@ -30,7 +30,7 @@ BSDF_DIFFUSE, BSDF_MIRROR, BSDF_DIELECTRIC, BSDF_MICROFACET = 0, 1, 2, 3
 EMITTER_AREA, EMITTER_POINT, EMITTER_ENVMAP = 0, 1, 2
 INTEGRATOR_PATH_MIS, INTEGRATOR_PATH_MATS = 0, 1
 MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1
-TRAVERSAL_REFERENCE, TRAVERSAL_ORDERED, TRAVERSAL_SAH = 0, 1, 2
+TRAVERSAL_REFERENCE, TRAVERSAL_ORDERED = 0, 1
 
 _f = C.c_float
 _i32 = C.c_int32

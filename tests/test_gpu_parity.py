@@ -76,7 +76,7 @@ def setup(xml, width=None, height=None):
     return s, b, ctx
 
 
-@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED, nh.TRAVERSAL_SAH])
+@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED])
 def test_trace_parity_cbox(gpu, scene_dir, traversal):
     s, b, ctx = setup(os.path.join(scene_dir, "scenes/pa4/cbox/cbox_path_mis.xml"))
     orc = no.OracleScene(s)
@@ -85,7 +85,7 @@ def test_trace_parity_cbox(gpu, scene_dir, traversal):
     compare_trace(ctx, orc, *secondary_rays(orc, 20000, 11), traversal)
 
 
-@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED, nh.TRAVERSAL_SAH])
+@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED])
 def test_trace_parity_bumpy_mesh(gpu, tmp_path, traversal):
     xml, ntri = scenegen.bumpy_cbox_xml(str(tmp_path), 200, 100)
     assert ntri > 30000
@@ -114,7 +114,7 @@ def render_pair(xml, w, h, spp, seed=5, traversal=nh.TRAVERSAL_REFERENCE, integr
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("variant", ["c1", "c2"])
-@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED, nh.TRAVERSAL_SAH])
+@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED])
 def test_render_parity_cbox(gpu, tmp_path, variant, traversal, mode):
     xml = scenegen.cbox_xml(str(tmp_path), variant)
     g, r, s = render_pair(xml, 64, 48, 16, traversal=traversal, mode=mode)
@@ -134,10 +134,9 @@ def test_render_parity_path_mats(gpu, tmp_path, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_ORDERED, nh.TRAVERSAL_SAH])
-def test_render_parity_microfacet_mesh(gpu, tmp_path, mode, traversal):
+def test_render_parity_microfacet_mesh(gpu, tmp_path, mode):
     xml, _ = scenegen.bumpy_cbox_xml(str(tmp_path), 120, 60)
-    g, r, _ = render_pair(xml, 48, 40, 8, traversal=traversal, mode=mode)
+    g, r, _ = render_pair(xml, 48, 40, 8, traversal=nh.TRAVERSAL_ORDERED, mode=mode)
     e = rel_l2(g, r)
     print(f"microfacet mesh rel-L2 {e:.3e}")
     assert e < TOL_REL_L2
@@ -205,7 +204,7 @@ def test_wavefront_matches_megakernel(gpu, tmp_path, monkeypatch):
 def test_render_parity_envmap(gpu, tmp_path, texture, integrator, mode):
     """EnvMap emitter (NEE by luminance CDF, escaped-ray term) + png_texture lookups, GPU vs oracle."""
     xml = scenegen.envmap_xml(str(tmp_path), texture=texture, tex_size=(96, 48))
-    g, r, s = render_pair(xml, 64, 48, 8, integrator=integrator, mode=mode, traversal=nh.TRAVERSAL_SAH)
+    g, r, s = render_pair(xml, 64, 48, 8, integrator=integrator, mode=mode, traversal=nh.TRAVERSAL_ORDERED)
     e = rel_l2(g, r)
     print(f"envmap {texture} integrator={integrator} mode={mode}: rel-L2 {e:.3e}, max|d| {np.abs(g - r).max():.3e}")
     assert e < TOL_REL_L2
@@ -242,7 +241,7 @@ def test_render_parity_c5_small(gpu, tmp_path, mode):
     xml, ntri = scenegen.c5_xml(str(tmp_path), n_copies=4, n_phi=240, n_theta=60, width=48, height=40, spp=4,
                                 sky=(120, 60))
     assert ntri > 50000
-    g, r, s = render_pair(xml, 48, 40, 4, mode=mode, traversal=nh.TRAVERSAL_SAH)
+    g, r, s = render_pair(xml, 48, 40, 4, mode=mode, traversal=nh.TRAVERSAL_ORDERED)
     e = rel_l2(g, r)
     print(f"c5-small mode={mode}: rel-L2 {e:.3e}")
     assert e < TOL_REL_L2
