@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-calibrate", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl = RCCL over xGMI (production); gloo = host-side reduce, for rehearsing the "
+                        "multi-process flow with several ranks on one GPU")
     return p.parse_args()
 
 
@@ -180,8 +183,12 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = 0  # rehearsal: every rank on GPU 0
+            dist.init_process_group("gloo")
     import nori_hip as nh
 
     tmp = tempfile.mkdtemp(prefix="nh_bench_")
@@ -214,7 +221,7 @@ def main():
     ctx.reset_stats()
     if dist is not None:
         import torch
-        torch.cuda.synchronize()
+        ctx.synchronize()
         dist.barrier()
     ctx.render(0, 0, seed=args.seed, blocks=blocks, traversal=trav, clear=True)
     ctx.synchronize()
@@ -222,16 +229,21 @@ def main():
     for s in range(args.steps):
         ctx.render(s * R, (s + 1) * R, seed=args.seed, blocks=blocks, traversal=trav, clear=False, mode=mode)
     if dist is not None:
-        ptr, n = ctx.framebuffer_device_ptr()
         ctx.synchronize()
-        fb = _wrap_device(ptr, n, local)
-        dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
-        torch.cuda.synchronize()
+        if args.dist_backend == "nccl":
+            ptr, n = ctx.framebuffer_device_ptr()
+            fb = _wrap_device(ptr, n, local)
+            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+            torch.cuda.synchronize()
+        else:
+            fb = torch.from_numpy(ctx.framebuffer().reshape(-1))
+            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
     ctx.synchronize()
     t_end = time.perf_counter()
     elapsed = t_end - t_start
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = ctx.stats()

@@ -245,3 +245,24 @@ def test_render_parity_c5_small(gpu, tmp_path, mode):
     e = rel_l2(g, r)
     print(f"c5-small mode={mode}: rel-L2 {e:.3e}")
     assert e < TOL_REL_L2
+
+
+def test_framebuffer_device_pointer_wraps_in_torch(gpu, tmp_path):
+    """bench.py hands the device framebuffer to torch.distributed (RCCL) through
+    __cuda_array_interface__; the wrapped tensor must alias the context's framebuffer."""
+    import importlib.util
+    import torch
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(
+        os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    s, b, ctx = setup(scenegen.cbox_xml(str(tmp_path), "c2"), 64, 48)
+    ctx.render(0, 4, seed=2, clear=True, mode=nh.MODE_WAVEFRONT)
+    ptr, n = ctx.framebuffer_device_ptr()
+    ctx.synchronize()
+    t = bench._wrap_device(ptr, n, 0)
+    np.testing.assert_array_equal(t.cpu().numpy(), ctx.framebuffer().reshape(-1))
+    orig = ctx.framebuffer().reshape(-1).copy()
+    t.mul_(2.0)  # writes through to the context's buffer
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ctx.framebuffer().reshape(-1), orig * np.float32(2.0))
