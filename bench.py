@@ -129,7 +129,9 @@ def roofline(args, calib, st, W, H, R):
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     key = f"{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}"
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(key),
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            # PMC summaries are recorded for single-GPU runs (per-rank launches are smaller at N > 1)
+            "traffic": pmc_traffic(key) if int(os.environ.get("WORLD_SIZE", "1")) == 1 else None,
             "kernel": kernel, "avg_launch_ms": round(avg_ms, 4), "launches": launches,
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "bytes_per_sample": round(bytes_per_sample, 1),
