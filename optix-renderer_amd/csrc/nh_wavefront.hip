@@ -135,10 +135,10 @@ __global__ __launch_bounds__(256) void wf_generate(const DScene *__restrict__ Sp
 }
 
 
-// Stage a small BVH (nodes, leaf table, primitives) into dynamic LDS; returns the traversal view
-// to use. Called by all threads of the workgroup (contains a barrier).
+// Stage a small BVH (nodes, leaf table, primitives) into dynamic LDS and return a traversal view
+// of the copy. Instantiated only for SMALL kernels, so every traversal pointer derives from the
+// __shared__ array: the compiler emits ds_read, not flat loads. Called by the whole workgroup.
 __device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, const WfLaunch &L, float4 *lds) {
-    if (L.small_nodes + L.small_prims == 0) return tv;
     float4 *nodes = lds, *prims = lds + L.small_nodes;
     int2 *leaves = reinterpret_cast<int2 *>(prims + L.small_prims);
     for (int i = threadIdx.x; i < L.small_nodes; i += blockDim.x) nodes[i] = tv.nodes[i];
@@ -152,13 +152,19 @@ __device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, cons
     return t;
 }
 
+template <bool SMALL>
+__device__ __forceinline__ Traversal traversal_view(const Traversal &tv, const WfLaunch &L, float4 *lds) {
+    if constexpr (SMALL) return stage_small_scene(tv, L, lds);
+    else return tv;
+}
+
 // Grid-stride over the live queue (its length is read from the device count slot).
-template <int DEPTH, bool ORDERED, bool STATS>
+template <int DEPTH, bool ORDERED, bool STATS, bool SMALL>
 __global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
     extern __shared__ float4 lds_scene[];
     const DScene &S = *Sp;
-    const Traversal tv = stage_small_scene(tv_g, L, lds_scene);
+    const Traversal tv = traversal_view<SMALL>(tv_g, L, lds_scene);
     const QView qv = queue_view(L.cnt_in);
     const WfBuf &B = L.st.buf[L.in_q];
     TravStats st{0, 0, 0};
@@ -177,12 +183,12 @@ __global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, 
     if (STATS) flush_trav_stats(stat_shard(L.counters), queries, st);
 }
 
-template <int DEPTH, bool ORDERED, bool STATS>
+template <int DEPTH, bool ORDERED, bool STATS, bool SMALL>
 __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
     extern __shared__ float4 lds_scene[];
     const DScene &S = *Sp;
-    const Traversal tv = stage_small_scene(tv_g, L, lds_scene);
+    const Traversal tv = traversal_view<SMALL>(tv_g, L, lds_scene);
     const QView qv = queue_view(L.cnt_in + kCountGroup);
     TravStats st{0, 0, 0};
     unsigned long long queries = 0;
@@ -476,12 +482,12 @@ __global__ __launch_bounds__(256, 4) void wf_shade(const DScene *__restrict__ Sp
 // of a bounce whose extend / any-hit traversals are done and finishes every path in place, one
 // thread per path: shade, then its next closest-hit and shadow traversals, until it terminates --
 // the same operations in the same order as further wavefront bounces.
-template <int DEPTH, bool ORDERED, bool STATS>
+template <int DEPTH, bool ORDERED, bool STATS, bool SMALL>
 __global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
     extern __shared__ float4 lds_scene[];
     const DScene &S = *Sp;
-    const Traversal tv = stage_small_scene(tv_g, L, lds_scene);
+    const Traversal tv = traversal_view<SMALL>(tv_g, L, lds_scene);
     const QView qv = queue_view(L.cnt_in);
     const WfBuf &B = L.st.buf[L.in_q];
     TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
@@ -538,15 +544,19 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
 #undef NH_PT
         return;
     }
-    const size_t lds = 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves;
-#define NH_WF(K, O, T) hipLaunchKernelGGL((K<DEPTH, O, T>), grid, dim3(128), lds, st, S, tv, L)
+    const bool small = DEPTH == 16 && L.small_nodes + L.small_prims > 0;
+    const size_t lds = small ? 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves : 0;
+#define NH_WF2(K, O, T, SM) hipLaunchKernelGGL((K<DEPTH, O, T, SM>), grid, dim3(128), lds, st, S, tv, L)
+#define NH_WF(K, O, T) { if constexpr (DEPTH == 16) { if (small) NH_WF2(K, O, T, true); else NH_WF2(K, O, T, false); } \
+                         else NH_WF2(K, O, T, false); }
     if (shadow) {
-        if (ordered) { if (stats) NH_WF(wf_shadow, true, true); else NH_WF(wf_shadow, true, false); }
-        else { if (stats) NH_WF(wf_shadow, false, true); else NH_WF(wf_shadow, false, false); }
+        if (ordered) { if (stats) NH_WF(wf_shadow, true, true) else NH_WF(wf_shadow, true, false) }
+        else { if (stats) NH_WF(wf_shadow, false, true) else NH_WF(wf_shadow, false, false) }
     } else {
-        if (ordered) { if (stats) NH_WF(wf_extend, true, true); else NH_WF(wf_extend, true, false); }
-        else { if (stats) NH_WF(wf_extend, false, true); else NH_WF(wf_extend, false, false); }
+        if (ordered) { if (stats) NH_WF(wf_extend, true, true) else NH_WF(wf_extend, true, false) }
+        else { if (stats) NH_WF(wf_extend, false, true) else NH_WF(wf_extend, false, false) }
     }
+#undef NH_WF2
 #undef NH_WF
 }
 
@@ -562,10 +572,14 @@ template <int DEPTH>
 static void launch_wf_tail_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                              int bound, hipStream_t st) {
     const dim3 grid(std::max(1, (bound + 127) / 128));
-    const size_t lds = 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves;
-#define NH_TL(O, T) hipLaunchKernelGGL((wf_tail<DEPTH, O, T>), grid, dim3(128), lds, st, S, tv, L)
-    if (ordered) { if (stats) NH_TL(true, true); else NH_TL(true, false); }
-    else { if (stats) NH_TL(false, true); else NH_TL(false, false); }
+    const bool small = DEPTH == 16 && L.small_nodes + L.small_prims > 0;
+    const size_t lds = small ? 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves : 0;
+#define NH_TL2(O, T, SM) hipLaunchKernelGGL((wf_tail<DEPTH, O, T, SM>), grid, dim3(128), lds, st, S, tv, L)
+#define NH_TL(O, T) { if constexpr (DEPTH == 16) { if (small) NH_TL2(O, T, true); else NH_TL2(O, T, false); } \
+                      else NH_TL2(O, T, false); }
+    if (ordered) { if (stats) NH_TL(true, true) else NH_TL(true, false) }
+    else { if (stats) NH_TL(false, true) else NH_TL(false, false) }
+#undef NH_TL2
 #undef NH_TL
 }
 
