@@ -18,7 +18,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libnori_hip.so")
+# NH_LIB_PATH: an alternative in-tree build, for A/B measurements in one GPU session
+LIB_PATH = os.environ.get("NH_LIB_PATH") or os.path.join(_HERE, "lib", "libnori_hip.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"nori_hip: HIP library not built ({LIB_PATH}); run `make` or __graft_entry__.build()")
