@@ -245,25 +245,25 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     std::memset(&S, 0, sizeof(S));
     int rc;
     const size_t nv = d->n_vertices;
-    if ((rc = upload(c, c->scene_bufs, ds.data(), ds.size(), &S.shapes.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, db.data(), db.size(), &S.bsdfs.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, de.data(), de.size(), &S.emitters.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, d->emitter_cdf, (size_t)d->n_emitters + 1, &S.emitter_cdf.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, d->V, 3 * nv, &S.V.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, d->N, 3 * nv, &S.N.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, d->UV, 2 * nv, &S.UV.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, d->T, 3 * nv, &S.T.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, d->BT, 3 * nv, &S.BT.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, d->F, 3 * (size_t)d->n_faces, &S.F.p))) return rc;
-    if ((rc = upload(c, c->scene_bufs, d->area_cdf, (size_t)d->n_area_cdf, &S.area_cdf.p))) return rc;
+    if ((rc = upload(c, c->scene_bufs, ds.data(), ds.size(), &S.shapes))) return rc;
+    if ((rc = upload(c, c->scene_bufs, db.data(), db.size(), &S.bsdfs))) return rc;
+    if ((rc = upload(c, c->scene_bufs, de.data(), de.size(), &S.emitters))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->emitter_cdf, (size_t)d->n_emitters + 1, &S.emitter_cdf))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->V, 3 * nv, &S.V))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->N, 3 * nv, &S.N))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->UV, 2 * nv, &S.UV))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->T, 3 * nv, &S.T))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->BT, 3 * nv, &S.BT))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->F, 3 * (size_t)d->n_faces, &S.F))) return rc;
+    if ((rc = upload(c, c->scene_bufs, d->area_cdf, (size_t)d->n_area_cdf, &S.area_cdf))) return rc;
     S.envmap = d->envmap;
     if (d->envmap >= 0) {
         const nh_envmap &e = d->env;
         const size_t texels = (size_t)e.width * (size_t)e.height;
         const float *rgba = nullptr;
         if ((rc = upload(c, c->scene_bufs, e.rgba, 4 * texels, &rgba))) return rc;
-        S.env_rgba.p = reinterpret_cast<const float4 *>(rgba);
-        if ((rc = upload(c, c->scene_bufs, e.cdf, texels + 1, &S.env_cdf.p))) return rc;
+        S.env_rgba = reinterpret_cast<const float4 *>(rgba);
+        if ((rc = upload(c, c->scene_bufs, e.cdf, texels + 1, &S.env_cdf))) return rc;
         S.env_w = e.width;
         S.env_h = e.height;
         S.env_spherical = e.spherical;

@@ -22,33 +22,6 @@ constexpr uint64_t kPcgMult = 0x5851f42d4c957f2dULL;
 
 #define NHD __device__ __forceinline__
 
-// Pointer into device global memory held inside a struct that the kernels read from memory (DScene).
-// A pointer loaded from memory is a generic (flat) pointer to the compiler; indexing through the
-// global address space turns every access into a global_load (SGPR-base addressing, vmcnt-only
-// waits) instead of a flat_load.
-template <class T>
-struct GPtr {
-    const T *p;
-    NHD T operator[](size_t i) const {
-        if constexpr (sizeof(T) == 4) {
-            const uint32_t w = ((const __attribute__((address_space(1))) uint32_t *)(p + i))[0];
-            return __builtin_bit_cast(T, w);
-        } else {
-            static_assert(sizeof(T) % 16 == 0, "GPtr element must be 4 B or a multiple of 16 B");
-            T r;
-            const __attribute__((address_space(1))) uint4 *src = (const __attribute__((address_space(1))) uint4 *)(p + i);
-            uint4 *dst = reinterpret_cast<uint4 *>(&r);
-#pragma unroll
-            for (size_t k = 0; k < sizeof(T) / 16; ++k) {
-                const __attribute__((address_space(1))) uint4 &w = src[k];
-                dst[k] = make_uint4(w.x, w.y, w.z, w.w);
-            }
-            return r;
-        }
-    }
-    NHD GPtr operator+(size_t i) const { return GPtr{p + i}; }
-};
-
 NHD float f_sin(float x) { return (float)sin((double)x); }
 NHD float f_cos(float x) { return (float)cos((double)x); }
 
@@ -181,15 +154,15 @@ struct DScene {
     int root_kind;  // 0 = empty scene, 1 = root inner node 0, 2 = root is a leaf
     int root_start, root_count;
     // geometry / materials
-    GPtr<DShape> shapes;
-    GPtr<DBsdf> bsdfs;
-    GPtr<DEmitter> emitters;
-    GPtr<float> emitter_cdf;
+    const DShape *shapes;
+    const DBsdf *bsdfs;
+    const DEmitter *emitters;
+    const float *emitter_cdf;
     int n_emitters;
     int integrator;  // 0 path_mis, 1 path_mats
-    GPtr<float> V, N, UV, T, BT;
-    GPtr<uint32_t> F;
-    GPtr<float> area_cdf;
+    const float *V, *N, *UV, *T, *BT;
+    const uint32_t *F;
+    const float *area_cdf;
     // camera (perspective.cpp) and filter table (block.cpp)
     float s2c[16], c2w[16];
     float inv_w, inv_h, near_clip, far_clip;
@@ -199,14 +172,14 @@ struct DScene {
     float table[33];
     // EnvMap (environmentmap.cpp) and its albedo texture (PNGTexture.cpp / ConstantTexture)
     int envmap;  // emitter index, or -1
-    GPtr<float4> env_rgba;
-    GPtr<float> env_cdf;  // env_w * env_h + 1 entries
+    const float4 *env_rgba;
+    const float *env_cdf;  // env_w * env_h + 1 entries
     int env_w, env_h, env_spherical, env_constant;
     float env_norm, env_su, env_sv, env_ou, env_ov;
     float env_r, env_g, env_b;
 };
 
-NHD F3 ldv(GPtr<float> a, uint32_t i) { return f3(a[3 * i], a[3 * i + 1], a[3 * i + 2]); }
+NHD F3 ldv(const float *a, uint32_t i) { return f3(a[3 * i], a[3 * i + 1], a[3 * i + 2]); }
 
 // ---- frames (frame.h, common.cpp:292-306) ---------------------------------------
 struct Frame {
@@ -389,7 +362,7 @@ NHD F3 bsdf_sample(const DBsdf &b, F3 wi, float sx, float sy, F3 &wo, int &measu
 }
 
 // DiscretePDF::sample (dpdf.h:124-130): lower_bound then clamp
-NHD int dpdf_sample(GPtr<float> cdf, int n_entries, float x) {
+NHD int dpdf_sample(const float *cdf, int n_entries, float x) {
     int lo = 0, hi = n_entries + 1;  // first index with !(cdf[i] < x)
     while (lo < hi) {
         int mid = (lo + hi) >> 1;

@@ -43,7 +43,7 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
         return;
     }
     const int local = __float_as_int(a.w);
-    const GPtr<uint32_t> f = S.F + 3 * (size_t)(sh.f_off + local);
+    const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + local);
     const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
     if (sh.has_uv) {
         its.u = bx * S.UV[2 * i0] + by * S.UV[2 * i1] + bz * S.UV[2 * i2];
@@ -179,12 +179,12 @@ __device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e,
     const DShape sh = S.shapes[e.shape];
     F3 p, n;
     if (sh.type == SHAPE_MESH) {  // Mesh::sampleSurface (mesh.cpp:50-71)
-        const GPtr<float> cdf = S.area_cdf + sh.pdf_off;
+        const float *cdf = S.area_cdf + sh.pdf_off;
         int idt = dpdf_sample(cdf, sh.n_faces, sx);
         sx = (sx - cdf[idt]) / (cdf[idt + 1] - cdf[idt]);
         float su1 = f_sqrt(sx);  // squareToUniformTriangle (warp.cpp:162-166)
         float bu = 1.f - su1, bv = sy * su1, bw = 1.f - bu - bv;
-        const GPtr<uint32_t> f = S.F + 3 * (size_t)(sh.f_off + idt);
+        const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + idt);
         const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
         const F3 p0 = ldv(S.V, i0), p1 = ldv(S.V, i1), p2 = ldv(S.V, i2);
         p = add(add(scl(bu, p0), scl(bv, p1)), scl(bw, p2));
