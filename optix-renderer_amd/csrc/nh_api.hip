@@ -554,8 +554,6 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     std::memset(h_init, 0, kCountSlot * sizeof(unsigned));
     h_init[0] = (unsigned)P.n_paths;
     HIP_TRY(c, hipMemcpyAsync(slot[0], h_init, kCountSlot * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
-    nh::launch_wf_generate(c->d_scene, L, c->stream);  // timed with the whole chunk (kernel_ms_path)
-    HIP_TRY(c, hipGetLastError());
     const size_t append_bytes = 2 * kCountGroup * sizeof(unsigned);
     // per-bounce totals: in_e / in_s = live paths / shadow rays entering the bounce
     std::vector<uint64_t> in_e{(uint64_t)P.n_paths}, in_s{0};
@@ -567,6 +565,7 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     for (;; ++it) {
         const int in = it & 1;
         L.in_q = in;
+        L.first = it == 0;
         L.cnt_in = slot[in];
         L.cnt_out = slot[in ^ 1];
         if ((size_t)(it + 1) * 4 > c->wf_events.size()) {
@@ -645,17 +644,19 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
             c->stats.launches_shade++;
         }
     }
-    // bytes by construction (nh_wavefront.hip): shade loads 96 B per path (ray, hit, Li, throughput,
-    // rng, flags, pid), +16 pending BSDF sample after the first bounce, +17 (pending NEE + occlusion)
-    // per queued shadow ray; stores 116 B per survivor, 36 per new shadow ray, 12 per finished path
-    // (bounces shaded by wf_shade only; the tail kernel's work is not part of this account)
+    // bytes by construction (nh_wavefront.hip). Bounce 0 evaluates the camera sample in place: shade
+    // loads the hit (16 B) and writes the sample record (20 B) per path. Later bounces load 96 B per
+    // path (ray, hit, Li, throughput, rng, flags, pid) + 16 (pending BSDF sample) + 17 per queued
+    // shadow ray (pending NEE + occlusion). Every bounce stores 116 B per survivor, 36 per new
+    // shadow ray and 12 per finished path; extend moves 48 B per ray (16 at bounce 0: no ray load).
+    // (Bounces shaded by wf_shade only; the tail kernel's work is not part of this account.)
     for (size_t b = 0; b + 1 < in_e.size(); ++b) {
         const uint64_t shaded = in_e[b], nsh = in_s[b], ne = in_e[b + 1], ns = in_s[b + 1];
-        const uint64_t pend = b == 0 ? 0 : shaded;
+        const uint64_t loads = b == 0 ? shaded * (16 + 20) : shaded * (96 + 16) + nsh * 17;
         c->stats.paths_shaded += shaded;
-        c->stats.shade_state_bytes += shaded * 96 + pend * 16 + nsh * 17 + ne * 116 + ns * 36 + (shaded - ne) * 12;
-        c->stats.extend_queue_bytes += shaded * 48;  // ray in (32 B), hit out (16 B)
-        c->stats.shadow_queue_bytes += nsh * 37;     // ray in, path slot, occlusion byte out
+        c->stats.shade_state_bytes += loads + ne * 116 + ns * 36 + (shaded - ne) * 12;
+        c->stats.extend_queue_bytes += shaded * (b == 0 ? 16 : 48);
+        c->stats.shadow_queue_bytes += nsh * 37;  // ray in, path slot, occlusion byte out
     }
     return NH_OK;
 }

@@ -99,6 +99,7 @@ struct WfLaunch {
     float4 *rec_rgbx;
     float *rec_jy;
     int in_q;               // buffer (and count slot) read by this bounce
+    int first;              // bounce 0: paths come from the camera, not from a buffer
     unsigned *cnt_in;       // count slot of this bounce's input queues
     unsigned *cnt_out;      // count slot the shade kernel appends into
     int seg_cap;            // entries per shard segment of every queue / buffer
@@ -109,7 +110,6 @@ struct WfLaunch {
 };
 constexpr size_t kSmallSceneBytes = 16384;
 namespace nh {
-void launch_wf_generate(const nhd::DScene *S, const WfLaunch &L, hipStream_t st);
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                      bool shadow, bool persistent, int bound, int depth, hipStream_t st);
 void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, int bound, hipStream_t st);

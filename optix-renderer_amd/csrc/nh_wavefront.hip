@@ -2,8 +2,8 @@
 // (nh_kernels.hip li_path_mis, i.e. src/integrators/path_mis.cpp:16-150), split into
 // kernels over SoA path state in HBM so each stage runs at its own occupancy:
 //
-//   wf_generate  renderBlock's per-pixel prologue (render.cpp:441-447): seeding, jitter,
-//                camera ray (perspective.cpp:97-141)
+//   (bounce 0)   renderBlock's per-pixel prologue (render.cpp:441-447: seeding, jitter, camera
+//                ray) is evaluated in place by the first extend and shade kernels
 //   wf_extend    closest-hit traversal of every live path's ray (the BSDF-sampled ray is the
 //                MIS probe and the next bounce at once, path_mis.cpp:117/:146) -- the
 //                BVH-traversal kernel whose roofline bench.py reports
@@ -108,30 +108,38 @@ __device__ __forceinline__ void store_state(const WfBuf &B, int s, const PState 
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void wf_generate(const DScene *__restrict__ Sp, WfLaunch L) {
-    const DScene &S = *Sp;
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    if (p >= L.n_paths) return;
+// renderBlock's per-pixel prologue for path p = round * n_list + entry (render.cpp:441-447): seeding,
+// pixel jitter, the unused aperture sample, PerspectiveCamera::sampleRay (perspective.cpp:97-141).
+// Bounce 0 evaluates it in place -- in the extend kernel for the ray, again in the shade kernel
+// for its state -- instead of a generate kernel writing ~100 B per path that both read back.
+__device__ __forceinline__ void camera_sample(const DScene &S, const WfLaunch &L, int p, Rng &rng, float4 &ro,
+                                              float4 &rd, float &jx, float &jy) {
     const int k = p / L.n_list, i = p - k * L.n_list;
     const int pix = L.pixel_list[i];
     const int py = pix / S.width, px = pix - py * S.width;
-    Rng rng = path_rng(L.seed, (uint64_t)pix, (uint64_t)(L.s0 + k));
-    const float jx = rng.next1d(), jy = rng.next1d();
+    rng = path_rng(L.seed, (uint64_t)pix, (uint64_t)(L.s0 + k));
+    jx = rng.next1d();
+    jy = rng.next1d();
     rng.next1d();  // apertureSample (render.cpp:443), unused without depth of field
     rng.next1d();
     F3 o, d;
     float mint, maxt;
     camera_ray(S, (float)px + jx, (float)py + jy, o, d, mint, maxt);
-    const WfBuf &B = L.st.buf[L.in_q];
-    B.ray_o[p] = make_float4(o.x, o.y, o.z, mint);
-    B.ray_d[p] = make_float4(d.x, d.y, d.z, maxt);
-    B.rng[p] = rng.state;
-    B.li[p] = make_float4(0.f, 0.f, 0.f, 1.f);   // Li, w_mats
-    B.thr[p] = make_float4(1.f, 1.f, 1.f, 0.f);  // throughput, w_ems
-    B.flags[p] = F_FIRST;
-    B.pid[p] = p;
-    L.rec_rgbx[p] = make_float4(0.f, 0.f, 0.f, jx);
-    L.rec_jy[p] = jy;
+    ro = make_float4(o.x, o.y, o.z, mint);
+    rd = make_float4(d.x, d.y, d.z, maxt);
+}
+
+// the ray of queue entry q / slot s of this bounce
+__device__ __forceinline__ void load_ray(const DScene &S, const WfLaunch &L, const WfBuf &B, int q, int s, float4 &ro,
+                                         float4 &rd) {
+    if (L.first) {  // dense queue: slot = path id
+        Rng rng;
+        float jx, jy;
+        camera_sample(S, L, q, rng, ro, rd, jx, jy);
+    } else {
+        ro = B.ray_o[s];
+        rd = B.ray_d[s];
+    }
 }
 
 
@@ -171,7 +179,8 @@ __global__ __launch_bounds__(128) void wf_extend(const DScene *__restrict__ Sp, 
     unsigned long long queries = 0;
     for (int q = blockIdx.x * 128 + threadIdx.x; q < qv.n; q += gridDim.x * 128) {
         const int s = queue_slot(qv.pre, L.seg_cap, q);
-        const float4 ro = B.ray_o[s], rd = B.ray_d[s];
+        float4 ro, rd;
+        load_ray(S, L, B, q, s, ro, rd);
         Hit h;
         // a zero BSDF direction (maxt = -inf) misses every primitive: not traversed, as in the megakernel
         const bool live = rd.w >= ro.w;
@@ -256,8 +265,7 @@ __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp
                     ro = L.st.sh_o[slot];
                     rd = L.st.sh_d[slot];
                 } else {
-                    ro = B.ray_o[slot];
-                    rd = B.ray_d[slot];
+                    load_ray(S, L, B, q, slot, ro, rd);
                 }
                 // a zero BSDF direction (maxt = -inf) misses every primitive without a traversal
                 if (STATS && (ANY || rd.w >= ro.w)) ++queries;
@@ -286,13 +294,32 @@ __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp
 // writes its radiance to its sample record.
 __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv, const WfLaunch &L, const WfBuf &B,
                                            int s, PState &o, bool &nee, float4 &so, float4 &sd) {
-    const float4 ro = B.ray_o[s], rd = B.ray_d[s], hv = B.hit[s];
+    const float4 hv = B.hit[s];
+    float4 ro, rd, li4, th4;
+    int flags, pid;
+    Rng rng;
+    if (L.first) {  // bounce 0: the state wf_generate used to write (dense queue: slot = path id)
+        float jx, jy;
+        camera_sample(S, L, s, rng, ro, rd, jx, jy);
+        li4 = make_float4(0.f, 0.f, 0.f, 1.f);   // Li, w_mats
+        th4 = make_float4(1.f, 1.f, 1.f, 0.f);  // throughput, w_ems
+        flags = F_FIRST;
+        pid = s;
+        L.rec_rgbx[pid] = make_float4(0.f, 0.f, 0.f, jx);
+        L.rec_jy[pid] = jy;
+    } else {
+        ro = B.ray_o[s];
+        rd = B.ray_d[s];
+        li4 = B.li[s];
+        th4 = B.thr[s];
+        flags = B.flags[s];
+        pid = B.pid[s];
+        rng.state = B.rng[s];
+        rng.inc = ((uint64_t)(L.s0 + pid / L.n_list) << 1u) | 1u;
+    }
     const F3 org = xyz(ro), d = xyz(rd);
-    const float4 li4 = B.li[s], th4 = B.thr[s];
     F3 li = xyz(li4), t = xyz(th4);
     float w_mats = li4.w, w_ems = th4.w;
-    const int flags = B.flags[s];
-    const int pid = B.pid[s];
     Hit h;
     h.t = hv.x;
     h.u = hv.y;
@@ -302,9 +329,6 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
     Its its;
     bool have_its = false;
     const float n_lights = (float)S.n_emitters;
-    Rng rng;
-    rng.state = B.rng[s];
-    rng.inc = ((uint64_t)(L.s0 + pid / L.n_list) << 1u) | 1u;
     bool alive = true;
     if (S.integrator == 1) {  // ---------------- path_mats (path_mats.cpp:16-78)
         if (!(flags & F_FIRST)) t = mulc(t, xyz(B.pend_col[s]));
@@ -591,9 +615,6 @@ void launch_wf_tail(const DScene *S, const Traversal &tv, const WfLaunch &L, boo
     else launch_wf_tail_d<128>(S, tv, L, ordered, stats, bound, st);
 }
 
-void launch_wf_generate(const DScene *S, const WfLaunch &L, hipStream_t st) {
-    hipLaunchKernelGGL(wf_generate, dim3((L.n_paths + 255) / 256), dim3(256), 0, st, S, L);
-}
 
 void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, int bound, hipStream_t st) {
     // one 256-entry chunk per workgroup up to the bound; a multiple of kQueueShards (see wf_shade)
