@@ -60,6 +60,8 @@ struct nh_ctx {
     nh_render_stats stats{};
     // wavefront path state (nh_internal.h WfState), sized for wf_cap paths
     WfState wf{};
+    uint32_t *trav_spill = nullptr;  // persistent traversal stack spill (kPersistentBlocks * 128 * depth)
+    int trav_spill_depth = 0;
     std::vector<void *> wf_bufs;
     size_t wf_cap = 0;
     unsigned *h_counts = nullptr;  // pinned: kRing bounce-count copies + one initial count slot
@@ -174,6 +176,7 @@ void nh_destroy(nh_ctx *c) {
     (void)hipFree(c->counters);
     (void)hipFree(c->d_scene);
     free_all(c->wf_bufs);
+    (void)hipFree(c->trav_spill);
     if (c->h_counts) (void)hipHostFree(c->h_counts);
     for (hipEvent_t e : c->wf_events) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->wf_copy_ev)
@@ -548,6 +551,15 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     // traverse faster with one ray per lane
     bool persistent = c->depth > 20;
     if (const char *e = std::getenv("NH_PERSISTENT")) persistent = e[0] == '1';
+    if (persistent && c->trav_spill_depth < c->depth) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->trav_spill);
+        c->trav_spill = nullptr;
+        c->trav_spill_depth = c->depth;
+        HIP_TRY(c, hipMalloc(&c->trav_spill, (size_t)kPersistentBlocks * 128 * c->depth * sizeof(uint32_t)));
+    }
+    L.trav_spill = c->trav_spill;
+    L.spill_depth = c->trav_spill_depth;
     unsigned *slot[2] = {c->wf.counts, c->wf.counts + kCountSlot};
     // bounce 0 reads the dense queue written by generate: shard 0 holds all n_paths
     unsigned *h_init = c->h_counts + kRing * 2 * kCountGroup;

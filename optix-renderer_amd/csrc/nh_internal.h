@@ -106,8 +106,13 @@ struct WfLaunch {
     // small scenes: float4 / int2 counts of the BVH arrays staged into LDS by the traversal
     // kernels (0 = traverse from HBM)
     int small_nodes, small_leaves, small_prims;
+    // persistent traversal: per-lane stack spill area (kPersistentBlocks * 128 lanes x spill_depth)
+    uint32_t *trav_spill;
+    int spill_depth;
     unsigned long long *counters;
 };
+// persistent traversal grid: 16 workgroups of 128 lanes per CU (the 8 waves/SIMD its registers allow)
+constexpr int kPersistentBlocks = 256 * 16;
 constexpr size_t kSmallSceneBytes = 16384;
 namespace nh {
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,

@@ -218,11 +218,35 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
 }
 
 
+
+// Traversal stack of one lane for the persistent kernels: the top K entries live in LDS
+// (lane-interleaved, `stride` words apart), deeper entries spill to the lane's own region of a
+// global buffer. LDS per lane no longer scales with the tree depth, so deep trees (the 10M-triangle
+// C5 scene needs 35 entries) keep the occupancy that registers allow.
+template <int K>
+struct RingStack {
+    static_assert((K & (K - 1)) == 0, "K must be a power of two");
+    uint32_t *lds;   // this lane's first LDS slot
+    int stride;
+    uint32_t *glob;  // this lane's spill area (max depth - K entries)
+    NHD void push(int i, uint32_t e) {  // i = index of the new entry
+        uint32_t *slot = lds + (i & (K - 1)) * stride;
+        if (i >= K) glob[i - K] = *slot;  // the slot holds entry i - K: spill it
+        *slot = e;
+    }
+    NHD uint32_t pop(int i) {  // i = index of the top entry
+        uint32_t *slot = lds + (i & (K - 1)) * stride;
+        const uint32_t e = *slot;
+        if (i >= K) *slot = glob[i - K];  // entry i - K moves back into the window
+        return e;
+    }
+};
+
 // Resumable form of trace(): identical visits, box/primitive tests and order (hence identical
 // results and counters), but one unit of work per step() -- one inner node, one primitive, or
 // one stack pop -- so a persistent wave can hand finished lanes new rays between steps instead
 // of idling until its slowest lane is done (nh_wavefront.hip wf_trace_pt).
-template <bool ORDERED, bool ANY, bool STATS>
+template <bool ORDERED, bool ANY, bool STATS, class Stack>
 struct Tracer {
     F3 o, d, r;
     float mint, maxt;
@@ -263,7 +287,7 @@ struct Tracer {
         }
     }
 
-    NHD void step(const Traversal &tv, uint32_t *stk, int stride, TravStats &st) {
+    NHD void step(const Traversal &tv, Stack &stk, TravStats &st) {
         if (k < kend) {  // one primitive of the current leaf
             const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
             if (STATS) st.prims++;
@@ -298,7 +322,7 @@ struct Tracer {
             int next;
             if (hl && hr) {
                 const bool right_first = ORDERED && nr < nl;
-                stk[sp * stride] = ((uint32_t)cur << 1) | (right_first ? 0u : 1u);
+                stk.push(sp, ((uint32_t)cur << 1) | (right_first ? 0u : 1u));
                 ++sp;
                 next = right_first ? n3.y : n3.x;
             } else if (hl) {
@@ -314,7 +338,7 @@ struct Tracer {
         }
         if (sp > 0) {  // one deferred child: re-test its box against the current maxt
             --sp;
-            const uint32_t e = stk[sp * stride];
+            const uint32_t e = stk.pop(sp);
             const int parent = (int)(e >> 1), side = (int)(e & 1u);
             const float4 n0 = tv.nodes[4 * parent], n1 = tv.nodes[4 * parent + 1], n2 = tv.nodes[4 * parent + 2];
             if (STATS) st.boxes++;

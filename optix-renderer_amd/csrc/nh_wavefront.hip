@@ -220,10 +220,11 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
 // instead of waiting for its slowest ray (the 64-lane divergence that made one wave execute
 // ~10x the instructions of an average ray on the 1M-triangle scene).
 constexpr int kFetchBatch = 64;
-constexpr int kTraceBlocksMax = 1 << 20, kTraceBlocksPersistent = 256 * 8;
+constexpr int kTraceBlocksMax = 1 << 20;
+constexpr int kRingEntries = 16;
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS>
 __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
-    __shared__ uint32_t stk[DEPTH * 128];
+    __shared__ uint32_t stk[kRingEntries * 128];
     const DScene &S = *Sp;
     const QView qv = queue_view(L.cnt_in + (ANY ? kCountGroup : 0));
     const int n = qv.n;
@@ -231,11 +232,14 @@ __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp
     unsigned *fetch = L.cnt_in + (ANY ? 3 : 2) * kCountGroup;
     const WfBuf &B = L.st.buf[L.in_q];
     const int lane = threadIdx.x & 63;
-    uint32_t *my_stk = stk + threadIdx.x;
+    RingStack<kRingEntries> my_stk;
+    my_stk.lds = stk + threadIdx.x;
+    my_stk.stride = 128;
+    my_stk.glob = L.trav_spill + ((size_t)blockIdx.x * 128 + threadIdx.x) * (size_t)L.spill_depth;
     int seg = blockIdx.x & (kQueueShards - 1), tried = 0;
     int batch_next = 0, batch_end = 0;  // wave-uniform
     int slot = -1;                      // this lane's ray (queue slot), -1 = idle
-    Tracer<ORDERED, ANY, STATS> tr;
+    Tracer<ORDERED, ANY, STATS, RingStack<kRingEntries>> tr;
     TravStats st{0, 0, 0};
     unsigned long long queries = 0;
     for (;;) {
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp
         }
         if (!__any(slot >= 0)) break;
         if (slot >= 0) {
-            if (!tr.done) tr.step(tv, my_stk, 128, st);
+            if (!tr.done) tr.step(tv, my_stk, st);
             if (tr.done) {
                 if (ANY) {
                     B.occl[L.st.sh_slot[slot]] = tr.found ? 1 : 0;
@@ -555,7 +559,7 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
     // the queue length is only known on the device: size the grid from the host's upper bound
     // (the kernels stride over whatever the device count says)
     const int want = std::max(1, (bound + 127) / 128);
-    const dim3 grid(std::min(want, persistent ? kTraceBlocksPersistent : kTraceBlocksMax));
+    const dim3 grid(std::min(want, persistent ? kPersistentBlocks : kTraceBlocksMax));
     if (persistent) {
 #define NH_PT(A, O, T) hipLaunchKernelGGL((wf_trace_pt<DEPTH, O, A, T>), grid, dim3(128), 0, st, S, tv, L)
         if (shadow) {

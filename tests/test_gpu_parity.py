@@ -266,3 +266,24 @@ def test_framebuffer_device_pointer_wraps_in_torch(gpu, tmp_path):
     t.mul_(2.0)  # writes through to the context's buffer
     torch.cuda.synchronize()
     np.testing.assert_array_equal(ctx.framebuffer().reshape(-1), orig * np.float32(2.0))
+
+
+def test_persistent_traversal_deep_tree_spills(gpu, tmp_path, monkeypatch):
+    """A tree deeper than the persistent kernel's 16-entry LDS stack window: entries spill to the
+    global spill area and come back; the image and traversal counters still equal the
+    megakernel's (which keeps the whole stack in LDS)."""
+    xml, ntri = scenegen.bumpy_cbox_xml(str(tmp_path), 700, 250)
+    s = nh.Scene(xml)
+    s.set_resolution(40, 32)
+    b = nh.Bvh(s, n_threads=8)
+    assert b.desc.max_depth > 20, b.desc.max_depth
+    out = []
+    for mode, knob in ((nh.MODE_MEGAKERNEL, "0"), (nh.MODE_WAVEFRONT, "1")):
+        monkeypatch.setenv("NH_PERSISTENT", knob)
+        ctx = nh.Context(0)
+        ctx.upload(s, b)
+        ctx.render(0, 4, seed=21, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=mode, stats=True)
+        out.append((ctx.framebuffer(), ctx.stats()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    for k in ("ray_queries", "nodes_visited", "prims_tested"):
+        assert out[0][1][k] == out[1][1][k], k
