@@ -105,6 +105,7 @@ def roofline(args, calib, st, W, H, R):
       wavefront:  the dominant stage -- wf_shade: path-state bytes; wf_extend: the closest-hit
                   share of nodes/prims + 48 B per query (ray 32 B in, hit 16 B out)"""
     paths = calib["samples"]
+    NODE_BYTES = calib.get("node_bytes") or 64  # 128 when the 4-wide tree was traversed
     if args.mode == "wavefront":
         # dominant stage by measured time
         stage = max(("extend", "shadow", "shade"), key=lambda k: st[f"kernel_ms_{k}"])
@@ -135,6 +136,7 @@ def roofline(args, calib, st, W, H, R):
             "kernel": kernel, "avg_launch_ms": round(avg_ms, 4), "launches": launches,
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "bytes_per_sample": round(bytes_per_sample, 1),
+            "node_bytes": NODE_BYTES,
             "queries_per_sample": round(q / paths, 3),
             "nodes_per_query": round(nodes / max(q, 1), 3),
             "prims_per_query": round(prims / max(q, 1), 3),

@@ -191,7 +191,12 @@ typedef struct nh_hit_soa {
 /* ---- rendering ------------------------------------------------------------ */
 
 enum { NH_MODE_MEGAKERNEL = 0, NH_MODE_WAVEFRONT = 1 };
-enum { NH_TRAVERSAL_REFERENCE = 0, NH_TRAVERSAL_ORDERED = 1 };
+/* Visit orders of BVH::rayIntersect (src/utils/bvh.cpp:402-460); all three return the reference's hit.
+ *   REFERENCE  binary tree, left child first (the reference's order)
+ *   ORDERED    binary tree, nearer child first
+ *   WIDE       4-wide collapse of the same tree (same boxes), nearer child first; nh_render uses it
+ *              for deep trees whenever the traversal is not REFERENCE */
+enum { NH_TRAVERSAL_REFERENCE = 0, NH_TRAVERSAL_ORDERED = 1, NH_TRAVERSAL_WIDE = 2 };
 
 typedef struct nh_render_req {
     int32_t sample_begin;         /* sample rounds [sample_begin, sample_end) */
@@ -227,6 +232,9 @@ typedef struct nh_render_stats {
     /* wavefront mode: the tail kernel that finishes the last few live paths of a chunk in place */
     double kernel_ms_tail;
     uint64_t launches_tail;
+    /* bytes of one BVH node as counted in nodes_visited: 64 (binary tree) or 128 (the 4-wide
+       collapse, NH_TRAVERSAL_WIDE), for the last render */
+    uint64_t node_bytes;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;

@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -41,6 +42,7 @@ struct nh_ctx {
     std::vector<void *> scene_bufs, bvh_bufs;
     bool has_scene = false, has_bvh = false;
     int depth = 0;
+    int depth_wide = 0;  // stack bound of the 4-wide traversal
     int n_node_f4 = 0, n_leaves = 0, n_prim_f4 = 0;  // GPU BVH sizes (float4 / int2 entries)
     std::vector<uint32_t> bvh_indices, shape_offset;
     float *fb = nullptr;
@@ -321,6 +323,71 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     return NH_OK;
 }
 
+// 4-wide collapse of the GPU binary tree (nh_traverse.h Tracer4): every wide node takes the two
+// children of a binary node and, while it has fewer than 4, replaces its largest-area inner child
+// by that child's two children in place (left-first DFS order of the slots is kept). Wide nodes
+// are numbered depth first, the first child next to its parent. Boxes are the binary tree's own.
+static std::vector<float4> collapse_wide(const std::vector<float4> &nodes, const std::vector<int2> &leaves,
+                                         int &depth_out) {
+    struct Child {
+        float mn[3], mx[3];
+        int ref;  // binary: >= 0 inner node, < 0 leaf ~index
+    };
+    auto child = [&](int g, int side) {
+        const float *f = reinterpret_cast<const float *>(&nodes[4 * (size_t)g]);
+        Child ch;
+        const int o = side ? 6 : 0;
+        for (int i = 0; i < 3; ++i) { ch.mn[i] = f[o + i]; ch.mx[i] = f[o + 3 + i]; }
+        int refs[2];
+        std::memcpy(refs, &nodes[4 * (size_t)g + 3], 8);
+        ch.ref = refs[side];
+        return ch;
+    };
+    auto area = [](const Child &c) {
+        const float x = c.mx[0] - c.mn[0], y = c.mx[1] - c.mn[1], z = c.mx[2] - c.mn[2];
+        return x * y + y * z + z * x;
+    };
+    std::vector<float4> wide;
+    depth_out = 0;
+    if (nodes.empty()) return wide;
+    std::function<int(int, int)> make = [&](int g, int depth) -> int {
+        depth_out = std::max(depth_out, depth);
+        const int idx = (int)(wide.size() / nhd::kWideF4);
+        wide.resize(wide.size() + nhd::kWideF4);
+        std::vector<Child> ch{child(g, 0), child(g, 1)};
+        while (ch.size() < 4) {
+            int best = -1;
+            float best_a = -1.f;
+            for (int i = 0; i < (int)ch.size(); ++i)
+                if (ch[i].ref >= 0 && area(ch[i]) > best_a) { best = i; best_a = area(ch[i]); }
+            if (best < 0) break;
+            const int gi = ch[best].ref;
+            ch[best] = child(gi, 1);
+            ch.insert(ch.begin() + best, child(gi, 0));
+        }
+        int refs[4] = {nhd::kWideEmpty, nhd::kWideEmpty, nhd::kWideEmpty, nhd::kWideEmpty};
+        float box[6][4];
+        for (int j = 0; j < 4; ++j)
+            for (int a = 0; a < 3; ++a) { box[a][j] = 0.f; box[3 + a][j] = 0.f; }
+        for (int j = 0; j < (int)ch.size(); ++j) {
+            for (int a = 0; a < 3; ++a) { box[a][j] = ch[j].mn[a]; box[3 + a][j] = ch[j].mx[a]; }
+            if (ch[j].ref >= 0) {
+                refs[j] = make(ch[j].ref, depth + 1);
+            } else {
+                const int2 lf = leaves[(size_t)~ch[j].ref];
+                refs[j] = lf.y > 0 ? ~lf.x : nhd::kWideEmpty;  // an empty leaf holds nothing to hit
+            }
+        }
+        float4 *n = &wide[(size_t)idx * nhd::kWideF4];
+        for (int a = 0; a < 6; ++a) n[a] = make_float4(box[a][0], box[a][1], box[a][2], box[a][3]);
+        std::memcpy(&n[6], refs, 16);
+        n[7] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return idx;
+    };
+    make(0, 1);
+    return wide;
+}
+
 int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     if (!c || !b) return NH_ERR_INVALID;
     if (!c->has_scene) return fail(c, "nh_upload_bvh: upload the scene first"), NH_ERR_STATE;
@@ -411,6 +478,17 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
             p[2] = make_float4(p2[0], p2[1], p2[2], f0);
         }
     }
+    // leaf-end bits: the 4-wide traversal walks a leaf's records until this bit
+    for (const int2 &lf : leaves)
+        if (lf.y > 0) {
+            float4 &w = prims[3 * ((size_t)lf.x + lf.y - 1) + 2];
+            int bits;
+            std::memcpy(&bits, &w.w, 4);
+            bits |= nhd::kPrimLeafEnd;
+            std::memcpy(&w.w, &bits, 4);
+        }
+    int depth4 = 0;
+    const std::vector<float4> wide = collapse_wide(nodes, leaves, depth4);
     int rc;
     c->n_node_f4 = (int)nodes.size();
     c->n_leaves = (int)leaves.size();
@@ -418,6 +496,10 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     if ((rc = upload(c, c->bvh_bufs, nodes.data(), nodes.size(), &c->tv.nodes))) return rc;
     if ((rc = upload(c, c->bvh_bufs, leaves.data(), leaves.size(), &c->tv.leaves))) return rc;
     if ((rc = upload(c, c->bvh_bufs, prims.data(), prims.size(), &c->tv.prims))) return rc;
+    c->tv.wnodes = nullptr;
+    if (!wide.empty() && (rc = upload(c, c->bvh_bufs, wide.data(), wide.size(), &c->tv.wnodes))) return rc;
+    // deferred entries: at most 3 per wide level (+1 slack)
+    c->depth_wide = 3 * depth4 + 1;
     S.nodes = c->tv.nodes;
     S.prims = c->tv.prims;
     c->bvh_indices.assign(b->indices, b->indices + b->n_indices);
@@ -450,8 +532,15 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
     HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.u = (float *)p;
     HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.v = (float *)p;
     HIP_TRY(c, hipMalloc(&p, nn * 4)); tmp.push_back(p); hb.k = (int *)p;
-    nh::launch_trace(c->d_scene, c->tv, rb, hb, n, any_hit != 0, traversal == NH_TRAVERSAL_ORDERED, false, c->depth,
-                     c->counters, c->stream);
+    if (traversal == NH_TRAVERSAL_WIDE && c->tv.wnodes) {
+        HIP_TRY(c, hipMalloc(&p, nn * (size_t)c->depth_wide * sizeof(int2)));
+        tmp.push_back(p);
+        nh::launch_trace_wide(c->d_scene, c->tv, rb, hb, n, any_hit != 0, true, false, (int2 *)p, c->depth_wide,
+                              c->counters, c->stream);
+    } else {
+        nh::launch_trace(c->d_scene, c->tv, rb, hb, n, any_hit != 0, traversal != NH_TRAVERSAL_REFERENCE, false,
+                         c->depth, c->counters, c->stream);
+    }
     HIP_TRY(c, hipGetLastError());
     std::vector<int> k(nn);
     HIP_TRY(c, hipMemcpyAsync(out->hit, hb.hit, nn, hipMemcpyDeviceToHost, c->stream));
@@ -543,7 +632,7 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         L.small_leaves = c->n_leaves;
         L.small_prims = c->n_prim_f4;
     }
-    const bool ordered = q->traversal == NH_TRAVERSAL_ORDERED, stats = q->collect_stats != 0;
+    const bool ordered = q->traversal != NH_TRAVERSAL_REFERENCE, stats = q->collect_stats != 0;
     const int per_chunk = 256;  // wf_shade's chunk
     const int max_chunks = (P.n_paths + per_chunk - 1) / per_chunk;
     L.seg_cap = (max_chunks + kQueueShards - 1) / kQueueShards * per_chunk;
@@ -551,13 +640,20 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     // traverse faster with one ray per lane
     bool persistent = c->depth > 20;
     if (const char *e = std::getenv("NH_PERSISTENT")) persistent = e[0] == '1';
-    if (persistent && c->trav_spill_depth < c->depth) {
+    // the persistent kernels walk the 4-wide collapse of the tree (half the dependent node fetches)
+    // unless the reference's own visit order was asked for
+    bool wide = persistent && ordered && c->tv.wnodes != nullptr;
+    if (const char *e = std::getenv("NH_WIDE")) wide = wide && e[0] != '0';
+    // spill words per lane: binary entries are one word, wide entries two (8-B aligned)
+    const int spill_words = wide ? 2 * c->depth_wide : (c->depth + 1) / 2 * 2;
+    if (persistent && c->trav_spill_depth < spill_words) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         (void)hipFree(c->trav_spill);
         c->trav_spill = nullptr;
-        c->trav_spill_depth = c->depth;
-        HIP_TRY(c, hipMalloc(&c->trav_spill, (size_t)kPersistentBlocks * 128 * c->depth * sizeof(uint32_t)));
+        c->trav_spill_depth = spill_words;
+        HIP_TRY(c, hipMalloc(&c->trav_spill, (size_t)kPersistentBlocks * 128 * spill_words * sizeof(uint32_t)));
     }
+    c->stats.node_bytes = wide ? 16 * nhd::kWideF4 : 64;
     L.trav_spill = c->trav_spill;
     L.spill_depth = c->trav_spill_depth;
     unsigned *slot[2] = {c->wf.counts, c->wf.counts + kCountSlot};
@@ -593,13 +689,13 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         const int bound = (int)in_e[it == 0 ? 0 : it - 1];
         HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), c->stream));
         HIP_TRY(c, hipEventRecord(ev[0], c->stream));
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, persistent, bound, c->depth, c->stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, persistent, wide, bound, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[1], c->stream));
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, persistent, bound, c->depth, c->stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, persistent, wide, bound, c->depth, c->stream);
         HIP_TRY(c, hipEventRecord(ev[2], c->stream));
         tail = it > 0 && (int64_t)bound <= tail_at;
         if (tail) {
-            nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, bound, c->depth, c->stream);
+            nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, wide, bound, c->depth, c->stream);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev[3], c->stream));
             // the last regular bounce's output counts, for the byte accounting below
@@ -724,6 +820,9 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     if (c->integrator == 0 && c->n_emitters == 0) return fail(c, "No Emitter in scene!"), NH_ERR_INVALID;
     if (q->mode != NH_MODE_MEGAKERNEL && q->mode != NH_MODE_WAVEFRONT) return fail(c, "unknown render mode"), NH_ERR_INVALID;
     const bool wavefront = q->mode == NH_MODE_WAVEFRONT;
+    if (q->traversal < NH_TRAVERSAL_REFERENCE || q->traversal > NH_TRAVERSAL_WIDE)
+        return fail(c, "unknown traversal"), NH_ERR_INVALID;
+    c->stats.node_bytes = 64;  // binary tree unless the wavefront picks the 4-wide one
     HIP_TRY(c, hipSetDevice(c->device));
     int rc = ensure_pixel_list(c, q);
     if (rc) return rc;
@@ -809,7 +908,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
             rc = render_wavefront(c, q, L);
             if (rc) return rc;
         } else {
-            nh::launch_path(c->d_scene, c->tv, L, q->traversal == NH_TRAVERSAL_ORDERED, q->collect_stats != 0, c->depth,
+            nh::launch_path(c->d_scene, c->tv, L, q->traversal != NH_TRAVERSAL_REFERENCE, q->collect_stats != 0, c->depth,
                             c->stream);
         }
         HIP_TRY(c, hipGetLastError());

@@ -51,6 +51,9 @@ __device__ __forceinline__ unsigned long long *stat_shard(unsigned long long *c)
 namespace nh {
 void launch_trace(const nhd::DScene *S, const nhd::Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n,
                   bool any, bool ordered, bool stats, int depth, unsigned long long *ctr, hipStream_t st);
+void launch_trace_wide(const nhd::DScene *S, const nhd::Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n,
+                       bool any, bool ordered, bool stats, int2 *spill, int spill_depth, unsigned long long *ctr,
+                       hipStream_t st);
 void launch_path(const nhd::DScene *S, const nhd::Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
                  int depth, hipStream_t st);
 void launch_splat(const SplatLaunch &P, hipStream_t st);
@@ -106,7 +109,8 @@ struct WfLaunch {
     // small scenes: float4 / int2 counts of the BVH arrays staged into LDS by the traversal
     // kernels (0 = traverse from HBM)
     int small_nodes, small_leaves, small_prims;
-    // persistent traversal: per-lane stack spill area (kPersistentBlocks * 128 lanes x spill_depth)
+    // persistent traversal: per-lane stack spill area (kPersistentBlocks * 128 lanes x spill_depth
+    // 32-bit words; the 4-wide traversal spills (ref, distance) pairs)
     uint32_t *trav_spill;
     int spill_depth;
     unsigned long long *counters;
@@ -116,8 +120,8 @@ constexpr int kPersistentBlocks = 256 * 16;
 constexpr size_t kSmallSceneBytes = 16384;
 namespace nh {
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                     bool shadow, bool persistent, int bound, int depth, hipStream_t st);
+                     bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st);
 void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, int bound, hipStream_t st);
 void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                    int bound, int depth, hipStream_t st);
+                    bool wide, int bound, int depth, hipStream_t st);
 }  // namespace nh

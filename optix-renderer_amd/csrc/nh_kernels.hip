@@ -216,6 +216,33 @@ __global__ __launch_bounds__(BLOCK) void nh_trace_kernel(const DScene *__restric
     if (STATS) flush_stats(st, i < n ? 1u : 0u, stat_shard(counters));
 }
 
+// The same entry point over the 4-wide collapse (nh_traverse.h Tracer4), run to completion per
+// lane: LDS window of 16 (ref, distance) entries, deeper entries in the lane's `spill` area.
+template <bool ORDERED, bool ANY, bool STATS>
+__global__ __launch_bounds__(64) void nh_trace_wide_kernel(const DScene *__restrict__ Sp, Traversal tv, RayBatch rb,
+                                                           HitBatch hb, int n, int2 *spill, int spill_depth,
+                                                           unsigned long long *counters) {
+    __shared__ int s_ref[16 * 64];
+    __shared__ float s_near[16 * 64];
+    const DScene &S = *Sp;
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    TravStats st{0, 0, 0};
+    if (i < n) {
+        RingStack2<16> stk{s_ref + threadIdx.x, s_near + threadIdx.x, 64, spill + (size_t)i * spill_depth};
+        Tracer4<ORDERED, ANY, STATS, RingStack2<16>> tr;
+        tr.begin(S, tv, f3(rb.ox[i], rb.oy[i], rb.oz[i]), f3(rb.dx[i], rb.dy[i], rb.dz[i]), rb.mint[i], rb.maxt[i], st);
+        while (!tr.done) tr.step(tv, stk, st);
+        hb.hit[i] = tr.found ? 1 : 0;
+        if (!ANY) {
+            hb.t[i] = tr.found ? tr.best.t : INFINITY;
+            hb.u[i] = tr.found ? tr.best.u : 0.f;
+            hb.v[i] = tr.found ? tr.best.v : 0.f;
+            hb.k[i] = tr.found ? tr.best.k : -1;
+        }
+    }
+    if (STATS) flush_stats(st, i < n ? 1u : 0u, stat_shard(counters));
+}
+
 template <int BLOCK, int DEPTH, bool ORDERED, bool STATS, int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__restrict__ Sp, Traversal tv, PathLaunch L) {
     __shared__ uint32_t stk[DEPTH * BLOCK];
@@ -408,6 +435,23 @@ void launch_trace(const DScene *S, const Traversal &tv, const RayBatch &rb, cons
     else if (depth <= 32) launch_trace_d<128, 32>(S, tv, rb, hb, n, any, ordered, stats, ctr, st);
     else if (depth <= 64) launch_trace_d<64, 64>(S, tv, rb, hb, n, any, ordered, stats, ctr, st);
     else launch_trace_d<64, 128>(S, tv, rb, hb, n, any, ordered, stats, ctr, st);
+}
+
+void launch_trace_wide(const DScene *S, const Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n, bool any,
+                       bool ordered, bool stats, int2 *spill, int spill_depth, unsigned long long *ctr,
+                       hipStream_t st) {
+    if (n <= 0) return;
+    dim3 grid((n + 63) / 64);
+#define NH_TW(O, A, T) \
+    hipLaunchKernelGGL((nh_trace_wide_kernel<O, A, T>), grid, dim3(64), 0, st, S, tv, rb, hb, n, spill, spill_depth, ctr)
+    if (ordered) {
+        if (any) { if (stats) NH_TW(true, true, true); else NH_TW(true, true, false); }
+        else { if (stats) NH_TW(true, false, true); else NH_TW(true, false, false); }
+    } else {
+        if (any) { if (stats) NH_TW(false, true, true); else NH_TW(false, true, false); }
+        else { if (stats) NH_TW(false, false, true); else NH_TW(false, false, false); }
+    }
+#undef NH_TW
 }
 
 template <int BLOCK, int DEPTH, int MINW>

@@ -107,7 +107,12 @@ struct Traversal {
     const float4 *nodes;
     const int2 *leaves;
     const float4 *prims;
+    const float4 *wnodes;  // 4-wide collapse of the same tree (kWideF4 float4 per node), see Tracer4
 };
+
+// primitive record type / leaf-end bits (word 2 .w of the record)
+constexpr int kPrimSphere = 1, kPrimLeafEnd = 2;
+NHD bool prim_is_tri(float4 c) { return (__float_as_int(c.w) & kPrimSphere) == 0; }
 
 // Test the primitives of one leaf. Returns true when an any-hit query is answered.
 template <bool ANY, bool STATS>
@@ -118,7 +123,7 @@ NHD bool leaf_test(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float 
         const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
         if (STATS) st.prims++;
         float t, u = 0.f, v = 0.f;
-        bool hit = (__float_as_int(c.w) == 0) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
+        bool hit = prim_is_tri(c) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
                                               : sphere_test(a, o, d, mint, maxt, t);
         if (!hit) continue;
         if (ANY) return true;
@@ -292,7 +297,7 @@ struct Tracer {
             const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
             if (STATS) st.prims++;
             float t, u = 0.f, v = 0.f;
-            const bool hit = (__float_as_int(c.w) == 0) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
+            const bool hit = prim_is_tri(c) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
                                                         : sphere_test(a, o, d, mint, maxt, t);
             if (hit) {
                 if (ANY) {
@@ -358,6 +363,182 @@ struct Tracer {
             const int2 lf = tv.leaves[~ref];
             k = lf.x;
             kend = lf.x + lf.y;
+            cur = -1;
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// 4-wide traversal of the same tree. nh_api.hip collapses the reference's binary tree: a wide
+// node's children are binary descendants (an inner child is replaced by its two children, the
+// largest-area one first, until there are 4), in left-first DFS order, with the descendants'
+// own boxes -- no new boxes. Skipping the boxes of the collapsed intermediate nodes changes no
+// result: a descendant's box lies inside its ancestor's (the reference builds every box as the
+// union of its primitives), and the slab arithmetic is monotone in the bounds, so the rounded
+// [near, far] of a descendant lies inside its ancestor's -- whenever the descendant passes
+// `mint <= far && near <= maxt`, the skipped ancestor would have passed too (with the same or a
+// larger maxt, since maxt only shrinks). Leaves are primitive ranges ending at the record whose
+// kPrimLeafEnd bit is set (no leaf-table fetch).
+//
+// Wide node (128 B, one cache line) = 8 x float4:
+//   [0..5] min.x[4], min.y[4], min.z[4], max.x[4], max.y[4], max.z[4] of the 4 child slots
+//   [6]    int4 child refs: >= 0 wide node, kWideEmpty unused slot, else leaf ~first primitive
+//   [7]    unused
+constexpr int kWideF4 = 8;
+constexpr int kWideEmpty = (int)0x80000000;
+
+// Traversal stack of one lane, (ref, entry distance) pairs: the top K entries live in LDS
+// (lane-interleaved, `stride` words apart), deeper entries spill to the lane's own global area.
+template <int K>
+struct RingStack2 {
+    static_assert((K & (K - 1)) == 0, "K must be a power of two");
+    int *lds_ref;      // this lane's first LDS slot (refs)
+    float *lds_near;   // this lane's first LDS slot (entry distances)
+    int stride;
+    int2 *glob;        // this lane's spill area
+    NHD void push(int i, int ref, float nr) {
+        const int o = (i & (K - 1)) * stride;
+        if (i >= K) glob[i - K] = make_int2(lds_ref[o], __float_as_int(lds_near[o]));
+        lds_ref[o] = ref;
+        lds_near[o] = nr;
+    }
+    NHD void pop(int i, int &ref, float &nr) {
+        const int o = (i & (K - 1)) * stride;
+        ref = lds_ref[o];
+        nr = lds_near[o];
+        if (i >= K) {
+            const int2 e = glob[i - K];
+            lds_ref[o] = e.x;
+            lds_near[o] = __int_as_float(e.y);
+        }
+    }
+};
+
+// ORDERED: nearer first, equal distances in slot (= left-first DFS) order; REFERENCE: slot order
+template <bool ORDERED>
+NHD bool wide_before(bool va, float na, int sa, bool vb, float nb, int sb) {
+    if (!va) return false;
+    if (!vb) return true;
+    if (ORDERED && na != nb) return na < nb;
+    return sa < sb;
+}
+
+// Resumable 4-wide traversal (same step protocol as Tracer: one wide node, one primitive or one
+// stack pop per step). Answers: smallest t, ties to the largest leaf-order position k.
+template <bool ORDERED, bool ANY, bool STATS, class Stack>
+struct Tracer4 {
+    F3 o, d, r;
+    float mint, maxt;
+    int cur;  // wide node to visit next, or -1
+    int k;    // primitive under test, or -1
+    int sp;
+    bool found, done;
+    Hit best;
+
+    NHD void begin(const DScene &S, const Traversal &tv, F3 o_, F3 d_, float mint_, float maxt_, TravStats &st) {
+        o = o_;
+        d = d_;
+        mint = mint_;
+        maxt = maxt_;
+        // adaptive ray epsilon (bvh.cpp:407-410)
+        if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));
+        best.k = -1;
+        best.t = INFINITY;
+        found = false;
+        done = true;
+        sp = 0;
+        cur = -1;
+        k = -1;
+        if (S.root_kind == 0 || maxt < mint) return;
+        r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        float near_t;
+        if (STATS) st.boxes++;
+        if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d,
+                      r, mint, maxt, near_t))
+            return;
+        done = false;
+        if (S.root_kind == 2) k = tv.leaves[0].x;  // a single leaf: records up to the leaf-end bit
+        else cur = 0;
+    }
+
+    NHD void step(const Traversal &tv, Stack &stk, TravStats &st) {
+        if (k >= 0) {  // one primitive of the current leaf
+            const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
+            if (STATS) st.prims++;
+            float t, u = 0.f, v = 0.f;
+            const bool hit = prim_is_tri(c) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
+                                            : sphere_test(a, o, d, mint, maxt, t);
+            if (hit) {
+                if (ANY) {
+                    found = true;
+                    done = true;
+                    return;
+                }
+                if (t < maxt || k > best.k) {
+                    found = true;
+                    maxt = t;
+                    best.t = t;
+                    best.u = u;
+                    best.v = v;
+                    best.k = k;
+                }
+            }
+            k = (__float_as_int(c.w) & kPrimLeafEnd) ? -1 : k + 1;
+            return;
+        }
+        if (cur >= 0) {  // one wide node: test its child boxes
+            const float4 *n = tv.wnodes + (size_t)kWideF4 * cur;
+            const float4 mnx = n[0], mny = n[1], mnz = n[2], mxx = n[3], mxy = n[4], mxz = n[5];
+            const int4 ref = *reinterpret_cast<const int4 *>(&n[6]);
+            float n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f;
+            bool v0 = ref.x != kWideEmpty && box_test(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, d, r, mint, maxt, n0);
+            bool v1 = ref.y != kWideEmpty && box_test(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, d, r, mint, maxt, n1);
+            bool v2 = ref.z != kWideEmpty && box_test(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, d, r, mint, maxt, n2);
+            bool v3 = ref.w != kWideEmpty && box_test(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, d, r, mint, maxt, n3);
+            if (STATS) {
+                st.nodes++;
+                st.boxes += (ref.x != kWideEmpty) + (ref.y != kWideEmpty) + (ref.z != kWideEmpty) + (ref.w != kWideEmpty);
+            }
+            int r0 = ref.x, r1 = ref.y, r2 = ref.z, r3 = ref.w;
+            int s0 = 0, s1 = 1, s2 = 2, s3 = 3;
+            // 4-element sorting network (0,1)(2,3)(0,2)(1,3)(1,2) on (valid, near, slot)
+#define NH_CX(A, B)                                                                           \
+    if (wide_before<ORDERED>(v##B, n##B, s##B, v##A, n##A, s##A)) {                          \
+        bool tv_ = v##A; v##A = v##B; v##B = tv_;                                              \
+        float tn_ = n##A; n##A = n##B; n##B = tn_;                                             \
+        int tr_ = r##A; r##A = r##B; r##B = tr_;                                               \
+        int ts_ = s##A; s##A = s##B; s##B = ts_;                                               \
+    }
+            NH_CX(0, 1) NH_CX(2, 3) NH_CX(0, 2) NH_CX(1, 3) NH_CX(1, 2)
+#undef NH_CX
+            if (!v0) {
+                cur = -1;
+                return;
+            }
+            // the nearest child is entered, the others are deferred (farthest pushed first)
+            if (v3) stk.push(sp++, r3, n3);
+            if (v2) stk.push(sp++, r2, n2);
+            if (v1) stk.push(sp++, r1, n1);
+            enter(r0);
+            return;
+        }
+        if (sp > 0) {  // one deferred child: the visit-time test against the current maxt
+            int ref;
+            float nr;
+            stk.pop(--sp, ref, nr);
+            // its box passed with a larger-or-equal maxt; mint <= far does not depend on maxt
+            if (STATS) st.boxes++;
+            if (nr <= maxt) enter(ref);
+            return;
+        }
+        done = true;
+    }
+
+    NHD void enter(int ref) {
+        if (ref >= 0) {
+            cur = ref;
+        } else {
+            k = ~ref;
             cur = -1;
         }
     }

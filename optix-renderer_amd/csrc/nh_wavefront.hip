@@ -222,7 +222,55 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
 constexpr int kFetchBatch = 64;
 constexpr int kTraceBlocksMax = 1 << 20;
 constexpr int kRingEntries = 16;
-template <int DEPTH, bool ORDERED, bool ANY, bool STATS>
+//
+// WIDE: the 4-wide collapse of the tree (Tracer4), LDS window of 8 (ref, distance) pairs per lane.
+template <bool WIDE>
+struct PtStack {
+    using type = RingStack<kRingEntries>;
+    static __device__ __forceinline__ type make(uint32_t *lds, const WfLaunch &L) {
+        type s;
+        s.lds = lds + threadIdx.x;
+        s.stride = 128;
+        s.glob = L.trav_spill + ((size_t)blockIdx.x * 128 + threadIdx.x) * (size_t)L.spill_depth;
+        return s;
+    }
+};
+template <>
+struct PtStack<true> {
+    using type = RingStack2<kRingEntries / 2>;
+    static __device__ __forceinline__ type make(uint32_t *lds, const WfLaunch &L) {
+        type s;
+        s.lds_ref = reinterpret_cast<int *>(lds) + threadIdx.x;
+        s.lds_near = reinterpret_cast<float *>(lds + kRingEntries / 2 * 128) + threadIdx.x;
+        s.stride = 128;
+        s.glob = reinterpret_cast<int2 *>(L.trav_spill + ((size_t)blockIdx.x * 128 + threadIdx.x) * (size_t)L.spill_depth);
+        return s;
+    }
+};
+template <bool WIDE, bool ORDERED, bool ANY, bool STATS, class Stk>
+struct PtTracer { using type = Tracer<ORDERED, ANY, STATS, Stk>; };
+template <bool ORDERED, bool ANY, bool STATS, class Stk>
+struct PtTracer<true, ORDERED, ANY, STATS, Stk> { using type = Tracer4<ORDERED, ANY, STATS, Stk>; };
+
+// one traversal run to completion by this lane (tail kernel): binary tree with the whole stack in
+// LDS (stk: DEPTH x 128 words), or the 4-wide tree with the persistent kernels' LDS window + spill
+template <bool WIDE, int DEPTH, bool ORDERED, bool ANY, bool STATS>
+__device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S, const WfLaunch &L, F3 o, F3 d,
+                                           float mint, float maxt, Hit &h, uint32_t *stk, TravStats &st) {
+    if constexpr (WIDE) {
+        using Stk = typename PtStack<true>::type;
+        Stk s = PtStack<true>::make(stk, L);
+        Tracer4<ORDERED, ANY, STATS, Stk> tr;
+        tr.begin(S, tv, o, d, mint, maxt, st);
+        while (!tr.done) tr.step(tv, s, st);
+        h = tr.best;
+        return tr.found;
+    } else {
+        return trace<DEPTH, ORDERED, ANY, STATS>(tv, S, o, d, mint, maxt, h, stk + threadIdx.x, 128, st);
+    }
+}
+
+template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool WIDE>
 __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[kRingEntries * 128];
     const DScene &S = *Sp;
@@ -232,14 +280,12 @@ __global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp
     unsigned *fetch = L.cnt_in + (ANY ? 3 : 2) * kCountGroup;
     const WfBuf &B = L.st.buf[L.in_q];
     const int lane = threadIdx.x & 63;
-    RingStack<kRingEntries> my_stk;
-    my_stk.lds = stk + threadIdx.x;
-    my_stk.stride = 128;
-    my_stk.glob = L.trav_spill + ((size_t)blockIdx.x * 128 + threadIdx.x) * (size_t)L.spill_depth;
+    using Stk = typename PtStack<WIDE>::type;
+    Stk my_stk = PtStack<WIDE>::make(stk, L);
     int seg = blockIdx.x & (kQueueShards - 1), tried = 0;
     int batch_next = 0, batch_end = 0;  // wave-uniform
     int slot = -1;                      // this lane's ray (queue slot), -1 = idle
-    Tracer<ORDERED, ANY, STATS, RingStack<kRingEntries>> tr;
+    typename PtTracer<WIDE, ORDERED, ANY, STATS, Stk>::type tr;
     TravStats st{0, 0, 0};
     unsigned long long queries = 0;
     for (;;) {
@@ -510,7 +556,7 @@ __global__ __launch_bounds__(256, 4) void wf_shade(const DScene *__restrict__ Sp
 // of a bounce whose extend / any-hit traversals are done and finishes every path in place, one
 // thread per path: shade, then its next closest-hit and shadow traversals, until it terminates --
 // the same operations in the same order as further wavefront bounces.
-template <int DEPTH, bool ORDERED, bool STATS, bool SMALL>
+template <int DEPTH, bool ORDERED, bool STATS, bool SMALL, bool WIDE>
 __global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
     extern __shared__ float4 lds_scene[];
@@ -531,14 +577,14 @@ __global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Tr
             Hit h;
             const bool live = o.rd.w >= o.ro.w;
             q_e += live ? 1 : 0;
-            const bool found = live && trace<DEPTH, ORDERED, false, STATS>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w,
-                                                                           o.rd.w, h, stk + threadIdx.x, 128, st_e);
+            const bool found = live && trace_lane<WIDE, DEPTH, ORDERED, false, STATS>(tv, S, L, xyz(o.ro), xyz(o.rd),
+                                                                                      o.ro.w, o.rd.w, h, stk, st_e);
             B.hit[s] = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
             if (nee) {
                 ++q_s;
                 Hit hs;
-                B.occl[s] = trace<DEPTH, ORDERED, true, STATS>(tv, S, xyz(so), xyz(sd), so.w, sd.w, hs,
-                                                               stk + threadIdx.x, 128, st_s)
+                B.occl[s] = trace_lane<WIDE, DEPTH, ORDERED, true, STATS>(tv, S, L, xyz(so), xyz(sd), so.w, sd.w, hs,
+                                                                          stk, st_s)
                                 ? 1
                                 : 0;
             }
@@ -555,13 +601,17 @@ namespace nh {
 
 template <int DEPTH>
 static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                              bool shadow, bool persistent, int bound, hipStream_t st) {
+                              bool shadow, bool persistent, bool wide, int bound, hipStream_t st) {
     // the queue length is only known on the device: size the grid from the host's upper bound
     // (the kernels stride over whatever the device count says)
     const int want = std::max(1, (bound + 127) / 128);
     const dim3 grid(std::min(want, persistent ? kPersistentBlocks : kTraceBlocksMax));
     if (persistent) {
-#define NH_PT(A, O, T) hipLaunchKernelGGL((wf_trace_pt<DEPTH, O, A, T>), grid, dim3(128), 0, st, S, tv, L)
+#define NH_PT(A, O, T)                                                                               \
+    do {                                                                                             \
+        if (wide) hipLaunchKernelGGL((wf_trace_pt<DEPTH, O, A, T, true>), grid, dim3(128), 0, st, S, tv, L); \
+        else hipLaunchKernelGGL((wf_trace_pt<DEPTH, O, A, T, false>), grid, dim3(128), 0, st, S, tv, L);     \
+    } while (0)
         if (shadow) {
             if (ordered) { if (stats) NH_PT(true, true, true); else NH_PT(true, true, false); }
             else { if (stats) NH_PT(true, false, true); else NH_PT(true, false, false); }
@@ -589,34 +639,37 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
 }
 
 void launch_wf_trace(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool shadow,
-                     bool persistent, int bound, int depth, hipStream_t st) {
-    if (depth <= 16) launch_wf_trace_d<16>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
-    else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
-    else if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
-    else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, persistent, bound, st);
+                     bool persistent, bool wide, int bound, int depth, hipStream_t st) {
+    if (depth <= 16) launch_wf_trace_d<16>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
+    else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
+    else if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
+    else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
 }
 
 template <int DEPTH>
 static void launch_wf_tail_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                             int bound, hipStream_t st) {
-    const dim3 grid(std::max(1, (bound + 127) / 128));
+                             bool wide, int bound, hipStream_t st) {
+    // grid-stride; the wide variant's lanes own spill areas of the persistent grid's size
+    const dim3 grid(std::min(std::max(1, (bound + 127) / 128), wide ? kPersistentBlocks : kTraceBlocksMax));
     const bool small = DEPTH == 16 && L.small_nodes + L.small_prims > 0;
     const size_t lds = small ? 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves : 0;
-#define NH_TL2(O, T, SM) hipLaunchKernelGGL((wf_tail<DEPTH, O, T, SM>), grid, dim3(128), lds, st, S, tv, L)
-#define NH_TL(O, T) { if constexpr (DEPTH == 16) { if (small) NH_TL2(O, T, true); else NH_TL2(O, T, false); } \
-                      else NH_TL2(O, T, false); }
+#define NH_TL2(O, T, SM, W) hipLaunchKernelGGL((wf_tail<DEPTH, O, T, SM, W>), grid, dim3(128), lds, st, S, tv, L)
+#define NH_TL(O, T) { if constexpr (DEPTH == 16) { if (small) NH_TL2(O, T, true, false); \
+                                                   else if (wide) NH_TL2(O, T, false, true); \
+                                                   else NH_TL2(O, T, false, false); } \
+                      else { if (wide) NH_TL2(O, T, false, true); else NH_TL2(O, T, false, false); } }
     if (ordered) { if (stats) NH_TL(true, true) else NH_TL(true, false) }
     else { if (stats) NH_TL(false, true) else NH_TL(false, false) }
 #undef NH_TL2
 #undef NH_TL
 }
 
-void launch_wf_tail(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
-                    int depth, hipStream_t st) {
-    if (depth <= 16) launch_wf_tail_d<16>(S, tv, L, ordered, stats, bound, st);
-    else if (depth <= 32) launch_wf_tail_d<32>(S, tv, L, ordered, stats, bound, st);
-    else if (depth <= 64) launch_wf_tail_d<64>(S, tv, L, ordered, stats, bound, st);
-    else launch_wf_tail_d<128>(S, tv, L, ordered, stats, bound, st);
+void launch_wf_tail(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool wide,
+                    int bound, int depth, hipStream_t st) {
+    if (depth <= 16) launch_wf_tail_d<16>(S, tv, L, ordered, stats, wide, bound, st);
+    else if (depth <= 32) launch_wf_tail_d<32>(S, tv, L, ordered, stats, wide, bound, st);
+    else if (depth <= 64) launch_wf_tail_d<64>(S, tv, L, ordered, stats, wide, bound, st);
+    else launch_wf_tail_d<128>(S, tv, L, ordered, stats, wide, bound, st);
 }
 
 

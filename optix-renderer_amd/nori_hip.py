@@ -31,7 +31,7 @@ BSDF_DIFFUSE, BSDF_MIRROR, BSDF_DIELECTRIC, BSDF_MICROFACET = 0, 1, 2, 3
 EMITTER_AREA, EMITTER_POINT, EMITTER_ENVMAP = 0, 1, 2
 INTEGRATOR_PATH_MIS, INTEGRATOR_PATH_MATS = 0, 1
 MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1
-TRAVERSAL_REFERENCE, TRAVERSAL_ORDERED = 0, 1
+TRAVERSAL_REFERENCE, TRAVERSAL_ORDERED, TRAVERSAL_WIDE = 0, 1, 2
 
 _f = C.c_float
 _i32 = C.c_int32
@@ -117,7 +117,8 @@ class nh_render_stats(C.Structure):
                 ("shadow_nodes_visited", C.c_uint64), ("shadow_boxes_tested", C.c_uint64),
                 ("shadow_prims_tested", C.c_uint64), ("shade_state_bytes", C.c_uint64),
                 ("extend_queue_bytes", C.c_uint64), ("shadow_queue_bytes", C.c_uint64),
-                ("paths_shaded", C.c_uint64), ("kernel_ms_tail", C.c_double), ("launches_tail", C.c_uint64)]
+                ("paths_shaded", C.c_uint64), ("kernel_ms_tail", C.c_double), ("launches_tail", C.c_uint64),
+                ("node_bytes", C.c_uint64)]
 
 
 def _sig(name, res, *args):

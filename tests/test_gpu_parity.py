@@ -76,7 +76,11 @@ def setup(xml, width=None, height=None):
     return s, b, ctx
 
 
-@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED])
+TRAVERSALS = [pytest.param(nh.TRAVERSAL_REFERENCE, id="reference"), pytest.param(nh.TRAVERSAL_ORDERED, id="ordered"),
+              pytest.param(nh.TRAVERSAL_WIDE, id="wide")]
+
+
+@pytest.mark.parametrize("traversal", TRAVERSALS)
 def test_trace_parity_cbox(gpu, scene_dir, traversal):
     s, b, ctx = setup(os.path.join(scene_dir, "scenes/pa4/cbox/cbox_path_mis.xml"))
     orc = no.OracleScene(s)
@@ -85,7 +89,7 @@ def test_trace_parity_cbox(gpu, scene_dir, traversal):
     compare_trace(ctx, orc, *secondary_rays(orc, 20000, 11), traversal)
 
 
-@pytest.mark.parametrize("traversal", [nh.TRAVERSAL_REFERENCE, nh.TRAVERSAL_ORDERED])
+@pytest.mark.parametrize("traversal", TRAVERSALS)
 def test_trace_parity_bumpy_mesh(gpu, tmp_path, traversal):
     xml, ntri = scenegen.bumpy_cbox_xml(str(tmp_path), 200, 100)
     assert ntri > 30000
@@ -211,12 +215,14 @@ def test_render_parity_envmap(gpu, tmp_path, texture, integrator, mode):
     assert nh.to_rgb(r, s.border).mean() > 0.05
 
 
-@pytest.mark.parametrize("knob", ["NH_PERSISTENT=1", "NH_PERSISTENT=0", "NH_LDS_SCENE=0", "NH_TAIL=0", "NH_TAIL=1000000"])
+@pytest.mark.parametrize("knob", ["NH_PERSISTENT=1", "NH_PERSISTENT=1,NH_WIDE=0", "NH_PERSISTENT=0",
+                                  "NH_LDS_SCENE=0", "NH_TAIL=0", "NH_TAIL=1000000", "NH_PERSISTENT=1,NH_TAIL=1000000"])
 def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
     """The traversal variants the wavefront picks per scene (persistent ray-fetching traversal for
-    deep BVHs, per-lane traversal, LDS-staged small BVHs) all give the megakernel's framebuffer
-    bit for bit, on a microfacet mesh (deep BVH) and on the Cornell box (LDS-sized BVH)."""
-    name, val = knob.split("=")
+    deep BVHs over the binary or the 4-wide tree, per-lane traversal, LDS-staged small BVHs) all give
+    the megakernel's framebuffer bit for bit, on a microfacet mesh (deep BVH) and on the Cornell box
+    (LDS-sized BVH). Binary-tree variants also visit exactly the megakernel's nodes and primitives."""
+    knobs = [k.split("=") for k in knob.split(",")]
     for xml in (scenegen.bumpy_cbox_xml(str(tmp_path), 160, 80)[0], scenegen.cbox_xml(str(tmp_path), "c1")):
         s = nh.Scene(xml)
         s.set_resolution(48, 40)
@@ -224,13 +230,19 @@ def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
         ref = nh.Context(0)
         ref.upload(s, b)
         ref.render(0, 6, seed=11, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_MEGAKERNEL, stats=True)
-        monkeypatch.setenv(name, val)
+        for name, val in knobs:
+            monkeypatch.setenv(name, val)
         ctx = nh.Context(0)
         ctx.upload(s, b)
         ctx.render(0, 6, seed=11, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT, stats=True)
-        monkeypatch.delenv(name)
+        for name, _ in knobs:
+            monkeypatch.delenv(name)
         np.testing.assert_array_equal(ref.framebuffer(), ctx.framebuffer())
-        for k in ("ray_queries", "nodes_visited", "prims_tested"):
+        wide = ctx.stats()["node_bytes"] == 128
+        env = dict(knobs)
+        persistent = env["NH_PERSISTENT"] == "1" if "NH_PERSISTENT" in env else b.desc.max_depth + 2 > 20
+        assert wide == (persistent and env.get("NH_WIDE") != "0"), xml
+        for k in ("ray_queries",) if wide else ("ray_queries", "nodes_visited", "prims_tested"):
             assert ref.stats()[k] == ctx.stats()[k], (xml, k)
 
 
@@ -277,6 +289,7 @@ def test_persistent_traversal_deep_tree_spills(gpu, tmp_path, monkeypatch):
     s.set_resolution(40, 32)
     b = nh.Bvh(s, n_threads=8)
     assert b.desc.max_depth > 20, b.desc.max_depth
+    monkeypatch.setenv("NH_WIDE", "0")
     out = []
     for mode, knob in ((nh.MODE_MEGAKERNEL, "0"), (nh.MODE_WAVEFRONT, "1")):
         monkeypatch.setenv("NH_PERSISTENT", knob)
@@ -287,3 +300,26 @@ def test_persistent_traversal_deep_tree_spills(gpu, tmp_path, monkeypatch):
     np.testing.assert_array_equal(out[0][0], out[1][0])
     for k in ("ray_queries", "nodes_visited", "prims_tested"):
         assert out[0][1][k] == out[1][1][k], k
+
+
+def test_wide_traversal_deep_tree(gpu, tmp_path, monkeypatch):
+    """The 4-wide collapse on a deep tree (stack deeper than its 8-entry LDS window, so entries
+    spill): closest and any hit bit-exact against the oracle's binary traversal, and the persistent
+    wavefront render over it equals the megakernel's image bit for bit."""
+    xml, ntri = scenegen.bumpy_cbox_xml(str(tmp_path), 700, 250)
+    s = nh.Scene(xml)
+    s.set_resolution(40, 32)
+    b = nh.Bvh(s, n_threads=8)
+    ctx = nh.Context(0)
+    ctx.upload(s, b)
+    orc = no.OracleScene(s)
+    compare_trace(ctx, orc, *random_rays(20000, -0.6, 1.2, 13), nh.TRAVERSAL_WIDE)
+    compare_trace(ctx, orc, *secondary_rays(orc, 20000, 17), nh.TRAVERSAL_WIDE)
+    ctx.render(0, 4, seed=21, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_MEGAKERNEL, stats=True)
+    ref, q = ctx.framebuffer(), ctx.stats()["ray_queries"]
+    monkeypatch.setenv("NH_PERSISTENT", "1")
+    ctx.reset_stats()
+    ctx.render(0, 4, seed=21, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT, stats=True)
+    assert ctx.stats()["node_bytes"] == 128
+    assert ctx.stats()["ray_queries"] == q
+    np.testing.assert_array_equal(ref, ctx.framebuffer())
