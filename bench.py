@@ -8,8 +8,10 @@ diffuse), 1024x1024, 256 spp, path_mis, per-path pcg32 seeding. One step = `--ro
 (generate, then extend / any-hit / shade per bounce until no path is alive) or, with
 --mode megakernel, one path-kernel launch; then one ImageBlock splat. The default K=16 steps
 render the full 256 spp. Multi-GPU: one process per GPU (torchrun), 32x32 image blocks dealt
-round-robin to ranks (tile shard, fixed total image => strong scaling), one RCCL reduce (sum)
-of the RGBW framebuffer to rank 0 inside the timed region.
+round-robin to ranks (tile shard); a step is `--rounds` x N sample rounds over each rank's 1/N
+of the blocks, so every GPU traces the same 16.7M samples per step at any N (weak scaling: at N
+GPUs the K steps render N x K x rounds spp of the same image); one RCCL reduce (sum) of the RGBW
+framebuffer to rank 0 inside the timed region.
 
 The JSON line also carries:
   roofline      the dominant kernel (largest summed HIP-event time on the context's stream):
@@ -208,7 +210,8 @@ def main():
     blocks = nh.tile_shard(W, H, world, rank) if world > 1 else None
     trav = nh.TRAVERSAL_ORDERED if args.traversal == "ordered" else nh.TRAVERSAL_REFERENCE
     mode = nh.MODE_WAVEFRONT if args.mode == "wavefront" else nh.MODE_MEGAKERNEL
-    R = args.rounds
+    # rounds per step and rank: each rank's 1/N of the image for N x --rounds rounds (weak scaling)
+    R = args.rounds * world
 
     # calibration launch (in-kernel counters; same seeds as the first timed step)
     calib = None
@@ -271,7 +274,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference Cornell box scene files, per-path pcg32 seeds)",

@@ -666,7 +666,9 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
     // per-bounce totals: in_e / in_s = live paths / shadow rays entering the bounce
     std::vector<uint64_t> in_e{(uint64_t)P.n_paths}, in_s{0};
     // below this many live paths the rest of the chunk runs in one wf_tail launch
-    int64_t tail_at = std::max<int64_t>(P.n_paths / 256, 8192);  // measured optimum on C2: 64k-128k of 16.7M
+    // measured on 16.7M-path chunks: C2 3025 / 3030 / 2692 Msamples/s at 64k / 262k / 1M,
+    // bumpy-1M 708 / 744 / 739 / 603 at 64k / 262k / 1M / 3M
+    int64_t tail_at = std::max<int64_t>(P.n_paths / 64, 8192);
     if (const char *e = std::getenv("NH_TAIL")) tail_at = std::atoll(e);
     bool tail = false;
     int it = 0;

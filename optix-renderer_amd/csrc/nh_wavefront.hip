@@ -599,6 +599,22 @@ __global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Tr
 namespace nh {
 
 
+// Persistent grids hold exactly the workgroups that are resident at once (occupancy of this
+// instantiation x CUs, at most kPersistentBlocks -- the spill area's size): a workgroup that
+// waits for a free slot would find the pool drained by the time it starts, or leave a tail.
+template <auto KERN>
+static void launch_persistent(int want, hipStream_t st, const DScene *S, const Traversal &tv, const WfLaunch &L) {
+    static const int resident = [] {
+        int per_cu = 0, dev = 0, n_cu = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, KERN, 128, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+        return std::min(kPersistentBlocks, per_cu * std::max(n_cu, 1));
+    }();
+    hipLaunchKernelGGL(KERN, dim3(std::min(want, resident)), dim3(128), 0, st, S, tv, L);
+}
+
 template <int DEPTH>
 static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                               bool shadow, bool persistent, bool wide, int bound, hipStream_t st) {
@@ -609,8 +625,8 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
     if (persistent) {
 #define NH_PT(A, O, T)                                                                               \
     do {                                                                                             \
-        if (wide) hipLaunchKernelGGL((wf_trace_pt<DEPTH, O, A, T, true>), grid, dim3(128), 0, st, S, tv, L); \
-        else hipLaunchKernelGGL((wf_trace_pt<DEPTH, O, A, T, false>), grid, dim3(128), 0, st, S, tv, L);     \
+        if (wide) launch_persistent<wf_trace_pt<DEPTH, O, A, T, true>>(want, st, S, tv, L);              \
+        else launch_persistent<wf_trace_pt<DEPTH, O, A, T, false>>(want, st, S, tv, L);                  \
     } while (0)
         if (shadow) {
             if (ordered) { if (stats) NH_PT(true, true, true); else NH_PT(true, true, false); }
