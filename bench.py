@@ -57,6 +57,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-calibrate", action="store_true")
+    p.add_argument("--pools", type=int, default=2,
+                   help="wavefront path pools in flight (2: a chunk's last bounces overlap the next chunk)")
+    p.add_argument("--roofline-steps", type=int, default=4,
+                   help="with --pools > 1: steps of the serialized pass that times the kernels for the roofline")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (production); gloo = host-side reduce, for rehearsing the "
@@ -212,6 +216,7 @@ def main():
     mode = nh.MODE_WAVEFRONT if args.mode == "wavefront" else nh.MODE_MEGAKERNEL
     # rounds per step and rank: each rank's 1/N of the image for N x --rounds rounds (weak scaling)
     R = args.rounds * world
+    os.environ["NH_POOLS"] = str(args.pools)
 
     # calibration launch (in-kernel counters; same seeds as the first timed step)
     calib = None
@@ -255,6 +260,19 @@ def main():
         elapsed = float(t.item())
     st = ctx.stats()
     total_samples = W * H * R * args.steps
+    roof_pass = None
+    if args.mode == "wavefront" and args.pools > 1 and calib is not None and args.roofline_steps > 0:
+        # Kernels of overlapping pools share the GPU, so their event durations are no kernel roofline:
+        # time the kernels in a serialized pass (one pool) over the same workload instead.
+        os.environ["NH_POOLS"] = "1"
+        ctx.reset_stats()
+        base = R * (args.steps + args.warmup)
+        for s in range(args.roofline_steps):
+            ctx.render(base + s * R, base + (s + 1) * R, seed=args.seed, blocks=blocks, traversal=trav, mode=mode)
+        ctx.synchronize()
+        st = ctx.stats()
+        roof_pass = f"serialized pass: {args.roofline_steps} steps with one path pool (kernels alone on the GPU)"
+        os.environ["NH_POOLS"] = str(args.pools)
 
     if rank == 0:
         value = total_samples / elapsed / 1e6
@@ -262,6 +280,7 @@ def main():
         roof = None
         if calib is not None and calib["samples"] > 0:
             roof = roofline(args, calib, st, W, H, R)
+            roof["timed"] = roof_pass or "the timed region"
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(scene, args.cpu_seconds, args.seed)
@@ -280,7 +299,7 @@ def main():
             "data": "synthetic (reference Cornell box scene files, per-path pcg32 seeds)",
             "config": {"workload": f"{scene_desc}, {R * args.steps} spp, path_mis", "config": args.config,
                        "width": W, "height": H, "spp": R * args.steps, "rounds_per_step": R,
-                       "mode": args.mode, "traversal": args.traversal,
+                       "mode": args.mode, "traversal": args.traversal, "pools": args.pools,
                        "parallelism": f"tile-shard x{world} + RCCL reduce" if world > 1 else "single GPU",
                        "bvh_build_s": round(bvh_s, 3), "upload_s": round(upload_s, 3)},
             "roofline": roof,

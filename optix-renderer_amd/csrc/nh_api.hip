@@ -10,6 +10,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <deque>
+#include <thread>
 #include <functional>
 #include <cmath>
 #include <cstdio>
@@ -25,6 +27,46 @@
 using nhd::DBsdf;
 using nhd::DEmitter;
 using nhd::DShape;
+
+// ---- wavefront pipeline state (used by nh_render, see the pipeline section below) ----
+constexpr int kRing = 4;   // bounce-count copies in flight per pool
+constexpr int kPools = 2;  // path pools in flight: one drains its last bounces while the next fills the GPU
+
+// one chunk of sample rounds of one nh_render call
+struct WfJob {
+    uint64_t seq;  // submission order = splat order
+    int s0, rounds;
+    uint64_t seed;
+    bool ordered, stats;
+};
+
+// A path pool: the device state one chunk needs (double-buffered path state, shadow queue, sample
+// records, block ImageBlocks, traversal spill area) plus its own stream, events and pinned
+// count ring, and the host-side state machine of the chunk it is running.
+struct WfPool {
+    hipStream_t stream = nullptr;
+    WfState wf{};
+    std::vector<void *> bufs;
+    size_t cap = 0;  // paths
+    float4 *rec = nullptr;
+    float *rec_jy = nullptr;
+    size_t rec_cap = 0;
+    float4 *staging = nullptr;
+    size_t staging_cap = 0;
+    uint32_t *spill = nullptr;
+    int spill_words = 0;
+    unsigned *h_counts = nullptr;  // pinned: kRing bounce-count copies + one initial count slot
+    hipEvent_t copy_ev[kRing] = {};
+    std::vector<hipEvent_t> events;  // 4 per bounce (timing)
+    hipEvent_t ev_begin = nullptr, ev_path = nullptr, ev_splat0 = nullptr, ev_splat = nullptr;
+    enum State { IDLE, ENQUEUE, COUNTS, SPLAT, FINISH } state = IDLE;
+    WfJob job{};
+    WfLaunch L{};
+    bool persistent = false, wide = false, tail = false, draining = false;
+    int64_t tail_at = 0, drain_at = 0;
+    int it = 0;
+    std::vector<uint64_t> in_e, in_s;  // live paths / shadow rays entering each bounce
+};
 
 struct nh_ctx {
     int device = 0;
@@ -60,16 +102,19 @@ struct nh_ctx {
     bool have_list = false;
     unsigned long long *counters = nullptr;  // [0-3] queries, nodes, boxes, prims; [4] invalid; [8-11] wavefront shadow share
     nh_render_stats stats{};
-    // wavefront path state (nh_internal.h WfState), sized for wf_cap paths
-    WfState wf{};
-    uint32_t *trav_spill = nullptr;  // persistent traversal stack spill (kPersistentBlocks * 128 * depth)
-    int trav_spill_depth = 0;
-    std::vector<void *> wf_bufs;
-    size_t wf_cap = 0;
-    unsigned *h_counts = nullptr;  // pinned: kRing bounce-count copies + one initial count slot
-    std::vector<hipEvent_t> wf_events;  // 4 per bounce, reused across chunks
-    hipEvent_t wf_copy_ev[4] = {};
+    // wavefront pipeline (see "Wavefront pipeline" below): path pools, each on its own stream, and
+    // the queue of chunks not yet started
+    WfPool pools[kPools];
+    std::deque<WfJob> jobs;
+    uint64_t job_seq = 0, splat_seq = 0;  // chunks are splatted into fb in submission order
+    hipEvent_t fb_ev = nullptr;           // the last enqueued write of fb (clear or splat)
+    bool fb_ev_set = false;
 };
+
+extern "C" {
+static void pool_free(WfPool &p);
+static int pipeline_drain(nh_ctx *c);
+}
 
 namespace {
 
@@ -151,7 +196,8 @@ int nh_create(int device, nh_ctx **out) {
     auto *c = new nh_ctx();
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->counters, kStatShards * kStatStride * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->counters, kStatShards * kStatStride * sizeof(unsigned long long)) != hipSuccess ||
+        hipEventCreateWithFlags(&c->fb_ev, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return NH_ERR_DEVICE;
     }
@@ -163,6 +209,7 @@ int nh_create(int device, nh_ctx **out) {
 void nh_destroy(nh_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    (void)pipeline_drain(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_all(c->scene_bufs);
     free_all(c->bvh_bufs);
@@ -177,12 +224,8 @@ void nh_destroy(nh_ctx *c) {
     (void)hipFree(c->staging);
     (void)hipFree(c->counters);
     (void)hipFree(c->d_scene);
-    free_all(c->wf_bufs);
-    (void)hipFree(c->trav_spill);
-    if (c->h_counts) (void)hipHostFree(c->h_counts);
-    for (hipEvent_t e : c->wf_events) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->wf_copy_ev)
-        if (e) (void)hipEventDestroy(e);
+    for (WfPool &p : c->pools) pool_free(p);
+    if (c->fb_ev) (void)hipEventDestroy(c->fb_ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -190,6 +233,7 @@ void nh_destroy(nh_ctx *c) {
 int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     if (!c || !d) return NH_ERR_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc_ = pipeline_drain(c)) return rc_;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (d->camera.width <= 0 || d->camera.height <= 0) return fail(c, "invalid camera resolution"), NH_ERR_INVALID;
     if (d->camera.lens_radius > 1e-4f)
@@ -392,6 +436,7 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     if (!c || !b) return NH_ERR_INVALID;
     if (!c->has_scene) return fail(c, "nh_upload_bvh: upload the scene first"), NH_ERR_STATE;
     HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc_ = pipeline_drain(c)) return rc_;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     free_all(c->bvh_bufs);
     c->has_bvh = false;
@@ -517,6 +562,7 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
     if (!c->has_bvh) return fail(c, "nh_trace_rays: no BVH uploaded"), NH_ERR_STATE;
     if (n == 0) return NH_OK;
     HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc_ = pipeline_drain(c)) return rc_;
     std::vector<void *> tmp;
     const float *in[8];
     const float *src[8] = {r->ox, r->oy, r->oz, r->dx, r->dy, r->dz, r->mint, r->maxt};
@@ -567,62 +613,132 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
 }
 
 
-constexpr int kRing = 4;  // bounce-count copies in flight
+// ============================================================================================
+// Wavefront pipeline
+//
+// nh_render splits its sample rounds into chunks (jobs) and runs each chunk on a path pool:
+// camera paths -> {extend, any-hit, shade} per bounce until no path is alive (the tail kernel
+// finishes the last few in place) -> ImageBlock splat of the chunk's sample records into the
+// master framebuffer. Queue lengths stay on the device (nh_internal.h count slots); the host
+// enqueues bounce i+1 before it reads bounce i's counts (2 KB into pinned memory), so the GPU never
+// idles on a host round trip, and exactly one empty bounce is enqueued at the end.
+//
+// The last bounces of a chunk carry few paths whose traversals are long latency chains: a lone
+// pool leaves most of the GPU idle there. kPools pools on their own streams overlap that drain
+// with the next chunk's full bounces (of the same call or of the next nh_render call: a wavefront
+// nh_render returns once every chunk it submitted has started and every running pool is draining;
+// anything that reads results -- nh_synchronize, nh_get_framebuffer, nh_get_stats, ... -- first
+// runs the pipeline to completion). Splats are enqueued in submission order, each waiting for the
+// previous write of the framebuffer, so the master ImageBlock receives chunks in the serial
+// reference's order and the image is bit-identical to a one-pool run.
+// ============================================================================================
+
 constexpr size_t kWfBytesPerPath = 2 * (16 * 7 + 8 + 4 + 4 + 4 + 1) + 36;  // two buffers + shadow queue
 
-static int ensure_wf(nh_ctx *c, size_t n) {
-    if (c->wf_cap >= n) return NH_OK;
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    free_all(c->wf_bufs);
-    c->wf = WfState{};
-    c->wf_cap = 0;
-    auto alloc = [&](auto *&ptr, size_t count) -> bool {
-        void *p = nullptr;
-        if (hipMalloc(&p, count * sizeof(*ptr)) != hipSuccess) return false;
-        c->wf_bufs.push_back(p);
-        ptr = static_cast<std::remove_reference_t<decltype(ptr)>>(p);
-        return true;
-    };
-    WfState &W = c->wf;
-    const size_t nq = n + (size_t)(kQueueShards + 2) * 256;  // shard segments round up to whole shade blocks
-    bool ok = true;
-    for (WfBuf &B : W.buf)
-        ok = ok && alloc(B.ray_o, nq) && alloc(B.ray_d, nq) && alloc(B.hit, nq) && alloc(B.rng, nq) &&
-             alloc(B.li, nq) && alloc(B.thr, nq) && alloc(B.pend_ems, nq) && alloc(B.pend_col, nq) &&
-             alloc(B.pdfmat, nq) && alloc(B.flags, nq) && alloc(B.pid, nq) && alloc(B.occl, nq);
-    ok = ok && alloc(W.sh_o, nq) && alloc(W.sh_d, nq) && alloc(W.sh_slot, nq) &&
-         alloc(W.counts, 2 * kCountSlot);
-    if (!ok) {
-        free_all(c->wf_bufs);
-        c->wf = WfState{};
-        return fail(c, "hipMalloc failed for wavefront path state"), NH_ERR_DEVICE;
-    }
-    if (!c->h_counts) {
-        if (hipHostMalloc(reinterpret_cast<void **>(&c->h_counts),
+static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t staging_f4) {
+    if (!p.stream) {
+        HIP_TRY(c, hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));
+        if (hipHostMalloc(reinterpret_cast<void **>(&p.h_counts),
                           (kRing * 2 * kCountGroup + kCountSlot) * sizeof(unsigned)) != hipSuccess)
             return fail(c, "hipHostMalloc failed"), NH_ERR_DEVICE;
-        for (hipEvent_t &e : c->wf_copy_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (hipEvent_t &e : p.copy_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (hipEvent_t *e : {&p.ev_begin, &p.ev_path, &p.ev_splat0, &p.ev_splat}) HIP_TRY(c, hipEventCreate(e));
     }
-    c->wf_cap = n;
+    if (p.cap < n) {
+        free_all(p.bufs);
+        p.wf = WfState{};
+        p.cap = 0;
+        auto alloc = [&](auto *&ptr, size_t count) -> bool {
+            void *q = nullptr;
+            if (hipMalloc(&q, count * sizeof(*ptr)) != hipSuccess) return false;
+            p.bufs.push_back(q);
+            ptr = static_cast<std::remove_reference_t<decltype(ptr)>>(q);
+            return true;
+        };
+        WfState &W = p.wf;
+        const size_t nq = n + (size_t)(kQueueShards + 2) * 256;  // shard segments round up to whole shade blocks
+        bool ok = true;
+        for (WfBuf &B : W.buf)
+            ok = ok && alloc(B.ray_o, nq) && alloc(B.ray_d, nq) && alloc(B.hit, nq) && alloc(B.rng, nq) &&
+                 alloc(B.li, nq) && alloc(B.thr, nq) && alloc(B.pend_ems, nq) && alloc(B.pend_col, nq) &&
+                 alloc(B.pdfmat, nq) && alloc(B.flags, nq) && alloc(B.pid, nq) && alloc(B.occl, nq);
+        ok = ok && alloc(W.sh_o, nq) && alloc(W.sh_d, nq) && alloc(W.sh_slot, nq) && alloc(W.counts, 2 * kCountSlot) &&
+             alloc(p.rec, n) && alloc(p.rec_jy, n);
+        if (!ok) {
+            free_all(p.bufs);
+            p.wf = WfState{};
+            p.rec = nullptr;
+            p.rec_jy = nullptr;
+            return fail(c, "hipMalloc failed for wavefront path state"), NH_ERR_DEVICE;
+        }
+        p.cap = n;
+    }
+    if (p.staging_cap < staging_f4) {
+        (void)hipFree(p.staging);
+        p.staging = nullptr;
+        p.staging_cap = staging_f4;
+        HIP_TRY(c, hipMalloc(&p.staging, staging_f4 * sizeof(float4)));
+    }
     return NH_OK;
 }
 
-// One chunk of rounds through generate -> {extend, any-hit, shade} per bounce until no path is
-// alive. Queue lengths stay on the device (nh_internal.h count slots); the host enqueues bounce
-// i+1 before it waits for bounce i's counts (2 KB into pinned memory), so the GPU never idles
-// on a host round trip and exactly one empty bounce is enqueued at the end. Kernel times come
-// from per-launch events read once the chunk has finished.
-static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch &P) {
-    WfLaunch L{};
-    L.st = c->wf;
-    L.n_paths = P.n_paths;
-    L.n_list = P.n_list;
-    L.s0 = P.s0;
-    L.seed = P.seed;
-    L.pixel_list = P.pixel_list;
-    L.rec_rgbx = P.rec_rgbx;
-    L.rec_jy = P.rec_jy;
-    L.counters = P.counters;
+static void pool_free(WfPool &p) {
+    free_all(p.bufs);
+    (void)hipFree(p.staging);
+    (void)hipFree(p.spill);
+    if (p.h_counts) (void)hipHostFree(p.h_counts);
+    for (hipEvent_t e : p.events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : p.copy_ev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {p.ev_begin, p.ev_path, p.ev_splat0, p.ev_splat})
+        if (e) (void)hipEventDestroy(e);
+    if (p.stream) (void)hipStreamDestroy(p.stream);
+    p = WfPool{};
+}
+
+static SplatLaunch make_splat(const nh_ctx *c, const float4 *rec, const float *rec_jy, float4 *staging, int rounds) {
+    SplatLaunch P{};
+    P.fb = c->fb;
+    P.width = c->width;
+    P.height = c->height;
+    P.border = c->border;
+    P.reach = (int)std::floor(c->filter.radius + 0.5f);
+    P.nbx = c->nbx;
+    P.n_rounds = rounds;
+    P.n_list = c->n_list;
+    P.pixel_map = c->pixel_map;
+    P.block_rank = c->block_rank;
+    P.rec_rgbx = rec;
+    P.rec_jy = rec_jy;
+    P.radius = c->filter.radius;
+    P.lookup = c->filter.lookup_factor;
+    std::memcpy(P.table, c->filter.table, sizeof(P.table));
+    P.blocks = c->block_ids;
+    P.block_slot = c->block_slot;
+    P.n_blocks = c->n_blocks;
+    P.staging = staging;
+    return P;
+}
+
+static size_t block_px(const nh_ctx *c) { return (size_t)(32 + 2 * c->border) * (32 + 2 * c->border); }
+
+// start job j on idle pool p: buffers, traversal choice, initial queue (all n_paths camera paths)
+static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
+    const int n_paths = j.rounds * c->n_list;
+    int rc = pool_alloc(c, p, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c));
+    if (rc) return rc;
+    p.job = j;
+    WfLaunch &L = p.L;
+    L = WfLaunch{};
+    L.st = p.wf;
+    L.n_paths = n_paths;
+    L.n_list = c->n_list;
+    L.s0 = j.s0;
+    L.seed = j.seed;
+    L.pixel_list = c->pixel_list;
+    L.rec_rgbx = p.rec;
+    L.rec_jy = p.rec_jy;
+    L.counters = c->counters;
     // scenes whose BVH fits in a few KB (the Cornell box: < 1 KB) are traversed from an LDS copy
     const size_t scene_bytes = 16 * (size_t)(c->n_node_f4 + c->n_prim_f4) + 8 * (size_t)c->n_leaves;
     bool small = scene_bytes <= kSmallSceneBytes;
@@ -632,112 +748,158 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         L.small_leaves = c->n_leaves;
         L.small_prims = c->n_prim_f4;
     }
-    const bool ordered = q->traversal != NH_TRAVERSAL_REFERENCE, stats = q->collect_stats != 0;
     const int per_chunk = 256;  // wf_shade's chunk
-    const int max_chunks = (P.n_paths + per_chunk - 1) / per_chunk;
+    const int max_chunks = (n_paths + per_chunk - 1) / per_chunk;
     L.seg_cap = (max_chunks + kQueueShards - 1) / kQueueShards * per_chunk;
     // persistent traversal pays off on deep BVHs (long, divergent traversals); cbox-like scenes
     // traverse faster with one ray per lane
-    bool persistent = c->depth > 20;
-    if (const char *e = std::getenv("NH_PERSISTENT")) persistent = e[0] == '1';
+    p.persistent = c->depth > 20;
+    if (const char *e = std::getenv("NH_PERSISTENT")) p.persistent = e[0] == '1';
     // the persistent kernels walk the 4-wide collapse of the tree (half the dependent node fetches)
     // unless the reference's own visit order was asked for
-    bool wide = persistent && ordered && c->tv.wnodes != nullptr;
-    if (const char *e = std::getenv("NH_WIDE")) wide = wide && e[0] != '0';
+    p.wide = p.persistent && j.ordered && c->tv.wnodes != nullptr;
+    if (const char *e = std::getenv("NH_WIDE")) p.wide = p.wide && e[0] != '0';
     // spill words per lane: binary entries are one word, wide entries two (8-B aligned)
-    const int spill_words = wide ? 2 * c->depth_wide : (c->depth + 1) / 2 * 2;
-    if (persistent && c->trav_spill_depth < spill_words) {
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        (void)hipFree(c->trav_spill);
-        c->trav_spill = nullptr;
-        c->trav_spill_depth = spill_words;
-        HIP_TRY(c, hipMalloc(&c->trav_spill, (size_t)kPersistentBlocks * 128 * spill_words * sizeof(uint32_t)));
+    const int spill_words = p.wide ? 2 * c->depth_wide : (c->depth + 1) / 2 * 2;
+    if (p.persistent && p.spill_words < spill_words) {
+        HIP_TRY(c, hipStreamSynchronize(p.stream));
+        (void)hipFree(p.spill);
+        p.spill = nullptr;
+        p.spill_words = spill_words;
+        HIP_TRY(c, hipMalloc(&p.spill, (size_t)kPersistentBlocks * 128 * spill_words * sizeof(uint32_t)));
     }
-    c->stats.node_bytes = wide ? 16 * nhd::kWideF4 : 64;
-    L.trav_spill = c->trav_spill;
-    L.spill_depth = c->trav_spill_depth;
-    unsigned *slot[2] = {c->wf.counts, c->wf.counts + kCountSlot};
-    // bounce 0 reads the dense queue written by generate: shard 0 holds all n_paths
-    unsigned *h_init = c->h_counts + kRing * 2 * kCountGroup;
-    std::memset(h_init, 0, kCountSlot * sizeof(unsigned));
-    h_init[0] = (unsigned)P.n_paths;
-    HIP_TRY(c, hipMemcpyAsync(slot[0], h_init, kCountSlot * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
-    const size_t append_bytes = 2 * kCountGroup * sizeof(unsigned);
-    // per-bounce totals: in_e / in_s = live paths / shadow rays entering the bounce
-    std::vector<uint64_t> in_e{(uint64_t)P.n_paths}, in_s{0};
-    // below this many live paths the rest of the chunk runs in one wf_tail launch
+    c->stats.node_bytes = p.wide ? 16 * nhd::kWideF4 : 64;
+    L.trav_spill = p.spill;
+    L.spill_depth = p.spill_words;
     // measured on 16.7M-path chunks: C2 3025 / 3030 / 2692 Msamples/s at 64k / 262k / 1M,
     // bumpy-1M 708 / 744 / 739 / 603 at 64k / 262k / 1M / 3M
-    int64_t tail_at = std::max<int64_t>(P.n_paths / 64, 8192);
-    if (const char *e = std::getenv("NH_TAIL")) tail_at = std::atoll(e);
-    bool tail = false;
-    int it = 0;
-    for (;; ++it) {
-        const int in = it & 1;
-        L.in_q = in;
-        L.first = it == 0;
-        L.cnt_in = slot[in];
-        L.cnt_out = slot[in ^ 1];
-        if ((size_t)(it + 1) * 4 > c->wf_events.size()) {
-            for (int k = 0; k < 64; ++k) {
-                hipEvent_t e;
-                HIP_TRY(c, hipEventCreate(&e));
-                c->wf_events.push_back(e);
-            }
-        }
-        hipEvent_t *ev = &c->wf_events[(size_t)it * 4];
-        // upper bound of this bounce's live paths: the input of the previous bounce (known: the
-        // host has read the counts up to bounce it-2)
-        const int bound = (int)in_e[it == 0 ? 0 : it - 1];
-        HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), c->stream));
-        HIP_TRY(c, hipEventRecord(ev[0], c->stream));
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, persistent, wide, bound, c->depth, c->stream);
-        HIP_TRY(c, hipEventRecord(ev[1], c->stream));
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, persistent, wide, bound, c->depth, c->stream);
-        HIP_TRY(c, hipEventRecord(ev[2], c->stream));
-        tail = it > 0 && (int64_t)bound <= tail_at;
-        if (tail) {
-            nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, wide, bound, c->depth, c->stream);
-            HIP_TRY(c, hipGetLastError());
-            HIP_TRY(c, hipEventRecord(ev[3], c->stream));
-            // the last regular bounce's output counts, for the byte accounting below
-            HIP_TRY(c, hipEventSynchronize(c->wf_copy_ev[(it - 1) % kRing]));
-            const unsigned *hp = c->h_counts + (size_t)((it - 1) % kRing) * 2 * kCountGroup;
-            uint64_t ne = 0, ns = 0;
-            for (int s = 0; s < kQueueShards; ++s) {
-                ne += hp[s * kCountStride];
-                ns += hp[kCountGroup + s * kCountStride];
-            }
-            in_e.push_back(ne);
-            in_s.push_back(ns);
-            break;
-        }
-        nh::launch_wf_shade(c->d_scene, c->tv, L, bound, c->stream);
-        HIP_TRY(c, hipGetLastError());
-        HIP_TRY(c, hipEventRecord(ev[3], c->stream));
-        unsigned *h = c->h_counts + (size_t)(it % kRing) * 2 * kCountGroup;
-        HIP_TRY(c, hipMemcpyAsync(h, slot[in ^ 1], append_bytes, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipEventRecord(c->wf_copy_ev[it % kRing], c->stream));
-        if (it == 0) continue;
-        // counts of bounce it-1 (its copy was enqueued before bounce it, which keeps the GPU busy)
-        HIP_TRY(c, hipEventSynchronize(c->wf_copy_ev[(it - 1) % kRing]));
-        const unsigned *hp = c->h_counts + (size_t)((it - 1) % kRing) * 2 * kCountGroup;
-        uint64_t ne = 0, ns = 0;
-        for (int s = 0; s < kQueueShards; ++s) {
-            const unsigned ce = hp[s * kCountStride], cs = hp[kCountGroup + s * kCountStride];
-            if (ce > (unsigned)L.seg_cap || cs > ce) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
-            ne += ce;
-            ns += cs;
-        }
-        if (ne > (uint64_t)P.n_paths) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
-        in_e.push_back(ne);
-        in_s.push_back(ns);
-        if (ne == 0) break;  // bounce `it` was enqueued empty: the chunk is done
-        if (it > 100000) return fail(c, "wavefront did not terminate"), NH_ERR_DEVICE;
+    p.tail_at = std::max<int64_t>(n_paths / 64, 8192);
+    if (const char *e = std::getenv("NH_TAIL")) p.tail_at = std::atoll(e);
+    // below this many live paths the pool counts as draining: the next chunk may start beside it
+    p.drain_at = std::max<int64_t>(n_paths / 8, p.tail_at);
+    HIP_TRY(c, hipEventRecord(p.ev_begin, p.stream));
+    // bounce 0 reads the dense camera queue: shard 0 holds all n_paths
+    unsigned *h_init = p.h_counts + kRing * 2 * kCountGroup;
+    std::memset(h_init, 0, kCountSlot * sizeof(unsigned));
+    h_init[0] = (unsigned)n_paths;
+    HIP_TRY(c, hipMemcpyAsync(p.wf.counts, h_init, kCountSlot * sizeof(unsigned), hipMemcpyHostToDevice, p.stream));
+    p.in_e.assign(1, (uint64_t)n_paths);
+    p.in_s.assign(1, 0);
+    p.it = 0;
+    p.tail = false;
+    p.draining = false;
+    p.state = WfPool::ENQUEUE;
+    return NH_OK;
+}
+
+// enqueue bounce p.it (extend, any-hit, then shade or, once few paths are left, the tail kernel)
+static int pool_enqueue(nh_ctx *c, WfPool &p) {
+    WfLaunch &L = p.L;
+    const int it = p.it, in = it & 1;
+    unsigned *slot[2] = {p.wf.counts, p.wf.counts + kCountSlot};
+    L.in_q = in;
+    L.first = it == 0;
+    L.cnt_in = slot[in];
+    L.cnt_out = slot[in ^ 1];
+    while ((size_t)(it + 1) * 4 > p.events.size()) {
+        hipEvent_t e;
+        HIP_TRY(c, hipEventCreate(&e));
+        p.events.push_back(e);
     }
-    HIP_TRY(c, hipEventSynchronize(c->wf_events[(size_t)it * 4 + 3]));
-    for (int b = 0; b <= it; ++b) {
-        hipEvent_t *ev = &c->wf_events[(size_t)b * 4];
+    hipEvent_t *ev = &p.events[(size_t)it * 4];
+    // upper bound of this bounce's live paths: the input of the previous bounce (known: the host
+    // has read the counts up to bounce it-2)
+    const int bound = (int)p.in_e[it == 0 ? 0 : it - 1];
+    const bool ordered = p.job.ordered, stats = p.job.stats;
+    HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), p.stream));
+    HIP_TRY(c, hipEventRecord(ev[0], p.stream));
+    nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, p.persistent, p.wide, bound, c->depth, p.stream);
+    HIP_TRY(c, hipEventRecord(ev[1], p.stream));
+    nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, p.persistent, p.wide, bound, c->depth, p.stream);
+    HIP_TRY(c, hipEventRecord(ev[2], p.stream));
+    if (it > 0 && (int64_t)bound <= p.tail_at) {
+        nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, p.wide, bound, c->depth, p.stream);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipEventRecord(ev[3], p.stream));
+        p.tail = true;
+        p.draining = true;
+        p.state = WfPool::SPLAT;
+        return NH_OK;
+    }
+    nh::launch_wf_shade(c->d_scene, c->tv, L, bound, p.stream);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(ev[3], p.stream));
+    unsigned *h = p.h_counts + (size_t)(it % kRing) * 2 * kCountGroup;
+    HIP_TRY(c, hipMemcpyAsync(h, slot[in ^ 1], 2 * kCountGroup * sizeof(unsigned), hipMemcpyDeviceToHost, p.stream));
+    HIP_TRY(c, hipEventRecord(p.copy_ev[it % kRing], p.stream));
+    if (it == 0) {
+        p.it = 1;  // bounce 1 is sized by bounce 0's input: enqueue it before reading any count
+    } else {
+        p.state = WfPool::COUNTS;
+    }
+    return NH_OK;
+}
+
+// counts appended by bounce b (live paths, shadow rays entering bounce b+1)
+static int pool_counts(nh_ctx *c, WfPool &p, int b, uint64_t &ne, uint64_t &ns) {
+    const unsigned *hp = p.h_counts + (size_t)(b % kRing) * 2 * kCountGroup;
+    ne = ns = 0;
+    for (int s = 0; s < kQueueShards; ++s) {
+        const unsigned ce = hp[s * kCountStride], cs = hp[kCountGroup + s * kCountStride];
+        if (ce > (unsigned)p.L.seg_cap || cs > ce) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
+        ne += ce;
+        ns += cs;
+    }
+    if (ne > (uint64_t)p.L.n_paths) return fail(c, "wavefront queue counts out of range"), NH_ERR_DEVICE;
+    return NH_OK;
+}
+
+// bounce it-1's counts have arrived: bounce it was enqueued empty (done) or enqueue bounce it+1
+static int pool_read(nh_ctx *c, WfPool &p) {
+    uint64_t ne, ns;
+    int rc = pool_counts(c, p, p.it - 1, ne, ns);
+    if (rc) return rc;
+    p.in_e.push_back(ne);
+    p.in_s.push_back(ns);
+    if ((int64_t)ne < p.drain_at) p.draining = true;
+    if (ne == 0) {
+        p.state = WfPool::SPLAT;
+        return NH_OK;
+    }
+    if (++p.it > 100000) return fail(c, "wavefront did not terminate"), NH_ERR_DEVICE;
+    p.state = WfPool::ENQUEUE;
+    return NH_OK;
+}
+
+// the chunk's paths are enqueued to completion: splat its records into the master ImageBlock
+// after the previous write of the framebuffer (called in submission order)
+static int pool_splat(nh_ctx *c, WfPool &p) {
+    HIP_TRY(c, hipEventRecord(p.ev_path, p.stream));
+    if (p.job.stats) nh::launch_count_invalid(p.rec, (size_t)p.L.n_paths, c->counters, p.stream);
+    if (c->fb_ev_set) HIP_TRY(c, hipStreamWaitEvent(p.stream, c->fb_ev, 0));
+    HIP_TRY(c, hipEventRecord(p.ev_splat0, p.stream));
+    nh::launch_splat(make_splat(c, p.rec, p.rec_jy, p.staging, p.job.rounds), p.stream);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(p.ev_splat, p.stream));
+    HIP_TRY(c, hipEventRecord(c->fb_ev, p.stream));
+    c->fb_ev_set = true;
+    c->splat_seq++;
+    p.draining = true;
+    p.state = WfPool::FINISH;
+    return NH_OK;
+}
+
+// the chunk has finished on the device: kernel times and byte accounting into the stats
+static int pool_finish(nh_ctx *c, WfPool &p) {
+    if (p.tail) {  // the last regular bounce's output counts, for the byte accounting below
+        uint64_t ne, ns;
+        int rc = pool_counts(c, p, p.it - 1, ne, ns);
+        if (rc) return rc;
+        p.in_e.push_back(ne);
+        p.in_s.push_back(ns);
+    }
+    for (int b = 0; b <= p.it; ++b) {
+        hipEvent_t *ev = &p.events[(size_t)b * 4];
         float a = 0.f, sh = 0.f, d = 0.f;
         (void)hipEventElapsedTime(&a, ev[0], ev[1]);
         (void)hipEventElapsedTime(&sh, ev[1], ev[2]);
@@ -746,7 +908,7 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
         c->stats.kernel_ms_shadow += sh;
         c->stats.launches_extend++;
         c->stats.launches_shadow++;
-        if (tail && b == it) {
+        if (p.tail && b == p.it) {
             c->stats.kernel_ms_tail += d;
             c->stats.launches_tail++;
         } else {
@@ -754,20 +916,96 @@ static int render_wavefront(nh_ctx *c, const nh_render_req *q, const PathLaunch 
             c->stats.launches_shade++;
         }
     }
+    float tp = 0.f, ts = 0.f;
+    (void)hipEventElapsedTime(&tp, p.ev_begin, p.ev_path);
+    (void)hipEventElapsedTime(&ts, p.ev_splat0, p.ev_splat);
+    c->stats.kernel_ms_path += tp;
+    c->stats.kernel_ms_splat += ts;
+    c->stats.launches_splat++;
+    c->stats.samples += (uint64_t)p.L.n_paths;
     // bytes by construction (nh_wavefront.hip). Bounce 0 evaluates the camera sample in place: shade
     // loads the hit (16 B) and writes the sample record (20 B) per path. Later bounces load 96 B per
     // path (ray, hit, Li, throughput, rng, flags, pid) + 16 (pending BSDF sample) + 17 per queued
     // shadow ray (pending NEE + occlusion). Every bounce stores 116 B per survivor, 36 per new
     // shadow ray and 12 per finished path; extend moves 48 B per ray (16 at bounce 0: no ray load).
     // (Bounces shaded by wf_shade only; the tail kernel's work is not part of this account.)
-    for (size_t b = 0; b + 1 < in_e.size(); ++b) {
-        const uint64_t shaded = in_e[b], nsh = in_s[b], ne = in_e[b + 1], ns = in_s[b + 1];
+    for (size_t b = 0; b + 1 < p.in_e.size(); ++b) {
+        const uint64_t shaded = p.in_e[b], nsh = p.in_s[b], ne = p.in_e[b + 1], ns = p.in_s[b + 1];
         const uint64_t loads = b == 0 ? shaded * (16 + 20) : shaded * (96 + 16) + nsh * 17;
         c->stats.paths_shaded += shaded;
         c->stats.shade_state_bytes += loads + ne * 116 + ns * 36 + (shaded - ne) * 12;
         c->stats.extend_queue_bytes += shaded * (b == 0 ? 16 : 48);
         c->stats.shadow_queue_bytes += nsh * 37;  // ray in, path slot, occlusion byte out
     }
+    p.state = WfPool::IDLE;
+    return NH_OK;
+}
+
+static bool event_done(hipEvent_t e) { return hipEventQuery(e) == hipSuccess; }
+
+static void pipeline_reset(nh_ctx *c) {
+    for (WfPool &p : c->pools)
+        if (p.stream) (void)hipStreamSynchronize(p.stream);
+    for (WfPool &p : c->pools) p.state = WfPool::IDLE;
+    c->jobs.clear();
+    c->splat_seq = c->job_seq;
+}
+
+// Drive the pools. all = run until every chunk has finished; otherwise return once every
+// submitted chunk has started and every busy pool is draining.
+static int pipeline_run(nh_ctx *c, bool all) {
+    const char *np = std::getenv("NH_POOLS");  // 1 = no overlap (A/B and tests)
+    const int n_pools = np ? std::max(1, std::min(kPools, std::atoi(np))) : kPools;
+    for (;;) {
+        bool progress = false;
+        for (WfPool &p : c->pools) {
+            int rc = NH_OK;
+            // a chunk starts on an idle pool once every running chunk is draining (staggered pools)
+            bool others_draining = true;
+            for (const WfPool &o : c->pools) others_draining = others_draining && (o.state == WfPool::IDLE || o.draining);
+            if (p.state == WfPool::IDLE && !c->jobs.empty() && &p - c->pools < n_pools && others_draining) {
+                rc = pool_start(c, p, c->jobs.front());
+                c->jobs.pop_front();
+                progress = true;
+            }
+            if (!rc && p.state == WfPool::ENQUEUE) {
+                rc = pool_enqueue(c, p);
+                progress = true;
+            }
+            if (!rc && p.state == WfPool::COUNTS && event_done(p.copy_ev[(p.it - 1) % kRing])) {
+                rc = pool_read(c, p);
+                progress = true;
+            }
+            if (!rc && p.state == WfPool::SPLAT && p.job.seq == c->splat_seq) {
+                rc = pool_splat(c, p);
+                progress = true;
+            }
+            if (!rc && p.state == WfPool::FINISH && event_done(p.ev_splat)) {
+                rc = pool_finish(c, p);
+                progress = true;
+            }
+            if (rc) {
+                pipeline_reset(c);
+                return rc;
+            }
+        }
+        if (c->jobs.empty()) {
+            bool idle = true, draining = true;
+            for (const WfPool &p : c->pools) {
+                idle = idle && p.state == WfPool::IDLE;
+                draining = draining && (p.state == WfPool::IDLE || p.draining);
+            }
+            if (idle || (!all && draining)) return NH_OK;
+        }
+        if (!progress) std::this_thread::yield();  // waiting on the device
+    }
+}
+
+static int pipeline_drain(nh_ctx *c) {
+    int rc = pipeline_run(c, true);
+    if (rc) return rc;
+    for (WfPool &p : c->pools)
+        if (p.stream) HIP_TRY(c, hipStreamSynchronize(p.stream));
     return NH_OK;
 }
 
@@ -775,6 +1013,7 @@ static int ensure_pixel_list(nh_ctx *c, const nh_render_req *q) {
     std::vector<int32_t> key;
     if (q->n_blocks > 0 && q->blocks) key.assign(q->blocks, q->blocks + q->n_blocks);
     if (c->have_list && key == c->list_key) return NH_OK;
+    if (int rc = pipeline_drain(c)) return rc;  // chunks in flight read the current list
     std::vector<int32_t> blocks = key;
     if (blocks.empty())
         for (int i = 0; i < c->nbx * c->nby; ++i) blocks.push_back(i);
@@ -824,117 +1063,102 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     const bool wavefront = q->mode == NH_MODE_WAVEFRONT;
     if (q->traversal < NH_TRAVERSAL_REFERENCE || q->traversal > NH_TRAVERSAL_WIDE)
         return fail(c, "unknown traversal"), NH_ERR_INVALID;
-    c->stats.node_bytes = 64;  // binary tree unless the wavefront picks the 4-wide one
+    if (c->border > 4) return fail(c, "reconstruction filters wider than border 4 are not supported"), NH_ERR_UNSUPPORTED;
     HIP_TRY(c, hipSetDevice(c->device));
-    int rc = ensure_pixel_list(c, q);
+    // only asynchronous wavefront renders overlap earlier chunks still in flight
+    int rc = NH_OK;
+    if (!wavefront || q->collect_stats || q->clear) rc = pipeline_drain(c);
     if (rc) return rc;
-    if (q->clear) HIP_TRY(c, hipMemsetAsync(c->fb, 0, c->fb_floats * sizeof(float), c->stream));
+    rc = ensure_pixel_list(c, q);
+    if (rc) return rc;
+    c->stats.node_bytes = 64;  // binary tree unless a wavefront pool picks the 4-wide one
+    if (q->clear) {
+        HIP_TRY(c, hipMemsetAsync(c->fb, 0, c->fb_floats * sizeof(float), c->stream));
+        HIP_TRY(c, hipEventRecord(c->fb_ev, c->stream));  // pools' splats wait for it
+        c->fb_ev_set = true;
+    }
     const int rounds = q->sample_end - q->sample_begin;
     if (rounds == 0 || c->n_list == 0) return NH_OK;
-    // sample records per chunk of rounds (20 B per sample)
-    size_t budget = (size_t)1 << 30;
-    if (const char *e = std::getenv("NH_RECORD_BUDGET_MB")) budget = (size_t)std::max(1L, std::atol(e)) << 20;
-    size_t per_round = (size_t)c->n_list;
-    if (c->border > 4) return fail(c, "reconstruction filters wider than border 4 are not supported"), NH_ERR_UNSUPPORTED;
-    const size_t block_px = (size_t)(32 + 2 * c->border) * (32 + 2 * c->border);
-    size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px * 16;
-    if (wavefront) {  // path state: ~200 B per path in flight
-        per_round_bytes += per_round * kWfBytesPerPath;
-        budget = (size_t)8 << 30;
-        if (const char *e = std::getenv("NH_WF_BUDGET_MB")) budget = (size_t)std::max(1L, std::atol(e)) << 20;
-    }
-    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / per_round_bytes));
-    while ((size_t)chunk * per_round > (size_t)0x7fffffff) chunk = std::max(1, chunk / 2);
-    if (c->rec_cap < (size_t)chunk * per_round) {
-        (void)hipFree(c->rec);
-        (void)hipFree(c->rec_jy);
-        c->rec = nullptr;
-        c->rec_jy = nullptr;
-        c->rec_cap = (size_t)chunk * per_round;
-        HIP_TRY(c, hipMalloc(&c->rec, c->rec_cap * sizeof(float4)));
-        HIP_TRY(c, hipMalloc(&c->rec_jy, c->rec_cap * sizeof(float)));
-    }
-    if (c->staging_cap < (size_t)chunk * c->n_blocks * block_px) {
-        (void)hipFree(c->staging);
-        c->staging = nullptr;
-        c->staging_cap = (size_t)chunk * c->n_blocks * block_px;
-        HIP_TRY(c, hipMalloc(&c->staging, c->staging_cap * sizeof(float4)));
-    }
-    if (wavefront) {
-        rc = ensure_wf(c, (size_t)chunk * per_round);
-        if (rc) return rc;
-    }
     if (q->collect_stats)
         HIP_TRY(c, hipMemsetAsync(c->counters, 0, kStatShards * kStatStride * sizeof(unsigned long long), c->stream));
-    struct Ev {
-        hipEvent_t a, b, d;
-    };
-    std::vector<Ev> evs;
-    for (int s = q->sample_begin; s < q->sample_end; s += chunk) {
-        const int k = std::min(chunk, q->sample_end - s);
-        PathLaunch L{};
-        L.n_paths = k * c->n_list;
-        L.n_list = c->n_list;
-        L.s0 = s;
-        L.seed = q->seed;
-        L.pixel_list = c->pixel_list;
-        L.rec_rgbx = c->rec;
-        L.rec_jy = c->rec_jy;
-        L.counters = c->counters;
-        SplatLaunch P{};
-        P.fb = c->fb;
-        P.width = c->width;
-        P.height = c->height;
-        P.border = c->border;
-        P.reach = (int)std::floor(c->filter.radius + 0.5f);
-        P.nbx = c->nbx;
-        P.n_rounds = k;
-        P.n_list = c->n_list;
-        P.pixel_map = c->pixel_map;
-        P.block_rank = c->block_rank;
-        P.rec_rgbx = c->rec;
-        P.rec_jy = c->rec_jy;
-        P.radius = c->filter.radius;
-        P.lookup = c->filter.lookup_factor;
-        std::memcpy(P.table, c->filter.table, sizeof(P.table));
-        P.blocks = c->block_ids;
-        P.block_slot = c->block_slot;
-        P.n_blocks = c->n_blocks;
-        P.staging = c->staging;
-        Ev ev;
-        HIP_TRY(c, hipEventCreate(&ev.a));
-        HIP_TRY(c, hipEventCreate(&ev.b));
-        HIP_TRY(c, hipEventCreate(&ev.d));
-        HIP_TRY(c, hipEventRecord(ev.a, c->stream));
-        if (wavefront) {
-            rc = render_wavefront(c, q, L);
-            if (rc) return rc;
-        } else {
-            nh::launch_path(c->d_scene, c->tv, L, q->traversal != NH_TRAVERSAL_REFERENCE, q->collect_stats != 0, c->depth,
-                            c->stream);
+    const size_t per_round = (size_t)c->n_list;
+    const size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px(c) * 16 +
+                                   (wavefront ? per_round * kWfBytesPerPath : 0);
+    // device memory per chunk: sample records + block ImageBlocks (+ path state, per pool)
+    size_t budget = wavefront ? (size_t)8 << 30 : (size_t)1 << 30;
+    if (const char *e = std::getenv(wavefront ? "NH_WF_BUDGET_MB" : "NH_RECORD_BUDGET_MB"))
+        budget = (size_t)std::max(1L, std::atol(e)) << 20;
+    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / per_round_bytes));
+    while ((size_t)chunk * per_round > (size_t)0x7fffffff) chunk = std::max(1, chunk / 2);
+
+    if (wavefront) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // pixel list / clear / counters are in place
+        for (int s = q->sample_begin; s < q->sample_end; s += chunk)
+            c->jobs.push_back(WfJob{c->job_seq++, s, std::min(chunk, q->sample_end - s), q->seed,
+                                    q->traversal != NH_TRAVERSAL_REFERENCE, q->collect_stats != 0});
+        rc = q->collect_stats ? pipeline_drain(c) : pipeline_run(c, false);
+        if (rc) return rc;
+    } else {
+        if (c->rec_cap < (size_t)chunk * per_round) {
+            (void)hipFree(c->rec);
+            (void)hipFree(c->rec_jy);
+            c->rec = nullptr;
+            c->rec_jy = nullptr;
+            c->rec_cap = (size_t)chunk * per_round;
+            HIP_TRY(c, hipMalloc(&c->rec, c->rec_cap * sizeof(float4)));
+            HIP_TRY(c, hipMalloc(&c->rec_jy, c->rec_cap * sizeof(float)));
         }
-        HIP_TRY(c, hipGetLastError());
-        HIP_TRY(c, hipEventRecord(ev.b, c->stream));
-        if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters, c->stream);
-        nh::launch_splat(P, c->stream);
-        HIP_TRY(c, hipGetLastError());
-        HIP_TRY(c, hipEventRecord(ev.d, c->stream));
-        evs.push_back(ev);
+        if (c->staging_cap < (size_t)chunk * c->n_blocks * block_px(c)) {
+            (void)hipFree(c->staging);
+            c->staging = nullptr;
+            c->staging_cap = (size_t)chunk * c->n_blocks * block_px(c);
+            HIP_TRY(c, hipMalloc(&c->staging, c->staging_cap * sizeof(float4)));
+        }
+        struct Ev {
+            hipEvent_t a, b, d;
+        };
+        std::vector<Ev> evs;
+        for (int s = q->sample_begin; s < q->sample_end; s += chunk) {
+            const int k = std::min(chunk, q->sample_end - s);
+            PathLaunch L{};
+            L.n_paths = k * c->n_list;
+            L.n_list = c->n_list;
+            L.s0 = s;
+            L.seed = q->seed;
+            L.pixel_list = c->pixel_list;
+            L.rec_rgbx = c->rec;
+            L.rec_jy = c->rec_jy;
+            L.counters = c->counters;
+            Ev ev;
+            HIP_TRY(c, hipEventCreate(&ev.a));
+            HIP_TRY(c, hipEventCreate(&ev.b));
+            HIP_TRY(c, hipEventCreate(&ev.d));
+            HIP_TRY(c, hipEventRecord(ev.a, c->stream));
+            nh::launch_path(c->d_scene, c->tv, L, q->traversal != NH_TRAVERSAL_REFERENCE, q->collect_stats != 0,
+                            c->depth, c->stream);
+            HIP_TRY(c, hipGetLastError());
+            HIP_TRY(c, hipEventRecord(ev.b, c->stream));
+            if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters, c->stream);
+            nh::launch_splat(make_splat(c, c->rec, c->rec_jy, c->staging, k), c->stream);
+            HIP_TRY(c, hipGetLastError());
+            HIP_TRY(c, hipEventRecord(ev.d, c->stream));
+            evs.push_back(ev);
+        }
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (auto &ev : evs) {
+            float a = 0, b = 0;
+            (void)hipEventElapsedTime(&a, ev.a, ev.b);
+            (void)hipEventElapsedTime(&b, ev.b, ev.d);
+            c->stats.kernel_ms_path += a;
+            c->stats.kernel_ms_splat += b;
+            c->stats.launches_path++;
+            c->stats.launches_splat++;
+            (void)hipEventDestroy(ev.a);
+            (void)hipEventDestroy(ev.b);
+            (void)hipEventDestroy(ev.d);
+        }
+        c->stats.samples += (uint64_t)rounds * (uint64_t)c->n_list;
     }
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (auto &ev : evs) {
-        float a = 0, b = 0;
-        (void)hipEventElapsedTime(&a, ev.a, ev.b);
-        (void)hipEventElapsedTime(&b, ev.b, ev.d);
-        c->stats.kernel_ms_path += a;
-        c->stats.kernel_ms_splat += b;
-        c->stats.launches_path += wavefront ? 0 : 1;
-        c->stats.launches_splat++;
-        (void)hipEventDestroy(ev.a);
-        (void)hipEventDestroy(ev.b);
-        (void)hipEventDestroy(ev.d);
-    }
-    c->stats.samples += (uint64_t)rounds * (uint64_t)c->n_list;
     if (q->collect_stats) {
         unsigned long long hs[kStatShards * kStatStride], h[16] = {};
         HIP_TRY(c, hipMemcpy(hs, c->counters, sizeof(hs), hipMemcpyDeviceToHost));
@@ -956,6 +1180,8 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
 int nh_synchronize(nh_ctx *c) {
     if (!c) return NH_ERR_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
+    int rc = pipeline_drain(c);
+    if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return NH_OK;
 }
@@ -965,6 +1191,8 @@ int nh_get_framebuffer(nh_ctx *c, float *rgbw, size_t n) {
     if (!c->has_scene) return fail(c, "no scene"), NH_ERR_STATE;
     if (n < c->fb_floats) return fail(c, "framebuffer destination too small"), NH_ERR_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
+    int rc = pipeline_drain(c);
+    if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemcpy(rgbw, c->fb, c->fb_floats * sizeof(float), hipMemcpyDeviceToHost));
     return NH_OK;
@@ -980,12 +1208,18 @@ int nh_framebuffer_device_ptr(nh_ctx *c, void **dptr, size_t *n) {
 
 int nh_get_stats(nh_ctx *c, nh_render_stats *out) {
     if (!c || !out) return NH_ERR_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    int rc = pipeline_drain(c);  // kernel times of chunks still in flight
+    if (rc) return rc;
     *out = c->stats;
     return NH_OK;
 }
 
 int nh_reset_stats(nh_ctx *c) {
     if (!c) return NH_ERR_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    int rc = pipeline_drain(c);
+    if (rc) return rc;
     std::memset(&c->stats, 0, sizeof(c->stats));
     return NH_OK;
 }
@@ -994,6 +1228,10 @@ int nh_reduce_framebuffers(nh_ctx **ctxs, int32_t n, int32_t root) {
     if (!ctxs || n <= 0 || root < 0 || root >= n) return NH_ERR_INVALID;
     for (int i = 0; i < n; ++i)
         if (!ctxs[i] || !ctxs[i]->has_scene || ctxs[i]->fb_floats != ctxs[0]->fb_floats) return NH_ERR_INVALID;
+    for (int i = 0; i < n; ++i) {
+        (void)hipSetDevice(ctxs[i]->device);
+        if (pipeline_drain(ctxs[i])) return NH_ERR_DEVICE;
+    }
     if (n == 1) return NH_OK;
     std::vector<ncclComm_t> comms(n);
     std::vector<int> devs(n);

@@ -323,3 +323,28 @@ def test_wide_traversal_deep_tree(gpu, tmp_path, monkeypatch):
     assert ctx.stats()["node_bytes"] == 128
     assert ctx.stats()["ray_queries"] == q
     np.testing.assert_array_equal(ref, ctx.framebuffer())
+
+
+def test_pipelined_chunks_match_one_pool(gpu, tmp_path, monkeypatch):
+    """Asynchronous wavefront renders: several nh_render calls, several chunks per call (small
+    memory budget), two path pools overlapping one chunk's last bounces with the next chunk.
+    Splats land in submission order, so the framebuffer equals the one-pool run bit for bit, and
+    both match the oracle."""
+    xml = scenegen.cbox_xml(str(tmp_path), "c1")
+    s = nh.Scene(xml)
+    s.set_resolution(64, 48)
+    b = nh.Bvh(s)
+    monkeypatch.setenv("NH_WF_BUDGET_MB", "2")  # ~3 rounds per chunk at 64x48
+    out = []
+    for pools in ("2", "1"):
+        ctx = nh.Context(0)
+        ctx.upload(s, b)
+        ctx.render(0, 0, clear=True, mode=nh.MODE_WAVEFRONT)
+        for s0 in range(0, 12, 4):
+            ctx.render(s0, s0 + 4, seed=9, traversal=nh.TRAVERSAL_ORDERED, mode=nh.MODE_WAVEFRONT)
+        ctx.synchronize()
+        out.append(ctx.framebuffer())
+        monkeypatch.setenv("NH_POOLS", "1")
+    np.testing.assert_array_equal(out[0], out[1])
+    r = no.OracleScene(s).render(0, 12, seed=9)
+    assert rel_l2(out[0], r) < TOL_REL_L2
