@@ -88,6 +88,40 @@ NHD bool tri_test(float4 a, float4 b, float4 c, F3 o, F3 d, float mint, float ma
     return t >= mint && t <= maxt;
 }
 
+// tri_test without early exits: the same predicates on the same values (so the same answer, NaNs
+// included), evaluated in full. In SIMT code an early return only skips work when every lane of
+// the wave takes it; otherwise it costs a branch and exec-mask bookkeeping per test.
+NHD bool tri_test_nb(float4 a, float4 b, float4 c, F3 o, F3 d, float mint, float maxt, float &t, float &u, float &v) {
+    const F3 p0 = f3(a.x, a.y, a.z), e1 = sub(f3(b.x, b.y, b.z), p0), e2 = sub(f3(c.x, c.y, c.z), p0);
+    const F3 pvec = cross(d, e2);
+    const float det = dot(e1, pvec);
+    const float inv_det = 1.0f / det;
+    const F3 tvec = sub(o, p0);
+    u = dot(tvec, pvec) * inv_det;
+    const F3 qvec = cross(tvec, e1);
+    v = dot(d, qvec) * inv_det;
+    t = dot(e2, qvec) * inv_det;
+    const bool ok_det = !(det > -1e-8f && det < 1e-8f);
+    const bool ok_u = !(u < 0.0f || u > 1.0f);
+    const bool ok_v = !(v < 0.0f || u + v > 1.0f);
+    return ok_det & ok_u & ok_v & (t >= mint) & (t <= maxt);
+}
+
+// box_test for rays whose 1/d components are all finite (no zero direction component): the
+// reference's per-axis t1/t2 swap is min/max (the products are monotone in the bounds, and no NaN
+// arises: finite differences times finite r), and its running max/min with the per-axis early-outs
+// give the same final near/far as one max/min over the axes. Returns the hit test; near in near_out.
+NHD bool box_test_finite(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, F3 o, F3 r, float mint,
+                         float maxt, float &near_out) {
+    const float ax = (mnx - o.x) * r.x, bx = (mxx - o.x) * r.x;
+    const float ay = (mny - o.y) * r.y, by = (mxy - o.y) * r.y;
+    const float az = (mnz - o.z) * r.z, bz = (mxz - o.z) * r.z;
+    const float near_t = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float far_t = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    near_out = near_t;
+    return (near_t <= far_t) & (mint <= far_t) & (near_t <= maxt);
+}
+
 // Sphere::rayIntersect (sphere.cpp:67-94)
 NHD bool sphere_test(float4 a, F3 o, F3 d, float mint, float maxt, float &t) {
     F3 L = sub(o, f3(a.x, a.y, a.z));
@@ -402,6 +436,23 @@ struct RingStack2 {
         lds_ref[o] = ref;
         lds_near[o] = nr;
     }
+    // entries i0 .. i0+m-1 (m <= 3 < K) are about to be written with put(): spill the entries
+    // K below them that still occupy their ring slots
+    NHD void reserve(int i0, int m) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int i = i0 + j;
+            if (j < m && i >= K) {
+                const int o = (i & (K - 1)) * stride;
+                glob[i - K] = make_int2(lds_ref[o], __float_as_int(lds_near[o]));
+            }
+        }
+    }
+    NHD void put(int i, int ref, float nr) {
+        const int o = (i & (K - 1)) * stride;
+        lds_ref[o] = ref;
+        lds_near[o] = nr;
+    }
     NHD void pop(int i, int &ref, float &nr) {
         const int o = (i & (K - 1)) * stride;
         ref = lds_ref[o];
@@ -423,6 +474,13 @@ NHD bool wide_before(bool va, float na, int sa, bool vb, float nb, int sb) {
     return sa < sb;
 }
 
+// wide_before for slots a < b as a branch-free 0/1: does child a come before child b?
+template <bool ORDERED>
+NHD int wide_first(bool va, float na, bool vb, float nb) {
+    // valid before invalid; among valid: nearer first, equal near (never NaN for a hit) in slot order
+    return (va & (!vb | !ORDERED | (na <= nb))) ? 1 : 0;
+}
+
 // Resumable 4-wide traversal (same step protocol as Tracer: one wide node, one primitive or one
 // stack pop per step). Answers: smallest t, ties to the largest leaf-order position k.
 template <bool ORDERED, bool ANY, bool STATS, class Stack>
@@ -433,6 +491,7 @@ struct Tracer4 {
     int k;    // primitive under test, or -1
     int sp;
     bool found, done;
+    bool finite_r;  // all 1/d components finite: branch-free box tests (box_test_finite)
     Hit best;
 
     NHD void begin(const DScene &S, const Traversal &tv, F3 o_, F3 d_, float mint_, float maxt_, TravStats &st) {
@@ -451,6 +510,7 @@ struct Tracer4 {
         k = -1;
         if (S.root_kind == 0 || maxt < mint) return;
         r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        finite_r = fabsf(r.x) < INFINITY && fabsf(r.y) < INFINITY && fabsf(r.z) < INFINITY;
         float near_t;
         if (STATS) st.boxes++;
         if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d,
@@ -461,12 +521,80 @@ struct Tracer4 {
         else cur = 0;
     }
 
+    // One iteration: (pop deferred children until one passes) -> (one wide node) -> (one primitive),
+    // each part only if the lane has that work. A wave executes every part some lane needs anyway,
+    // so chaining them lets a lane do a pop, a node and a primitive for the cost of one divergent
+    // iteration; the per-lane sequence of operations (and so every result and counter) is unchanged.
     NHD void step(const Traversal &tv, Stack &stk, TravStats &st) {
+        if (k < 0 && cur < 0) {  // deferred children: the visit-time test against the current maxt
+            while (sp > 0) {
+                int ref;
+                float nr;
+                stk.pop(--sp, ref, nr);
+                // its box passed with a larger-or-equal maxt; mint <= far does not depend on maxt
+                if (STATS) st.boxes++;
+                if (nr <= maxt) {
+                    enter(ref);
+                    break;
+                }
+            }
+            if (k < 0 && cur < 0) {
+                done = true;
+                return;
+            }
+        }
+        if (cur >= 0) {  // one wide node: test its child boxes
+            const float4 *n = tv.wnodes + (size_t)kWideF4 * cur;
+            const float4 mnx = n[0], mny = n[1], mnz = n[2], mxx = n[3], mxy = n[4], mxz = n[5];
+            const int4 ref = *reinterpret_cast<const int4 *>(&n[6]);
+            float n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f;
+            bool v0, v1, v2, v3;
+            if (finite_r) {
+                v0 = box_test_finite(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, r, mint, maxt, n0) & (ref.x != kWideEmpty);
+                v1 = box_test_finite(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, r, mint, maxt, n1) & (ref.y != kWideEmpty);
+                v2 = box_test_finite(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, r, mint, maxt, n2) & (ref.z != kWideEmpty);
+                v3 = box_test_finite(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, r, mint, maxt, n3) & (ref.w != kWideEmpty);
+            } else {
+                v0 = ref.x != kWideEmpty && box_test(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, d, r, mint, maxt, n0);
+                v1 = ref.y != kWideEmpty && box_test(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, d, r, mint, maxt, n1);
+                v2 = ref.z != kWideEmpty && box_test(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, d, r, mint, maxt, n2);
+                v3 = ref.w != kWideEmpty && box_test(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, d, r, mint, maxt, n3);
+            }
+            if (STATS) {
+                st.nodes++;
+                st.boxes += (ref.x != kWideEmpty) + (ref.y != kWideEmpty) + (ref.z != kWideEmpty) + (ref.w != kWideEmpty);
+            }
+            // Order of the hit children without moving them: rank_i = number of children before i
+            // (wide_before: nearer first / slot order on ties, or slot order alone). cIJ (I < J) says
+            // child I comes before child J; for two valid children exactly one of the two holds.
+            const int c01 = wide_first<ORDERED>(v0, n0, v1, n1), c02 = wide_first<ORDERED>(v0, n0, v2, n2);
+            const int c03 = wide_first<ORDERED>(v0, n0, v3, n3), c12 = wide_first<ORDERED>(v1, n1, v2, n2);
+            const int c13 = wide_first<ORDERED>(v1, n1, v3, n3), c23 = wide_first<ORDERED>(v2, n2, v3, n3);
+            const int rk0 = 3 - c01 - c02 - c03;
+            const int rk1 = c01 + 2 - c12 - c13;
+            const int rk2 = c02 + c12 + 1 - c23;
+            const int rk3 = c03 + c13 + c23;
+            const int nv = (int)v0 + (int)v1 + (int)v2 + (int)v3;
+            if (nv == 0) {
+                cur = -1;
+            } else {
+                // the nearest child is entered; child of rank r >= 1 is deferred at depth
+                // sp + nv-1-r (farthest deepest, as pushing farthest first)
+                stk.reserve(sp, nv - 1);
+                const int top = sp + nv - 1;
+                if (v0 && rk0) stk.put(top - rk0, ref.x, n0);
+                if (v1 && rk1) stk.put(top - rk1, ref.y, n1);
+                if (v2 && rk2) stk.put(top - rk2, ref.z, n2);
+                if (v3 && rk3) stk.put(top - rk3, ref.w, n3);
+                sp = top;
+                enter((v0 && !rk0) ? ref.x : (v1 && !rk1) ? ref.y : (v2 && !rk2) ? ref.z : ref.w);
+            }
+        }
         if (k >= 0) {  // one primitive of the current leaf
             const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
             if (STATS) st.prims++;
             float t, u = 0.f, v = 0.f;
-            const bool hit = prim_is_tri(c) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
+            const bool hit = prim_is_tri(c) ? tri_test_nb(a, b, c, o, d, mint, maxt, t, u, v)
                                             : sphere_test(a, o, d, mint, maxt, t);
             if (hit) {
                 if (ANY) {
@@ -484,54 +612,8 @@ struct Tracer4 {
                 }
             }
             k = (__float_as_int(c.w) & kPrimLeafEnd) ? -1 : k + 1;
-            return;
         }
-        if (cur >= 0) {  // one wide node: test its child boxes
-            const float4 *n = tv.wnodes + (size_t)kWideF4 * cur;
-            const float4 mnx = n[0], mny = n[1], mnz = n[2], mxx = n[3], mxy = n[4], mxz = n[5];
-            const int4 ref = *reinterpret_cast<const int4 *>(&n[6]);
-            float n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f;
-            bool v0 = ref.x != kWideEmpty && box_test(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, d, r, mint, maxt, n0);
-            bool v1 = ref.y != kWideEmpty && box_test(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, d, r, mint, maxt, n1);
-            bool v2 = ref.z != kWideEmpty && box_test(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, d, r, mint, maxt, n2);
-            bool v3 = ref.w != kWideEmpty && box_test(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, d, r, mint, maxt, n3);
-            if (STATS) {
-                st.nodes++;
-                st.boxes += (ref.x != kWideEmpty) + (ref.y != kWideEmpty) + (ref.z != kWideEmpty) + (ref.w != kWideEmpty);
-            }
-            int r0 = ref.x, r1 = ref.y, r2 = ref.z, r3 = ref.w;
-            int s0 = 0, s1 = 1, s2 = 2, s3 = 3;
-            // 4-element sorting network (0,1)(2,3)(0,2)(1,3)(1,2) on (valid, near, slot)
-#define NH_CX(A, B)                                                                           \
-    if (wide_before<ORDERED>(v##B, n##B, s##B, v##A, n##A, s##A)) {                          \
-        bool tv_ = v##A; v##A = v##B; v##B = tv_;                                              \
-        float tn_ = n##A; n##A = n##B; n##B = tn_;                                             \
-        int tr_ = r##A; r##A = r##B; r##B = tr_;                                               \
-        int ts_ = s##A; s##A = s##B; s##B = ts_;                                               \
-    }
-            NH_CX(0, 1) NH_CX(2, 3) NH_CX(0, 2) NH_CX(1, 3) NH_CX(1, 2)
-#undef NH_CX
-            if (!v0) {
-                cur = -1;
-                return;
-            }
-            // the nearest child is entered, the others are deferred (farthest pushed first)
-            if (v3) stk.push(sp++, r3, n3);
-            if (v2) stk.push(sp++, r2, n2);
-            if (v1) stk.push(sp++, r1, n1);
-            enter(r0);
-            return;
-        }
-        if (sp > 0) {  // one deferred child: the visit-time test against the current maxt
-            int ref;
-            float nr;
-            stk.pop(--sp, ref, nr);
-            // its box passed with a larger-or-equal maxt; mint <= far does not depend on maxt
-            if (STATS) st.boxes++;
-            if (nr <= maxt) enter(ref);
-            return;
-        }
-        done = true;
+        if (k < 0 && cur < 0 && sp == 0) done = true;
     }
 
     NHD void enter(int ref) {

@@ -262,6 +262,7 @@ __device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S,
         Stk s = PtStack<true>::make(stk, L);
         Tracer4<ORDERED, ANY, STATS, Stk> tr;
         tr.begin(S, tv, o, d, mint, maxt, st);
+#pragma unroll 1
         while (!tr.done) tr.step(tv, s, st);
         h = tr.best;
         return tr.found;
@@ -271,7 +272,7 @@ __device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S,
 }
 
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool WIDE>
-__global__ __launch_bounds__(128) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(7))) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[kRingEntries * 128];
     const DScene &S = *Sp;
     const QView qv = queue_view(L.cnt_in + (ANY ? kCountGroup : 0));

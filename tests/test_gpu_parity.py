@@ -34,6 +34,9 @@ def random_rays(n, lo, hi, seed):
     maxt[::7] = rng.uniform(0.1, 3.0, size=maxt[::7].shape).astype(np.float32)
     d[::11, 0] = 0.0
     d[::13, 1] = 0.0
+    # a denormal component (1/d = inf: the general slab path) and a tiny one (huge finite 1/d)
+    d[5::17, 2] = 1e-39
+    d[3::19, 1] = 3e-30
     return o, d.astype(np.float32), mint, maxt
 
 
