@@ -10,15 +10,15 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 CXX      ?= g++
 ARCH     ?= gfx950
 PKG      := optix-renderer_amd
-LIBDIR   := $(PKG)/lib
-OBJDIR   := build/obj
+LIBDIR   ?= $(PKG)/lib
+OBJDIR   ?= build/obj
 JOBS     ?= 8
 
 FP_FLAGS   := -ffp-contract=off -fno-fast-math
 HOST_FLAGS := -std=c++17 -O2 -fPIC -Wall -Wextra -Wno-unused-parameter $(FP_FLAGS) -Iinclude -I$(PKG)/host -pthread
 HIP_FLAGS  := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) $(FP_FLAGS) \
               -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero \
-              -Iinclude -I$(PKG)/csrc -Wno-unused-result
+              -Iinclude -I$(PKG)/csrc -Wno-unused-result $(EXTRA_HIP)
 
 HOST_SRC := $(PKG)/host/xml_lite.cpp $(PKG)/host/scene_loader.cpp $(PKG)/host/bvh_build.cpp $(PKG)/host/image_io.cpp \
             $(PKG)/host/png_decode.cpp

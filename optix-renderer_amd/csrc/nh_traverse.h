@@ -419,6 +419,13 @@ struct Tracer {
 //   [6]    int4 child refs: >= 0 wide node, kWideEmpty unused slot, else leaf ~first primitive
 //   [7]    unused
 constexpr int kWideF4 = 8;
+// work per Tracer4::step for a lane: up to this many wide nodes, then up to this many primitives
+#ifndef NH_NODES_PER_STEP
+#define NH_NODES_PER_STEP 1
+#endif
+#ifndef NH_PRIMS_PER_STEP
+#define NH_PRIMS_PER_STEP 2
+#endif
 constexpr int kWideEmpty = (int)0x80000000;
 
 // Traversal stack of one lane, (ref, entry distance) pairs: the top K entries live in LDS
@@ -543,7 +550,8 @@ struct Tracer4 {
                 return;
             }
         }
-        if (cur >= 0) {  // one wide node: test its child boxes
+#pragma unroll 1
+        for (int it = 0; it < NH_NODES_PER_STEP && cur >= 0; ++it) {  // one wide node: test its child boxes
             const float4 *n = tv.wnodes + (size_t)kWideF4 * cur;
             const float4 mnx = n[0], mny = n[1], mnz = n[2], mxx = n[3], mxy = n[4], mxz = n[5];
             const int4 ref = *reinterpret_cast<const int4 *>(&n[6]);
@@ -590,7 +598,8 @@ struct Tracer4 {
                 enter((v0 && !rk0) ? ref.x : (v1 && !rk1) ? ref.y : (v2 && !rk2) ? ref.z : ref.w);
             }
         }
-        if (k >= 0) {  // one primitive of the current leaf
+#pragma unroll 1
+        for (int it = 0; it < NH_PRIMS_PER_STEP && k >= 0; ++it) {  // one primitive of the current leaf
             const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
             if (STATS) st.prims++;
             float t, u = 0.f, v = 0.f;

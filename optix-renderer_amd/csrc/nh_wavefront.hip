@@ -271,6 +271,9 @@ __device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S,
     }
 }
 
+#ifndef NH_REFILL_MIN
+#define NH_REFILL_MIN 32
+#endif
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool WIDE>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(7))) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[kRingEntries * 128];
@@ -292,7 +295,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(7))) void w
     for (;;) {
         const bool idle = slot < 0;
         const unsigned long long im = __ballot(idle);
-        if (im) {
+        // refill once enough lanes are idle (each refill costs the ray fetch, 1/d and the root box
+        // test), or when the whole wave is idle
+        if (im && (__popcll(im) >= NH_REFILL_MIN || im == ~0ull)) {
             while (batch_next >= batch_end && tried < kQueueShards) {  // wave-uniform refill
                 const int lo = (int)((long long)seg * n / kQueueShards);
                 const int hi = (int)((long long)(seg + 1) * n / kQueueShards);

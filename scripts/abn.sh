@@ -1,0 +1,16 @@
+#!/usr/bin/env bash
+# Interleaved A/B/... of several library builds in one GPU session.
+# usage: scripts/abn.sh ROUNDS "libdirA libdirB ..." bench-args...   (libdir relative to optix-renderer_amd/)
+set -u
+n=$1; libs=$2; shift 2
+mkdir -p gpurun_out
+for i in $(seq 1 $n); do
+  for v in $libs; do
+    export NH_LIB_PATH=$PWD/optix-renderer_amd/$v/libnori_hip.so
+    timeout -k 10 300 python bench.py --no-cpu --no-calibrate "$@" > gpurun_out/ab_$v.$i.log 2>&1 || { echo "fail $v $i"; tail -3 gpurun_out/ab_$v.$i.log; exit 99; }
+    python3 -c "
+import json
+d=json.loads(open('gpurun_out/ab_$v.$i.log').read().strip().splitlines()[-1])
+print('$v', $i, d['value'], d['ms_per_step'])"
+  done
+done
