@@ -633,7 +633,7 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
 // reference's order and the image is bit-identical to a one-pool run.
 // ============================================================================================
 
-constexpr size_t kWfBytesPerPath = 2 * (16 * 7 + 8 + 4 + 4 + 4 + 1) + 36;  // two buffers + shadow queue
+constexpr size_t kWfBytesPerPath = 2 * (16 * 6 + 8 + 1) + 36;  // two buffers + shadow queue
 
 static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t staging_f4) {
     if (!p.stream) {
@@ -660,8 +660,7 @@ static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t staging_f4) {
         bool ok = true;
         for (WfBuf &B : W.buf)
             ok = ok && alloc(B.ray_o, nq) && alloc(B.ray_d, nq) && alloc(B.hit, nq) && alloc(B.rng, nq) &&
-                 alloc(B.li, nq) && alloc(B.thr, nq) && alloc(B.pend_ems, nq) && alloc(B.pend_col, nq) &&
-                 alloc(B.pdfmat, nq) && alloc(B.flags, nq) && alloc(B.pid, nq) && alloc(B.occl, nq);
+                 alloc(B.li, nq) && alloc(B.thr, nq) && alloc(B.pend, nq) && alloc(B.occl, nq);
         ok = ok && alloc(W.sh_o, nq) && alloc(W.sh_d, nq) && alloc(W.sh_slot, nq) && alloc(W.counts, 2 * kCountSlot) &&
              alloc(p.rec, n) && alloc(p.rec_jy, n);
         if (!ok) {
@@ -931,9 +930,13 @@ static int pool_finish(nh_ctx *c, WfPool &p) {
     // (Bounces shaded by wf_shade only; the tail kernel's work is not part of this account.)
     for (size_t b = 0; b + 1 < p.in_e.size(); ++b) {
         const uint64_t shaded = p.in_e[b], nsh = p.in_s[b], ne = p.in_e[b + 1], ns = p.in_s[b + 1];
-        const uint64_t loads = b == 0 ? shaded * (16 + 20) : shaded * (96 + 16) + nsh * 17;
+        // bounce 0: hit in, sample record out. Later: path state (ray_o, ray_d, li, thr 16 B each,
+        // rng 8 B) + hit in, the occlusion byte of a queued light sample (its 16-B pending term is
+        // read only when unoccluded, not counted); out: survivors' state, the pending term + shadow
+        // ray of each queued light sample, the radiance of each finished path
+        const uint64_t loads = b == 0 ? shaded * (16 + 20) : shaded * (72 + 16) + nsh * 1;
         c->stats.paths_shaded += shaded;
-        c->stats.shade_state_bytes += loads + ne * 116 + ns * 36 + (shaded - ne) * 12;
+        c->stats.shade_state_bytes += loads + ne * 72 + ns * (16 + 36) + (shaded - ne) * 12;
         c->stats.extend_queue_bytes += shaded * (b == 0 ? 16 : 48);
         c->stats.shadow_queue_bytes += nsh * 37;  // ray in, path slot, occlusion byte out
     }
@@ -1090,6 +1093,11 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         budget = (size_t)std::max(1L, std::atol(e)) << 20;
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / per_round_bytes));
     while ((size_t)chunk * per_round > (size_t)0x7fffffff) chunk = std::max(1, chunk / 2);
+    if (wavefront) {  // path ids of a chunk are packed into 26 bits of the path state (nh_wavefront.hip)
+        if (per_round > ((size_t)1 << 26))
+            return fail(c, "wavefront mode renders at most 2^26 pixels per context"), NH_ERR_UNSUPPORTED;
+        chunk = std::min(chunk, (int)(((size_t)1 << 26) / per_round));
+    }
 
     if (wavefront) {
         HIP_TRY(c, hipStreamSynchronize(c->stream));  // pixel list / clear / counters are in place

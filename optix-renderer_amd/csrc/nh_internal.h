@@ -67,16 +67,13 @@ constexpr int kQueueShards = 8, kCountStride = 32;
 // Wavefront path state (nh_wavefront.hip): one side of the double-buffered, dense SoA state.
 // Slot s of a buffer holds one live path; pid is its sample-record index (round * n_list + entry).
 struct WfBuf {
-    float4 *ray_o, *ray_d;   // (origin, mint), (direction, maxt) of the ray to trace next
+    float4 *ray_o;           // (origin, pdf of the BSDF sample that made the ray); mint = Epsilon
+    float4 *ray_d;           // (direction, flags << kPidBits | pid); maxt = +inf, -inf for d = 0
     float4 *hit;             // (t, u, v, prim index bits or -1) from the extend kernel
     uint64_t *rng;           // pcg32 state (inc is derived from the sample index)
     float4 *li;              // (Li, w_mats)
-    float4 *thr;             // (throughput, w_ems)
-    float4 *pend_ems;        // pending NEE: (Li_ems, pdfems)
-    float4 *pend_col;        // pending BSDF sample: (bsdf_col, pdfems_mats)
-    float *pdfmat;           // pending BSDF sample pdf (MIS weight of an emitter hit)
-    int *flags;              // measure | F_FIRST | F_NEE | path_mats counter
-    int *pid;
+    float4 *thr;             // (throughput, w_ems if the queued shadow ray is occluded)
+    float4 *pend;            // queued NEE: (w_ems * t * Li_ems, w_ems if unoccluded)
     uint8_t *occl;           // any-hit result of the path's shadow ray
 };
 struct WfState {

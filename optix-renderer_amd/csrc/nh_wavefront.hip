@@ -35,7 +35,15 @@ using namespace nhd;
 
 namespace {
 
-enum : int { F_FIRST = 1 << 2, F_NEE = 1 << 3 };  // bits 0-1: measure; bits 4-5: path_mats counter
+// Path flags. Stored (6 bits, packed with the path id into ray_d.w):
+//   F_DISCRETE  the BSDF sample of the last bounce was discrete (path_mis.cpp:136-140)
+//   F_NEE       the last bounce queued a shadow ray; its contribution waits in pend
+//   F_ZERO_COL  the last BSDF sample's weight was zero (isZero, path_mis.cpp:115): no MIS probe
+//   F_ZNAN      (w_ems * t) * 0 of an occluded light sample would not be 0 (non-finite t)
+//   bits 4-5    path_mats bounce counter
+// F_FIRST (bounce 0, paths straight from the camera) lives in registers only.
+enum : int { F_DISCRETE = 1, F_NEE = 2, F_ZERO_COL = 4, F_ZNAN = 8, F_FIRST = 64 };
+constexpr int kPidBits = 26;  // path id bits of ray_d.w (nh_api.hip caps a chunk at 2^26 paths)
 
 // rank of this lane among the wave's lanes with pred set, offset by the wave's reservation in
 // *counter (an LDS counter here)
@@ -86,24 +94,29 @@ __device__ __forceinline__ void flush_trav_stats(unsigned long long *dst, unsign
 // the state one shade step produces for a surviving path
 struct PState {
     float4 ro, rd;   // next ray (origin, mint), (direction, maxt)
-    float4 li, thr;  // (Li, w_mats), (throughput, w_ems)
-    float4 pe, pc;   // pending NEE (Li_ems, pdfems), pending BSDF sample (bsdf_col, pdfems_mats)
-    float pdfmat;
+    float4 li, thr;  // (Li, w_mats), (throughput, w_ems if the shadow ray is occluded)
+    float4 pe;       // queued NEE: (w_ems * t * Li_ems, w_ems if the shadow ray is unoccluded)
+    float pdfmat;    // pdf of the BSDF sample (MIS weight of an emitter the probe may hit)
     uint64_t rng;
     int flags, pid;
 };
 
+// HBM layout of a path (WfBuf): mint of a bounce ray is always Epsilon and maxt +inf, or -inf for
+// the zero direction Diffuse::sample leaves behind, so those two words carry pdfmat and
+// (flags << kPidBits | pid) instead.
 __device__ __forceinline__ void store_state(const WfBuf &B, int s, const PState &o) {
-    B.ray_o[s] = o.ro;
-    B.ray_d[s] = o.rd;
+    B.ray_o[s] = make_float4(o.ro.x, o.ro.y, o.ro.z, o.pdfmat);
+    B.ray_d[s] = make_float4(o.rd.x, o.rd.y, o.rd.z, __int_as_float((int)(((unsigned)o.flags << kPidBits) | (unsigned)o.pid)));
     B.li[s] = o.li;
     B.thr[s] = o.thr;
-    B.pend_ems[s] = o.pe;
-    B.pend_col[s] = o.pc;
-    B.pdfmat[s] = o.pdfmat;
+    if (o.flags & F_NEE) B.pend[s] = o.pe;
     B.rng[s] = o.rng;
-    B.flags[s] = o.flags;
-    B.pid[s] = o.pid;
+}
+
+// the traced ray of a stored path state
+__device__ __forceinline__ void unpack_ray(float4 &ro, float4 &rd) {
+    ro.w = kEps;
+    rd.w = (rd.x == 0 && rd.y == 0 && rd.z == 0) ? -INFINITY : INFINITY;
 }
 
 }  // namespace
@@ -139,6 +152,7 @@ __device__ __forceinline__ void load_ray(const DScene &S, const WfLaunch &L, con
     } else {
         ro = B.ray_o[s];
         rd = B.ray_d[s];
+        unpack_ray(ro, rd);
     }
 }
 
@@ -368,8 +382,9 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
         rd = B.ray_d[s];
         li4 = B.li[s];
         th4 = B.thr[s];
-        flags = B.flags[s];
-        pid = B.pid[s];
+        const int bits = __float_as_int(rd.w);
+        flags = (int)((unsigned)bits >> kPidBits);
+        pid = bits & ((1 << kPidBits) - 1);
         rng.state = B.rng[s];
         rng.inc = ((uint64_t)(L.s0 + pid / L.n_list) << 1u) | 1u;
     }
@@ -387,7 +402,6 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
     const float n_lights = (float)S.n_emitters;
     bool alive = true;
     if (S.integrator == 1) {  // ---------------- path_mats (path_mats.cpp:16-78)
-        if (!(flags & F_FIRST)) t = mulc(t, xyz(B.pend_col[s]));
         if (!found) {  // path_mats.cpp:26-35
             if (S.envmap >= 0) li = add(li, mulc(t, env_eval(S, d)));
             alive = false;
@@ -410,8 +424,7 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
                 int measure;
                 const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure);
                 const F3 nd = to_world(its.sh, wo);
-                o.pc = make_float4(col.x, col.y, col.z, 0.f);
-                o.pe = make_float4(0.f, 0.f, 0.f, 0.f);
+                t = mulc(t, col);  // path_mats.cpp: the throughput update of this bounce
                 o.pdfmat = 0.f;
                 o.ro = make_float4(its.p.x, its.p.y, its.p.z, kEps);
                 o.rd = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
@@ -420,36 +433,30 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
         }
     } else {  // ---------------- path_mis
         if (!(flags & F_FIRST)) {  // finish the previous bounce (path_mis.cpp:103-146)
-            const float4 pc = B.pend_col[s];
-            const F3 bsdf_col = xyz(pc);
-            F3 li_ems = f3(0, 0, 0);
-            float pdfems = 0.f, pdfems_mats = 0.f;
-            if (flags & F_NEE) {  // a queued light sample counts unless occluded (an unqueued one is all zero)
-                const float4 pe = B.pend_ems[s];
+            // the light sample counts unless occluded: its MIS-weighted term was computed by that
+            // bounce, Li += w_ems * t * Li_ems (:142), and w_ems is the unoccluded weight (:103-106)
+            if (flags & F_NEE) {
                 if (!B.occl[s]) {
-                    li_ems = xyz(pe);
-                    pdfems = pe.w;
-                    pdfems_mats = pc.w;
+                    const float4 pe = B.pend[s];
+                    li = add(li, xyz(pe));
+                    w_ems = pe.w;
+                } else if (flags & F_ZNAN) {
+                    li = add(li, f3(NAN, NAN, NAN));  // (w_ems * t) * 0 with a non-finite product
                 }
             }
-            if ((pdfems_mats + pdfems) > kEps) w_ems = pdfems / (pdfems_mats + pdfems);
-            if (!is_zero(bsdf_col) && found) {
+            // the MIS probe hit an emitter (:117-133): w_mats from the pdfs of both strategies
+            if (!(flags & F_ZERO_COL) && found) {
                 hit_info(S, tv, h, org, d, its);
                 have_its = true;
                 const int hem = S.shapes[its.shape].emitter;
                 if (hem >= 0) {
-                    const float pdfmat = B.pdfmat[s];
+                    const float pdfmat = ro.w;
                     const F3 wim = normalized(sub(its.p, org));
                     const float pdfmat_ems = emitter_pdf(S, S.emitters[hem], org, its.p, its.sh.n, wim) / n_lights;
                     if ((pdfmat + pdfmat_ems) > kEps) w_mats = pdfmat / (pdfmat + pdfmat_ems);
                 }
             }
-            if ((flags & 3) == M_DISCRETE) {
-                w_ems = 0.f;
-                w_mats = 1.f;
-            }
-            li = add(li, mulc(scl(w_ems, t), li_ems));
-            t = mulc(t, bsdf_col);
+            if (flags & F_DISCRETE) w_mats = 1.f;  // :136-140
         }
         if (!found) {  // path_mis.cpp:32-44: escaped rays see the environment map, no MIS weight
             if (S.envmap >= 0) li = add(li, mulc(t, env_eval(S, d)));
@@ -494,12 +501,29 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
                 const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
                 const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
                 const F3 nd = to_world(its.sh, wo);
-                o.pe = make_float4(li_ems.x, li_ems.y, li_ems.z, pdfems);
-                o.pc = make_float4(bsdf_col.x, bsdf_col.y, bsdf_col.z, pdfems_mats);
+                // w_ems of this bounce (:103-106): the occluded shadow ray leaves both pdfs 0 (w_ems
+                // keeps its value), the unoccluded one sets it from them; a discrete sample zeroes
+                // it either way (:136-140)
+                const bool discrete = measure == M_DISCRETE;
+                float w_occ = w_ems, w_un = w_ems;
+                if (nee && (pdfems_mats + pdfems) > kEps) w_un = pdfems / (pdfems_mats + pdfems);
+                if (discrete) w_occ = w_un = 0.f;
+                int fl = (discrete ? F_DISCRETE : 0) | (is_zero(bsdf_col) ? F_ZERO_COL : 0);
+                if (nee) {
+                    // Li += w_ems * t * Li_ems (:142) once the shadow ray is known to be unoccluded
+                    const F3 c = mulc(scl(w_un, t), li_ems);
+                    o.pe = make_float4(c.x, c.y, c.z, w_un);
+                    const F3 z = mulc(scl(w_occ, t), f3(0, 0, 0));
+                    fl |= F_NEE | ((z.x != 0.f || z.y != 0.f || z.z != 0.f) ? F_ZNAN : 0);
+                } else {
+                    li = add(li, mulc(scl(w_occ, t), li_ems));  // li_ems = 0: the same term, added now
+                }
+                w_ems = w_occ;
+                t = mulc(t, bsdf_col);  // :145
                 o.pdfmat = pdfmat;
                 o.ro = make_float4(its.p.x, its.p.y, its.p.z, kEps);
                 o.rd = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
-                o.flags = (measure & 3) | (nee ? F_NEE : 0);
+                o.flags = fl;
             }
         }
     }
