@@ -13,7 +13,7 @@ rows = []
 with open(path) as f:
     for r in csv.DictReader(f):
         name = r["Kernel_Name"]
-        if name.startswith(pat) or f" {pat}<" in name or f" {pat}(" in name:
+        if pat in name:
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), name))
 rows.sort()
 tail = rows[-n:]
