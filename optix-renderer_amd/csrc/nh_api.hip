@@ -538,6 +538,9 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     c->n_node_f4 = (int)nodes.size();
     c->n_leaves = (int)leaves.size();
     c->n_prim_f4 = (int)prims.size();
+    // one zero record past the end: the 4-wide traversal loads record k+1 together with record k
+    // (and tests it only when k does not end its leaf)
+    prims.resize(prims.size() + 3, make_float4(0.f, 0.f, 0.f, 0.f));
     if ((rc = upload(c, c->bvh_bufs, nodes.data(), nodes.size(), &c->tv.nodes))) return rc;
     if ((rc = upload(c, c->bvh_bufs, leaves.data(), leaves.size(), &c->tv.leaves))) return rc;
     if ((rc = upload(c, c->bvh_bufs, prims.data(), prims.size(), &c->tv.prims))) return rc;

@@ -419,13 +419,11 @@ struct Tracer {
 //   [6]    int4 child refs: >= 0 wide node, kWideEmpty unused slot, else leaf ~first primitive
 //   [7]    unused
 constexpr int kWideF4 = 8;
-// work per Tracer4::step for a lane: up to this many wide nodes, then up to this many primitives
+// work per Tracer4::step for a lane: up to this many wide nodes, then up to two primitives
 #ifndef NH_NODES_PER_STEP
 #define NH_NODES_PER_STEP 1
 #endif
-#ifndef NH_PRIMS_PER_STEP
-#define NH_PRIMS_PER_STEP 2
-#endif
+
 constexpr int kWideEmpty = (int)0x80000000;
 
 // Traversal stack of one lane, (ref, entry distance) pairs: the top K entries live in LDS
@@ -598,31 +596,40 @@ struct Tracer4 {
                 enter((v0 && !rk0) ? ref.x : (v1 && !rk1) ? ref.y : (v2 && !rk2) ? ref.z : ref.w);
             }
         }
-#pragma unroll 1
-        for (int it = 0; it < NH_PRIMS_PER_STEP && k >= 0; ++it) {  // one primitive of the current leaf
-            const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
-            if (STATS) st.prims++;
-            float t, u = 0.f, v = 0.f;
-            const bool hit = prim_is_tri(c) ? tri_test_nb(a, b, c, o, d, mint, maxt, t, u, v)
-                                            : sphere_test(a, o, d, mint, maxt, t);
-            if (hit) {
-                if (ANY) {
-                    found = true;
-                    done = true;
-                    return;
-                }
-                if (t < maxt || k > best.k) {
-                    found = true;
-                    maxt = t;
-                    best.t = t;
-                    best.u = u;
-                    best.v = v;
-                    best.k = k;
-                }
+        if (k >= 0) {  // up to two primitives of the current leaf, both records fetched at once
+            const float4 a0 = tv.prims[3 * k], b0 = tv.prims[3 * k + 1], c0 = tv.prims[3 * k + 2];
+            const float4 a1 = tv.prims[3 * k + 3], b1 = tv.prims[3 * k + 4], c1 = tv.prims[3 * k + 5];
+            if (prim(a0, b0, c0, st)) return;
+            if (k >= 0) {
+                if (prim(a1, b1, c1, st)) return;
             }
-            k = (__float_as_int(c.w) & kPrimLeafEnd) ? -1 : k + 1;
         }
         if (k < 0 && cur < 0 && sp == 0) done = true;
+    }
+
+    // test record k (a, b, c) and advance k; true when an any-hit query is answered
+    NHD bool prim(const float4 &a, const float4 &b, const float4 &c, TravStats &st) {
+        if (STATS) st.prims++;
+        float t, u = 0.f, v = 0.f;
+        const bool hit = prim_is_tri(c) ? tri_test_nb(a, b, c, o, d, mint, maxt, t, u, v)
+                                        : sphere_test(a, o, d, mint, maxt, t);
+        if (hit) {
+            if (ANY) {
+                found = true;
+                done = true;
+                return true;
+            }
+            if (t < maxt || k > best.k) {
+                found = true;
+                maxt = t;
+                best.t = t;
+                best.u = u;
+                best.v = v;
+                best.k = k;
+            }
+        }
+        k = (__float_as_int(c.w) & kPrimLeafEnd) ? -1 : k + 1;
+        return false;
     }
 
     NHD void enter(int ref) {

@@ -288,8 +288,11 @@ __device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S,
 #ifndef NH_REFILL_MIN
 #define NH_REFILL_MIN 32
 #endif
+#ifndef NH_PT_WAVES
+#define NH_PT_WAVES 6
+#endif
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool WIDE>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(7))) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES))) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[kRingEntries * 128];
     const DScene &S = *Sp;
     const QView qv = queue_view(L.cnt_in + (ANY ? kCountGroup : 0));
@@ -544,7 +547,10 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
 // One queue entry per thread; survivors are ranked within the workgroup (wave ballots + LDS
 // atomics), the workgroup reserves its ranges of the next buffer and the shadow queue with one
 // device-scope atomic each, then every thread stores its state at its final slot.
-__global__ __launch_bounds__(256, 4) void wf_shade(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+#ifndef NH_SHADE_WAVES
+#define NH_SHADE_WAVES 4
+#endif
+__global__ __launch_bounds__(256, NH_SHADE_WAVES) void wf_shade(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ unsigned s_n[2], s_base[2];
     const DScene &S = *Sp;
     const QView qv = queue_view(L.cnt_in);
