@@ -774,8 +774,9 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     L.trav_spill = p.spill;
     L.spill_depth = p.spill_words;
     // measured on 16.7M-path chunks: C2 3025 / 3030 / 2692 Msamples/s at 64k / 262k / 1M,
-    // bumpy-1M 708 / 744 / 739 / 603 at 64k / 262k / 1M / 3M
-    p.tail_at = std::max<int64_t>(n_paths / 64, 8192);
+    // bumpy-1M 708 / 744 / 739 / 603 at 64k / 262k / 1M / 3M; 67M-path C4 chunks 2102 / 2206 / 2226 / 2209
+    // at 1M / 262k / 131k / 64k
+    p.tail_at = std::min<int64_t>(std::max<int64_t>(n_paths / 64, 8192), 262144);
     if (const char *e = std::getenv("NH_TAIL")) p.tail_at = std::atoll(e);
     // below this many live paths the pool counts as draining: the next chunk may start beside it
     p.drain_at = std::max<int64_t>(n_paths / 8, p.tail_at);
