@@ -818,7 +818,9 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
     HIP_TRY(c, hipEventRecord(ev[0], p.stream));
     nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, p.persistent, p.wide, bound, c->depth, p.stream);
     HIP_TRY(c, hipEventRecord(ev[1], p.stream));
-    nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, p.persistent, p.wide, bound, c->depth, p.stream);
+    // bounce 0 has no shadow rays (the launch still runs: the kernels read the count on the device)
+    nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, p.persistent, p.wide, it == 0 ? 0 : bound, c->depth,
+                        p.stream);
     HIP_TRY(c, hipEventRecord(ev[2], p.stream));
     if (it > 0 && (int64_t)bound <= p.tail_at) {
         nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, p.wide, bound, c->depth, p.stream);

@@ -233,7 +233,10 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
 // traversal finished before the next Tracer step. A wave thus stays busy until the pool is empty
 // instead of waiting for its slowest ray (the 64-lane divergence that made one wave execute
 // ~10x the instructions of an average ray on the 1M-triangle scene).
-constexpr int kFetchBatch = 64;
+#ifndef NH_FETCH_BATCH
+#define NH_FETCH_BATCH 128
+#endif
+constexpr int kFetchBatch = NH_FETCH_BATCH;
 constexpr int kTraceBlocksMax = 1 << 20;
 constexpr int kRingEntries = 16;
 //
