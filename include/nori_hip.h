@@ -266,6 +266,11 @@ int nh_write_pfm(const char *path, const float *rgb, int32_t width, int32_t heig
    NULL (or cap too small) to query the size */
 int nh_image_load_png(const char *path, uint8_t *rgba, size_t cap, int32_t *width, int32_t *height);
 int nh_write_exr(const char *path, const float *rgb, int32_t width, int32_t height);
+/* Bitmap::saveToLDR (src/utils/bitmap.cpp:122-140): sRGB gamma (GammaCorrect, :109-112), bytes
+ * (uint8_t)Clamp(255 * v + 0.5, 0, 255) per channel, written as an 8-bit RGB PNG. nh_rgb_to_ldr
+ * produces the bytes only (3 per pixel, row 0 first). */
+int nh_rgb_to_ldr(const float *rgb, int32_t width, int32_t height, uint8_t *rgb8);
+int nh_write_png(const char *path, const float *rgb, int32_t width, int32_t height);
 
 /* device side */
 int nh_get_device_count(int *n);

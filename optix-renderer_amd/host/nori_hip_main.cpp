@@ -3,7 +3,8 @@
 // rendering the scene's path_mis / path_mats integrator on one MI355X through the
 // C-ABI and writing <scene>.exr next to the input (Bitmap::save, bitmap.cpp:82-110).
 //
-//   nori_hip scene.xml [--spp N] [--width W --height H] [--device D] [--ordered] [--pfm out.pfm]
+//   nori_hip scene.xml [--spp N] [--width W --height H] [--device D] [--ordered] [--pfm out.pfm] [--png]
+// --png also writes <scene>.png as Bitmap::saveToLDR (bitmap.cpp:122-140; the reference's hdrToLdr).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -20,10 +21,11 @@ static int die(const char *what, const char *msg) {
 
 int main(int argc, char **argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: nori_hip scene.xml [--spp N] [--width W --height H] [--device D] [--ordered] [--pfm out]\n");
+        std::fprintf(stderr, "usage: nori_hip scene.xml [--spp N] [--width W --height H] [--device D] [--ordered] [--pfm out] [--png]\n");
         return 1;
     }
     std::string scene_path = argv[1], pfm;
+    bool png = false;
     int spp = 0, w = 0, h = 0, device = 0, traversal = NH_TRAVERSAL_REFERENCE;
     for (int i = 2; i < argc; ++i) {
         std::string a = argv[i];
@@ -34,6 +36,7 @@ int main(int argc, char **argv) {
         else if (a == "--device") device = std::atoi(next());
         else if (a == "--ordered") traversal = NH_TRAVERSAL_ORDERED;
         else if (a == "--pfm") pfm = next();
+        else if (a == "--png") png = true;
         else return die("argument", a.c_str());
     }
     nh_scene *scene = nullptr;
@@ -69,6 +72,7 @@ int main(int argc, char **argv) {
     std::string out = scene_path;
     auto dot = out.find_last_of('.');
     if (dot != std::string::npos) out = out.substr(0, dot);
+    if (png) nh_write_png((out + ".png").c_str(), rgb.data(), W, H);
     out += ".exr";
     nh_write_exr(out.c_str(), rgb.data(), W, H);
     if (!pfm.empty()) nh_write_pfm(pfm.c_str(), rgb.data(), W, H);

@@ -145,6 +145,8 @@ _sig("nh_framebuffer_to_rgb", _i32, _fp, _i32, _i32, _i32, _fp)
 _sig("nh_write_pfm", _i32, C.c_char_p, _fp, _i32, _i32)
 _sig("nh_image_load_png", _i32, C.c_char_p, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(_i32), C.POINTER(_i32))
 _sig("nh_write_exr", _i32, C.c_char_p, _fp, _i32, _i32)
+_sig("nh_write_png", _i32, C.c_char_p, _fp, _i32, _i32)
+_sig("nh_rgb_to_ldr", _i32, _fp, _i32, _i32, C.POINTER(C.c_uint8))
 _sig("nh_get_device_count", _i32, C.POINTER(C.c_int))
 _sig("nh_create", _i32, C.c_int, C.POINTER(_vp))
 _sig("nh_destroy", None, _vp)
@@ -381,6 +383,21 @@ def to_rgb(rgbw: np.ndarray, border: int) -> np.ndarray:
 def write_exr(path: str, rgb: np.ndarray):
     rgb = np.ascontiguousarray(rgb, dtype=np.float32)
     _host_check(_lib.nh_write_exr(path.encode(), _fptr(rgb), rgb.shape[1], rgb.shape[0]), "write_exr")
+
+
+def write_png(path: str, rgb: np.ndarray):
+    """8-bit sRGB PNG as Bitmap::saveToLDR (src/utils/bitmap.cpp:122-140)."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    _host_check(_lib.nh_write_png(path.encode(), _fptr(rgb), rgb.shape[1], rgb.shape[0]), "write_png")
+
+
+def rgb_to_ldr(rgb: np.ndarray) -> np.ndarray:
+    """The bytes write_png stores: (H, W, 3) uint8."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    out = np.empty(rgb.shape[:2] + (3,), np.uint8)
+    _host_check(_lib.nh_rgb_to_ldr(_fptr(rgb), rgb.shape[1], rgb.shape[0],
+                                   out.ctypes.data_as(C.POINTER(C.c_uint8))), "rgb_to_ldr")
+    return out
 
 
 def write_pfm(path: str, rgb: np.ndarray):
