@@ -51,7 +51,10 @@ extern "C" {
 enum { NH_SHAPE_MESH = 0, NH_SHAPE_SPHERE = 1 };
 enum { NH_BSDF_DIFFUSE = 0, NH_BSDF_MIRROR = 1, NH_BSDF_DIELECTRIC = 2, NH_BSDF_MICROFACET = 3 };
 enum { NH_EMITTER_AREA = 0, NH_EMITTER_POINT = 1, NH_EMITTER_ENVMAP = 2 };
-enum { NH_INTEGRATOR_PATH_MIS = 0, NH_INTEGRATOR_PATH_MATS = 1 };
+/* path_mis (src/integrators/path_mis.cpp), path_mats (path_mats.cpp), and the single-bounce
+ * direct_ems / direct_mats / direct_mis (direct_ems.cpp, direct_mats.cpp, direct_mis.cpp) */
+enum { NH_INTEGRATOR_PATH_MIS = 0, NH_INTEGRATOR_PATH_MATS = 1, NH_INTEGRATOR_DIRECT_EMS = 2,
+       NH_INTEGRATOR_DIRECT_MATS = 3, NH_INTEGRATOR_DIRECT_MIS = 4 };
 
 /* One Nori Shape (src/shapes/mesh.cpp, src/shapes/sphere.cpp). Mesh data lives in
  * the scene-wide concatenated arrays at the given offsets. */

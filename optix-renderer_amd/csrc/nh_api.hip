@@ -327,7 +327,9 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         S.env_b = e.radiance[2];
     }
     S.n_emitters = (int)d->n_emitters;
-    S.integrator = d->integrator == NH_INTEGRATOR_PATH_MATS ? 1 : 0;
+    if (d->integrator < NH_INTEGRATOR_PATH_MIS || d->integrator > NH_INTEGRATOR_DIRECT_MIS)
+        return fail(c, "unknown integrator"), NH_ERR_INVALID;
+    S.integrator = d->integrator;
     std::memcpy(S.s2c, d->camera.sample_to_camera, sizeof(S.s2c));
     std::memcpy(S.c2w, d->camera.camera_to_world, sizeof(S.c2w));
     S.inv_w = d->camera.inv_output_size[0];
@@ -1067,9 +1069,13 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     if (!c || !q) return NH_ERR_INVALID;
     if (!c->has_scene || !c->has_bvh) return fail(c, "nh_render: scene and BVH must be uploaded"), NH_ERR_STATE;
     if (q->sample_end < q->sample_begin || q->sample_begin < 0) return fail(c, "invalid sample range"), NH_ERR_INVALID;
-    if (c->integrator == 0 && c->n_emitters == 0) return fail(c, "No Emitter in scene!"), NH_ERR_INVALID;
+    // path_mis throws it (path_mis.cpp:76-79); direct_mis would pick from an empty emitter list
+    if ((c->integrator == NH_INTEGRATOR_PATH_MIS || c->integrator == NH_INTEGRATOR_DIRECT_MIS) && c->n_emitters == 0)
+        return fail(c, "No Emitter in scene!"), NH_ERR_INVALID;
     if (q->mode != NH_MODE_MEGAKERNEL && q->mode != NH_MODE_WAVEFRONT) return fail(c, "unknown render mode"), NH_ERR_INVALID;
-    const bool wavefront = q->mode == NH_MODE_WAVEFRONT;
+    // the single-bounce direct integrators always run as the megakernel: one closest hit, the light
+    // sample(s) and at most one BSDF ray per path leave no bounce loop for path queues to balance
+    const bool wavefront = q->mode == NH_MODE_WAVEFRONT && c->integrator <= NH_INTEGRATOR_PATH_MATS;
     if (q->traversal < NH_TRAVERSAL_REFERENCE || q->traversal > NH_TRAVERSAL_WIDE)
         return fail(c, "unknown traversal"), NH_ERR_INVALID;
     if (c->border > 4) return fail(c, "reconstruction filters wider than border 4 are not supported"), NH_ERR_UNSUPPORTED;

@@ -243,6 +243,134 @@ __global__ __launch_bounds__(64) void nh_trace_wide_kernel(const DScene *__restr
     if (STATS) flush_stats(st, i < n ? 1u : 0u, stat_shard(counters));
 }
 
+
+// ---- single-bounce direct integrators (one closest hit from the camera) --------------------
+// Miss: the environment map, if any (direct_*.cpp:17-26). Hit on an emitter: its radiance toward
+// the camera, unweighted (:33-39).
+#define NH_DIRECT_PROLOGUE                                                                       \
+    Hit h;                                                                                       \
+    if (STATS) queries++;                                                                        \
+    if (!trace<DEPTH, ORDERED, false, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st))      \
+        return S.envmap >= 0 ? env_eval(S, d) : f3(0, 0, 0);                                     \
+    Its its;                                                                                     \
+    hit_info(S, tv, h, o, d, its);                                                               \
+    const DShape shape = S.shapes[its.shape];                                                    \
+    const DBsdf bsdf = S.bsdfs[shape.bsdf];                                                      \
+    F3 result = f3(0, 0, 0);                                                                     \
+    if (shape.emitter >= 0)                                                                      \
+        result = add(result, emitter_eval(S.emitters[shape.emitter], o, its.sh.n, normalized(sub(its.p, o))));
+
+// DirectEMSIntegrator::Li (src/integrators/direct_ems.cpp:14-70): one light sample per emitter, in
+// scene order, each with its own 2D sample; unoccluded ones add li * |cos| * f.
+template <int DEPTH, bool ORDERED, bool STATS>
+__device__ F3 li_direct_ems(const DScene &S, const Traversal &tv, Rng &rng, F3 o, F3 d, float mint, float maxt,
+                            uint32_t *stk, int stride, TravStats &st, uint32_t &queries) {
+    NH_DIRECT_PROLOGUE
+    const F3 wo = to_local(its.sh, neg(d));
+    for (int l = 0; l < S.n_emitters; ++l) {
+        const float ex = rng.next1d(), ey = rng.next1d();
+        ESample es;
+        const F3 li = emitter_sample(S, S.emitters[l], its.p, ex, ey, es);
+        if (is_zero(li)) continue;
+        Hit hs;
+        if (STATS) queries++;
+        if (trace<DEPTH, ORDERED, true, STATS>(tv, S, es.so, es.sd, es.smint, es.smaxt, hs, stk, stride, st)) continue;
+        const F3 we = to_local(its.sh, es.wi);
+        const F3 f = bsdf_eval(bsdf, wo, we, M_SOLID_ANGLE);
+        result = add(result, mulc(scl(fabsf(we.z), li), f));
+    }
+    return result;
+}
+
+// DirectMATSIntegrator::Li (src/integrators/direct_mats.cpp:16-83): one BSDF sample (the record's
+// measure preset to ESolidAngle); its ray adds the environment on a miss or the emitter it hits.
+template <int DEPTH, bool ORDERED, bool STATS>
+__device__ F3 li_direct_mats(const DScene &S, const Traversal &tv, Rng &rng, F3 o, F3 d, float mint, float maxt,
+                             uint32_t *stk, int stride, TravStats &st, uint32_t &queries) {
+    NH_DIRECT_PROLOGUE
+    const float bx = rng.next1d(), by = rng.next1d();
+    F3 wo;
+    int measure;
+    const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure);
+    if (is_zero(col)) return result;
+    const F3 nd = to_world(its.sh, wo);
+    Hit h2;
+    if (STATS) queries++;
+    if (!trace<DEPTH, ORDERED, false, STATS>(tv, S, its.p, nd, kEps, INFINITY, h2, stk, stride, st)) {
+        if (S.envmap >= 0) result = add(result, mulc(env_eval(S, nd), col));
+        return result;
+    }
+    Its its2;
+    hit_info(S, tv, h2, its.p, nd, its2);
+    const int hem = S.shapes[its2.shape].emitter;
+    if (hem >= 0)
+        result = add(result, mulc(emitter_eval(S.emitters[hem], its.p, its2.sh.n, normalized(sub(its2.p, its.p))), col));
+    return result;
+}
+
+// DirectMISIntegrator::Li (src/integrators/direct_mis.cpp:15-143): one emitter picked at random and
+// one BSDF sample, balance-heuristic weights; result + w_ems * result_ems + w_mat * result_mats.
+// Occluded light samples and BSDF rays that miss emitters still fill result_ems / result_mats with
+// the environment (:84-92, :127-135) under a weight of 0.
+template <int DEPTH, bool ORDERED, bool STATS>
+__device__ F3 li_direct_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, F3 d, float mint, float maxt,
+                            uint32_t *stk, int stride, TravStats &st, uint32_t &queries) {
+    NH_DIRECT_PROLOGUE
+    const float n_lights = (float)S.n_emitters;
+    F3 result_ems = f3(0, 0, 0), result_mats = f3(0, 0, 0);
+    float w_ems = 0.f, w_mat = 0.f;
+    const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, rng.next1d());
+    const DEmitter em = S.emitters[ei];
+    const float ex = rng.next1d(), ey = rng.next1d();
+    ESample es;
+    const F3 li = emitter_sample(S, em, its.p, ex, ey, es);
+    const F3 wi_l = to_local(its.sh, neg(d));
+    if (!is_zero(li)) {
+        Hit hs;
+        if (STATS) queries++;
+        if (!trace<DEPTH, ORDERED, true, STATS>(tv, S, es.so, es.sd, es.smint, es.smaxt, hs, stk, stride, st)) {
+            const F3 we = to_local(its.sh, es.wi);
+            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
+            const float cs = we.z;
+            const float pdf_ems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
+            const float pdf_mat = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
+            result_ems = f3(li.x * cs * f.x * n_lights, li.y * cs * f.y * n_lights, li.z * cs * f.z * n_lights);
+            if (pdf_ems + pdf_mat > kEps) w_ems = pdf_ems / (pdf_ems + pdf_mat);
+        } else if (S.envmap >= 0) {
+            result_ems = mulc(li, env_eval(S, es.sd));
+        }
+    }
+    const float bx = rng.next1d(), by = rng.next1d();
+    F3 wo;
+    int measure;
+    const F3 col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
+    if (measure == M_UNKNOWN) measure = M_SOLID_ANGLE;  // bqr_mat.measure = ESolidAngle before sample (:102)
+    if (!is_zero(col)) {
+        const F3 nd = to_world(its.sh, wo);
+        Hit h2;
+        if (STATS) queries++;
+        const bool hit2 = trace<DEPTH, ORDERED, false, STATS>(tv, S, its.p, nd, kEps, INFINITY, h2, stk, stride, st);
+        int hem = -1;
+        Its its2;
+        if (hit2) {
+            hit_info(S, tv, h2, its.p, nd, its2);
+            hem = S.shapes[its2.shape].emitter;
+        }
+        if (hem >= 0) {
+            const DEmitter e2 = S.emitters[hem];
+            const F3 wim = normalized(sub(its2.p, its.p));
+            result_mats = mulc(col, emitter_eval(e2, its.p, its2.sh.n, wim));
+            const float pdf_mat = bsdf_pdf(bsdf, wi_l, wo, measure);
+            const float pdf_e = emitter_pdf(S, e2, its.p, its2.p, its2.sh.n, wim) / n_lights;
+            if (pdf_mat + pdf_e > kEps) w_mat = pdf_mat / (pdf_mat + pdf_e);
+        } else if (S.envmap >= 0) {
+            result_mats = mulc(col, env_eval(S, nd));
+        }
+    }
+    return add(add(result, scl(w_ems, result_ems)), scl(w_mat, result_mats));
+}
+#undef NH_DIRECT_PROLOGUE
+
 template <int BLOCK, int DEPTH, bool ORDERED, bool STATS, int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__restrict__ Sp, Traversal tv, PathLaunch L) {
     __shared__ uint32_t stk[DEPTH * BLOCK];
@@ -264,9 +392,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
         F3 o, d;
         float mint, maxt;
         camera_ray(S, spx, spy, o, d, mint, maxt);
-        F3 li = S.integrator == 1
-                    ? li_path_mats<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries)
-                    : li_path_mis<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries);
+        F3 li;
+        switch (S.integrator) {
+            case 1: li = li_path_mats<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
+            case 2: li = li_direct_ems<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
+            case 3: li = li_direct_mats<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
+            case 4: li = li_direct_mis<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
+            default: li = li_path_mis<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
+        }
         const size_t r = (size_t)k * L.n_list + i;
         L.rec_rgbx[r] = make_float4(li.x, li.y, li.z, jx);
         L.rec_jy[r] = jy;

@@ -29,7 +29,7 @@ NH_OK = 0
 SHAPE_MESH, SHAPE_SPHERE = 0, 1
 BSDF_DIFFUSE, BSDF_MIRROR, BSDF_DIELECTRIC, BSDF_MICROFACET = 0, 1, 2, 3
 EMITTER_AREA, EMITTER_POINT, EMITTER_ENVMAP = 0, 1, 2
-INTEGRATOR_PATH_MIS, INTEGRATOR_PATH_MATS = 0, 1
+INTEGRATOR_PATH_MIS, INTEGRATOR_PATH_MATS, INTEGRATOR_DIRECT_EMS, INTEGRATOR_DIRECT_MATS, INTEGRATOR_DIRECT_MIS = 0, 1, 2, 3, 4
 MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1
 TRAVERSAL_REFERENCE, TRAVERSAL_ORDERED, TRAVERSAL_WIDE = 0, 1, 2
 

@@ -849,6 +849,123 @@ V3 li_path_mats(const no_scene &s, Sampler &smp, const Ray &ray) {  // path_mats
     return li;
 }
 
+
+// ---- single-bounce direct integrators ------------------------------------
+// first hit of the camera ray: miss -> environment (direct_*.cpp:17-26), emitter hit -> its radiance
+static bool direct_first_hit(const no_scene &s, const Ray &ray, Its &its, V3 &result) {
+    if (!bvh_intersect(s, ray, its, false)) {
+        result = s.envmap >= 0 ? env_eval(s, ray.d) : mk(0, 0, 0);
+        return false;
+    }
+    result = mk(0, 0, 0);
+    const nh_shape &shape = s.shapes[its.shape];
+    if (shape.emitter >= 0) result = result + emitter_eval(s, s.emitters[shape.emitter], erec(ray.o, its.p, its.sh.n));
+    return true;
+}
+
+V3 li_direct_ems(const no_scene &s, Sampler &smp, const Ray &ray) {  // direct_ems.cpp:14-70
+    Its its;
+    V3 result;
+    if (!direct_first_hit(s, ray, its, result)) return result;
+    const nh_bsdf &bsdf = s.bsdfs[s.shapes[its.shape].bsdf];
+    const V3 wo = its.sh.to_local(-ray.d);
+    for (const nh_emitter &l : s.emitters) {  // scene->getLights(), each with its own next2D
+        ERec eqr;
+        eqr.ref = its.p;
+        float ex, ey;
+        smp.next2d(ex, ey);
+        V3 li = emitter_sample(s, l, eqr, ex, ey);
+        if (is_zero(li)) continue;
+        Its dummy;
+        if (bvh_intersect(s, eqr.shadow, dummy, true)) continue;
+        BRec bq;
+        bq.wi = wo;
+        bq.wo = its.sh.to_local(eqr.wi);
+        bq.measure = ESolidAngle;
+        V3 f = bsdf_eval(bsdf, bq);
+        result = result + cmul(li * std::abs(its.sh.to_local(eqr.wi).z), f);
+    }
+    return result;
+}
+
+V3 li_direct_mats(const no_scene &s, Sampler &smp, const Ray &ray) {  // direct_mats.cpp:16-83
+    Its its;
+    V3 result;
+    if (!direct_first_hit(s, ray, its, result)) return result;
+    const nh_bsdf &bsdf = s.bsdfs[s.shapes[its.shape].bsdf];
+    BRec br;
+    br.wi = its.sh.to_local(-ray.d);
+    br.measure = ESolidAngle;
+    float bx, by;
+    smp.next2d(bx, by);
+    V3 col = bsdf_sample(bsdf, br, bx, by);
+    if (is_zero(col)) return result;
+    Ray sec = make_ray(its.p, its.sh.to_world(br.wo));
+    Its its2;
+    if (!bvh_intersect(s, sec, its2, false)) {
+        if (s.envmap >= 0) result = result + cmul(env_eval(s, sec.d), col);
+        return result;
+    }
+    const nh_shape &hs = s.shapes[its2.shape];
+    if (hs.emitter >= 0) result = result + cmul(emitter_eval(s, s.emitters[hs.emitter], erec(its.p, its2.p, its2.sh.n)), col);
+    return result;
+}
+
+V3 li_direct_mis(const no_scene &s, Sampler &smp, const Ray &ray) {  // direct_mis.cpp:15-143
+    Its its;
+    V3 result;
+    if (!direct_first_hit(s, ray, its, result)) return result;
+    const nh_bsdf &bsdf = s.bsdfs[s.shapes[its.shape].bsdf];
+    const float n_lights = (float)s.emitters.size();
+    V3 result_ems = mk(0, 0, 0), result_mats = mk(0, 0, 0);
+    float w_ems = 0.f, w_mat = 0.f;
+    size_t ei = dpdf_sample(s.emitter_cdf.data(), s.emitter_cdf.size(), smp.next1d());
+    const nh_emitter &l_ems = s.emitters[ei];
+    ERec eqr;
+    eqr.ref = its.p;
+    float ex, ey;
+    smp.next2d(ex, ey);
+    V3 li = emitter_sample(s, l_ems, eqr, ex, ey);
+    if (!is_zero(li)) {
+        Its dummy;
+        if (!bvh_intersect(s, eqr.shadow, dummy, true)) {
+            BRec bq;
+            bq.wi = its.sh.to_local(-ray.d);
+            bq.wo = its.sh.to_local(eqr.wi);
+            bq.measure = ESolidAngle;
+            V3 f = bsdf_eval(bsdf, bq);
+            float cs = its.sh.to_local(eqr.wi).z;
+            float pdf_ems = emitter_pdf(s, l_ems, eqr) / n_lights;
+            float pdf_mat = bsdf_pdf(bsdf, bq);
+            result_ems = cmul(li * cs, f) * n_lights;
+            if (pdf_ems + pdf_mat > kEps) w_ems = pdf_ems / (pdf_ems + pdf_mat);
+        } else if (s.envmap >= 0) {
+            result_ems = cmul(li, env_eval(s, eqr.shadow.d));
+        }
+    }
+    BRec bm;
+    bm.wi = its.sh.to_local(-ray.d);
+    bm.measure = ESolidAngle;
+    float bx, by;
+    smp.next2d(bx, by);
+    V3 col = bsdf_sample(bsdf, bm, bx, by);
+    if (!is_zero(col)) {
+        Ray sr = make_ray(its.p, its.sh.to_world(bm.wo));
+        Its its2;
+        if (bvh_intersect(s, sr, its2, false) && s.shapes[its2.shape].emitter >= 0) {
+            const nh_emitter &e2 = s.emitters[s.shapes[its2.shape].emitter];
+            ERec q2 = erec(its.p, its2.p, its2.sh.n);
+            result_mats = cmul(col, emitter_eval(s, e2, q2));
+            float pdf_mat = bsdf_pdf(bsdf, bm);
+            float pdf_e = emitter_pdf(s, e2, q2) / n_lights;
+            if (pdf_mat + pdf_e > kEps) w_mat = pdf_mat / (pdf_mat + pdf_e);
+        } else if (s.envmap >= 0) {
+            result_mats = cmul(col, env_eval(s, sr.d));
+        }
+    }
+    return result + w_ems * result_ems + w_mat * result_mats;
+}
+
 // PerspectiveCamera::sampleRay (perspective.cpp:97-141), no depth of field
 Ray camera_ray(const nh_camera &c, float px, float py) {
     const float *m = c.sample_to_camera;
@@ -884,7 +1001,13 @@ Ray camera_ray(const nh_camera &c, float px, float py) {
 }
 
 V3 li(const no_scene &s, Sampler &smp, const Ray &r) {
-    return s.integrator == NH_INTEGRATOR_PATH_MATS ? li_path_mats(s, smp, r) : li_path_mis(s, smp, r);
+    switch (s.integrator) {
+        case NH_INTEGRATOR_PATH_MATS: return li_path_mats(s, smp, r);
+        case NH_INTEGRATOR_DIRECT_EMS: return li_direct_ems(s, smp, r);
+        case NH_INTEGRATOR_DIRECT_MATS: return li_direct_mats(s, smp, r);
+        case NH_INTEGRATOR_DIRECT_MIS: return li_direct_mis(s, smp, r);
+        default: return li_path_mis(s, smp, r);
+    }
 }
 
 // ---- ImageBlock (src/utils/block.cpp) ------------------------------------

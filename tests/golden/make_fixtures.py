@@ -38,6 +38,16 @@ SCENE_FILES = [
     "scenes/pa4/tests/polylum5.obj",
     "scenes/pa3/tests/ttest-microfacet.xml",
     "scenes/pa3/tests/chi2test-microfacet.xml",
+    # direct_ems / direct_mats / direct_mis known-answer scenes (t-tests)
+    "scenes/pa3/tests/test-mesh.xml",
+    "scenes/pa3/tests/test-mesh-furnace.xml",
+    "scenes/pa3/tests/furnace.obj",
+    "scenes/pa3/tests/floor.obj",
+    "scenes/pa3/tests/polylum1.obj",
+    "scenes/pa3/tests/polylum2.obj",
+    "scenes/pa3/tests/polylum3.obj",
+    "scenes/pa3/tests/polylum4.obj",
+    "scenes/pa3/tests/polylum5.obj",
 ]
 
 

@@ -140,6 +140,39 @@ def test_render_parity_path_mats(gpu, tmp_path, mode):
     assert rel_l2(g, r) < TOL_REL_L2
 
 
+DIRECT = [pytest.param(nh.INTEGRATOR_DIRECT_EMS, id="direct_ems"), pytest.param(nh.INTEGRATOR_DIRECT_MATS, id="direct_mats"),
+          pytest.param(nh.INTEGRATOR_DIRECT_MIS, id="direct_mis")]
+
+
+@pytest.mark.parametrize("integrator", DIRECT)
+@pytest.mark.parametrize("scene", ["c1", "envmap"])
+def test_render_parity_direct(gpu, tmp_path, scene, integrator):
+    """direct_ems / direct_mats / direct_mis (single bounce, run as the megakernel also when the
+    wavefront mode is asked for) against the oracle: Cornell box with mirror + dielectric, and the
+    PNG environment map scene (env terms of misses, occluded light samples and BSDF rays)."""
+    xml = scenegen.cbox_xml(str(tmp_path), "c1") if scene == "c1" else \
+        scenegen.envmap_xml(str(tmp_path), texture="png", tex_size=(96, 48))
+    for mode in (nh.MODE_WAVEFRONT, nh.MODE_MEGAKERNEL):
+        g, r, s = render_pair(xml, 48, 40, 16, integrator=integrator, mode=mode, traversal=nh.TRAVERSAL_ORDERED)
+        print(f"{scene} integrator={integrator} mode={mode}: rel-L2 {rel_l2(g, r):.3e}, max|d| {np.abs(g - r).max():.3e}")
+        np.testing.assert_array_equal(g, r)
+        assert nh.to_rgb(r, s.border).mean() > 0.01
+
+
+def test_direct_ttest_scenes_match_oracle(gpu, scene_dir):
+    """The reference's direct-integrator known-answer scenes (scenes/pa3/tests/test-mesh*.xml, 1x1
+    pixel cameras): GPU render equals the oracle's bit for bit at 64 spp."""
+    for name in ("test-mesh.xml", "test-mesh-furnace.xml"):
+        path = os.path.join(scene_dir, "scenes/pa3/tests", name)
+        for i in range(len(scenegen.test_references(path))):
+            s = nh.Scene(path, i)
+            b = nh.Bvh(s)
+            ctx = nh.Context(0)
+            ctx.upload(s, b)
+            ctx.render(0, 64, seed=3, clear=True, mode=nh.MODE_MEGAKERNEL)
+            np.testing.assert_array_equal(ctx.framebuffer(), no.OracleScene(s).render(0, 64, seed=3))
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_render_parity_microfacet_mesh(gpu, tmp_path, mode):
     xml, _ = scenegen.bumpy_cbox_xml(str(tmp_path), 120, 60)

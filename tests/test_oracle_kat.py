@@ -86,9 +86,11 @@ def students_t_test(mean, variance, reference, n, alpha, num_tests):
     return not (pval < sidak or not math.isfinite(pval)), pval
 
 
-@pytest.mark.parametrize("name", ["test-furnace.xml", "test-direct.xml"])
+@pytest.mark.parametrize("name", ["pa4/tests/test-furnace.xml", "pa4/tests/test-direct.xml",
+                                  "pa3/tests/test-mesh.xml", "pa3/tests/test-mesh-furnace.xml"])
 def test_scene_ttests(scene_dir, name):
-    path = os.path.join(scene_dir, "scenes/pa4/tests", name)
+    """pa4: path_mats / path_mis; pa3: direct_ems / direct_mats / direct_mis (5 + 2 scenes each)."""
+    path = os.path.join(scene_dir, "scenes", name)
     refs = scenegen.test_references(path)
     rng = no.Pcg32()  # Independent sampler created once, never prepare()d (ttest.cpp:193-194)
     results = []
