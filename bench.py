@@ -300,7 +300,8 @@ def main():
             "config": {"workload": f"{scene_desc}, {R * args.steps} spp, path_mis", "config": args.config,
                        "width": W, "height": H, "spp": R * args.steps, "rounds_per_step": R,
                        "mode": args.mode, "traversal": args.traversal, "pools": args.pools,
-                       "parallelism": f"tile-shard x{world} + RCCL reduce" if world > 1 else "single GPU",
+                       "parallelism": (f"tile-shard x{world} + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce"
+                                       if world > 1 else "single GPU"),
                        "bvh_build_s": round(bvh_s, 3), "upload_s": round(upload_s, 3)},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -930,12 +930,8 @@ static int pool_finish(nh_ctx *c, WfPool &p) {
     c->stats.kernel_ms_splat += ts;
     c->stats.launches_splat++;
     c->stats.samples += (uint64_t)p.L.n_paths;
-    // bytes by construction (nh_wavefront.hip). Bounce 0 evaluates the camera sample in place: shade
-    // loads the hit (16 B) and writes the sample record (20 B) per path. Later bounces load 96 B per
-    // path (ray, hit, Li, throughput, rng, flags, pid) + 16 (pending BSDF sample) + 17 per queued
-    // shadow ray (pending NEE + occlusion). Every bounce stores 116 B per survivor, 36 per new
-    // shadow ray and 12 per finished path; extend moves 48 B per ray (16 at bounce 0: no ray load).
-    // (Bounces shaded by wf_shade only; the tail kernel's work is not part of this account.)
+    // bytes by construction (nh_wavefront.hip), per bounce shaded by wf_shade (the tail kernel's work
+    // is not part of this account); extend moves 48 B per ray (16 at bounce 0: no ray load).
     for (size_t b = 0; b + 1 < p.in_e.size(); ++b) {
         const uint64_t shaded = p.in_e[b], nsh = p.in_s[b], ne = p.in_e[b + 1], ns = p.in_s[b + 1];
         // bounce 0: hit in, sample record out. Later: path state (ray_o, ray_d, li, thr 16 B each,

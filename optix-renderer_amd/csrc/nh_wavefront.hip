@@ -8,9 +8,10 @@
 //                MIS probe and the next bounce at once, path_mis.cpp:117/:146) -- the
 //                BVH-traversal kernel whose roofline bench.py reports
 //   wf_shadow    any-hit traversal of the shadow rays queued by the previous shade (:89)
-//   wf_shade     finishes the previous bounce (shadow result -> w_ems, probe hit -> w_mats,
-//                discrete override, Li accumulation, :103-146), then shades the new hit
-//                (emitter term, Russian roulette, NEE sample, BSDF sample)
+//   wf_shade     finishes the previous bounce (an unoccluded shadow ray adds the light term that
+//                bounce computed and sets w_ems; probe hit -> w_mats; discrete override,
+//                :103-146), then shades the new hit (emitter term, Russian roulette, NEE sample,
+//                BSDF sample, this bounce's MIS-weighted light term and t *= bsdf weight)
 //
 // Path state is double-buffered and kept DENSE: wf_shade reads live path i of buffer A and
 // writes each surviving path's whole state to the next free slot of buffer B (ranks from wave
