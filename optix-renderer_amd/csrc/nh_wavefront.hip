@@ -239,7 +239,10 @@ __global__ __launch_bounds__(128) void wf_shadow(const DScene *__restrict__ Sp, 
 #endif
 constexpr int kFetchBatch = NH_FETCH_BATCH;
 constexpr int kTraceBlocksMax = 1 << 20;
-constexpr int kRingEntries = 16;
+#ifndef NH_RING_ENTRIES
+#define NH_RING_ENTRIES 16
+#endif
+constexpr int kRingEntries = NH_RING_ENTRIES;
 //
 // WIDE: the 4-wide collapse of the tree (Tracer4), LDS window of 8 (ref, distance) pairs per lane.
 template <bool WIDE>
