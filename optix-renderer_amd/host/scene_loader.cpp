@@ -25,6 +25,7 @@
 #include <fstream>
 #include <functional>
 #include <map>
+#include <memory>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -250,7 +251,20 @@ struct Obj {
 }  // namespace
 
 // Owning scene (the C handle).
+struct ObjKey {
+    uint32_t p, uv, n;
+    bool operator==(const ObjKey &o) const { return p == o.p && uv == o.uv && n == o.n; }
+};
+struct ObjText {
+    std::vector<V3> positions, normals;
+    std::vector<std::pair<float, float>> texcoords;
+    std::vector<uint32_t> indices;
+    std::vector<ObjKey> vertices;
+};
+
 struct SceneData {
+    // OBJ files parsed while loading (released once the scene is assembled)
+    std::map<std::string, std::shared_ptr<ObjText>> obj_cache;
     nh_camera camera{};
     nh_filter filter{};
     int32_t integrator = NH_INTEGRATOR_PATH_MIS;
@@ -414,34 +428,26 @@ std::string join_path(const std::string &base_dir, const std::string &rel) {
     return base_dir + "/" + rel;
 }
 
-// WavefrontOBJ::loadFromFile
-void load_obj(const std::string &path, const M4 &trafo, SceneData &sd, nh_shape &sh) {
+// Parsed OBJ text of WavefrontOBJ::loadFromFile before toWorld is applied: positions / normals as
+// read, texcoords, the dedup'd (p, uv, n) vertex keys and the triangle indices (quads split into
+// verts[0..2], verts[0], verts[2], verts[3] order as obj.cpp:130-160 does).
+ObjText parse_obj(const std::string &path) {
     std::ifstream is(path);
     if (is.fail()) throw SceneError("unable to open OBJ file \"" + path + "\"");
-    M4 inv = inverse(trafo);
-    struct Key {
-        uint32_t p, uv, n;
-        bool operator==(const Key &o) const { return p == o.p && uv == o.uv && n == o.n; }
-    };
     struct KeyHash {
-        size_t operator()(const Key &k) const {
+        size_t operator()(const ObjKey &k) const {
             size_t h = std::hash<uint32_t>()(k.p);
             h = h * 37 + std::hash<uint32_t>()(k.uv);
             h = h * 37 + std::hash<uint32_t>()(k.n);
             return h;
         }
     };
-    std::vector<V3> positions, normals;
-    std::vector<std::pair<float, float>> texcoords;
-    std::vector<uint32_t> indices;
-    std::vector<Key> vertices;
-    std::unordered_map<Key, uint32_t, KeyHash> vmap;
-    V3 bmin = v3(INFINITY, INFINITY, INFINITY), bmax = v3(-INFINITY, -INFINITY, -INFINITY);
-
+    ObjText o;
+    std::unordered_map<ObjKey, uint32_t, KeyHash> vmap;
     auto parse_vertex = [&](const std::string &s) {
         auto tk = tokenize(s, "/", true);
         if (tk.size() < 1 || tk.size() > 3) throw SceneError("invalid vertex data \"" + s + "\"");
-        Key k{(uint32_t)-1, (uint32_t)-1, (uint32_t)-1};
+        ObjKey k{(uint32_t)-1, (uint32_t)-1, (uint32_t)-1};
         k.p = (uint32_t)std::stoul(tk[0]);
         if (tk.size() >= 2 && !tk[1].empty()) k.uv = (uint32_t)std::stoul(tk[1]);
         if (tk.size() >= 3 && !tk[2].empty()) k.n = (uint32_t)std::stoul(tk[2]);
@@ -455,22 +461,19 @@ void load_obj(const std::string &path, const M4 &trafo, SceneData &sd, nh_shape 
         if (prefix == "v") {
             V3 p;
             line >> p.x >> p.y >> p.z;
-            p = xform_point(trafo, p);
-            bmin = v3(std::min(bmin.x, p.x), std::min(bmin.y, p.y), std::min(bmin.z, p.z));
-            bmax = v3(std::max(bmax.x, p.x), std::max(bmax.y, p.y), std::max(bmax.z, p.z));
-            positions.push_back(p);
+            o.positions.push_back(p);
         } else if (prefix == "vt") {
             float u = 0, v = 0;
             line >> u >> v;
-            texcoords.emplace_back(u, v);
+            o.texcoords.emplace_back(u, v);
         } else if (prefix == "vn") {
             V3 n;
             line >> n.x >> n.y >> n.z;
-            normals.push_back(normalized(xform_normal(inv, n)));
+            o.normals.push_back(n);
         } else if (prefix == "f") {
             std::string s1, s2, s3, s4;
             line >> s1 >> s2 >> s3 >> s4;
-            Key verts[6];
+            ObjKey verts[6];
             int nv = 3;
             verts[0] = parse_vertex(s1);
             verts[1] = parse_vertex(s2);
@@ -484,15 +487,38 @@ void load_obj(const std::string &path, const M4 &trafo, SceneData &sd, nh_shape 
             for (int i = 0; i < nv; ++i) {
                 auto it = vmap.find(verts[i]);
                 if (it == vmap.end()) {
-                    vmap[verts[i]] = (uint32_t)vertices.size();
-                    indices.push_back((uint32_t)vertices.size());
-                    vertices.push_back(verts[i]);
+                    vmap[verts[i]] = (uint32_t)o.vertices.size();
+                    o.indices.push_back((uint32_t)o.vertices.size());
+                    o.vertices.push_back(verts[i]);
                 } else {
-                    indices.push_back(it->second);
+                    o.indices.push_back(it->second);
                 }
             }
         }
     }
+    return o;
+}
+
+// WavefrontOBJ::loadFromFile. A scene that instantiates one OBJ file several times (Nori has no
+// instancing: C5 bakes ten transforms of one mesh) parses the text once; toWorld is applied to
+// the parsed values per shape, as the reference applies it while reading, so the floats are equal.
+void load_obj(const std::string &path, const M4 &trafo, SceneData &sd, nh_shape &sh) {
+    auto it_cache = sd.obj_cache.find(path);
+    if (it_cache == sd.obj_cache.end()) it_cache = sd.obj_cache.emplace(path, std::make_shared<ObjText>(parse_obj(path))).first;
+    const ObjText &obj = *it_cache->second;
+    const M4 inv = inverse(trafo);
+    std::vector<V3> positions(obj.positions.size()), normals(obj.normals.size());
+    V3 bmin = v3(INFINITY, INFINITY, INFINITY), bmax = v3(-INFINITY, -INFINITY, -INFINITY);
+    for (size_t i = 0; i < positions.size(); ++i) {
+        const V3 p = xform_point(trafo, obj.positions[i]);
+        bmin = v3(std::min(bmin.x, p.x), std::min(bmin.y, p.y), std::min(bmin.z, p.z));
+        bmax = v3(std::max(bmax.x, p.x), std::max(bmax.y, p.y), std::max(bmax.z, p.z));
+        positions[i] = p;
+    }
+    for (size_t i = 0; i < normals.size(); ++i) normals[i] = normalized(xform_normal(inv, obj.normals[i]));
+    const auto &texcoords = obj.texcoords;
+    const auto &indices = obj.indices;
+    const auto &vertices = obj.vertices;
     const uint32_t nvert = (uint32_t)vertices.size(), nface = (uint32_t)(indices.size() / 3);
     sh.type = NH_SHAPE_MESH;
     sh.v_offset = (uint32_t)(sd.V.size() / 3);
@@ -967,6 +993,7 @@ SceneData *load_scene(const std::string &path, int scene_index) {
     if (slash != std::string::npos) base_dir = path.substr(0, slash);
     auto sd = std::make_unique<SceneData>();
     build_scene(*scene, base_dir, *sd);
+    sd->obj_cache.clear();
     return sd.release();
 }
 

@@ -1188,6 +1188,33 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
         std::vector<uint32_t> temp(size);
         uint32_t *base = s->indices.data();
 
+        // Test-speed only: the centroid and box of every primitive are computed once (the same
+        // float values the reference recomputes inside each comparison, so every sort sees the same
+        // comparison results and produces the same order), and large disjoint subtrees are built
+        // on their own threads (they own disjoint node slots, index ranges and scratch).
+        std::vector<float> cen[3];
+        std::vector<Box> pbox(size);
+        for (int a = 0; a < 3; ++a) cen[a].resize(size);
+        for (uint32_t g = 0; g < size; ++g) {
+            for (int a = 0; a < 3; ++a) cen[a][g] = centroid(g, a);
+            pbox[g] = prim_box(g);
+        }
+        constexpr uint32_t kParallelPrims = 65536;
+        const int max_threads = (int)std::max(1u, std::thread::hardware_concurrency());
+        std::atomic<int> live_threads{1};
+        // run a(); b(); -- a on another thread when the range is large and a thread is free
+        auto fork2 = [&](uint32_t sz, const std::function<void()> &a, const std::function<void()> &b) {
+            if (sz >= kParallelPrims && live_threads.fetch_add(1) < max_threads) {
+                std::thread t(a);
+                b();
+                t.join();
+                live_threads.fetch_sub(1);
+            } else {
+                if (sz >= kParallelPrims) live_threads.fetch_sub(1);
+                a();
+                b();
+            }
+        };
         std::function<void(uint32_t, uint32_t *, uint32_t *, uint32_t *)> serial;
         serial = [&](uint32_t node_idx, uint32_t *start, uint32_t *end, uint32_t *tmp) {
             Node &node = nodes[node_idx];
@@ -1196,14 +1223,15 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
             int64_t best_index = -1, best_axis = -1;
             float *left_areas = (float *)tmp;
             for (int axis = 0; axis < 3; ++axis) {
-                std::sort(start, end, [&](uint32_t f1, uint32_t f2) { return centroid(f1, axis) < centroid(f2, axis); });
+                const float *c = cen[axis].data();
+                std::sort(start, end, [c](uint32_t f1, uint32_t f2) { return c[f1] < c[f2]; });
                 Box bbox; bbox.reset();
-                for (uint32_t i = 0; i < sz; ++i) { bbox.expand(prim_box(start[i])); left_areas[i] = (float)bbox.area(); }
+                for (uint32_t i = 0; i < sz; ++i) { bbox.expand(pbox[start[i]]); left_areas[i] = (float)bbox.area(); }
                 if (axis == 0) node.box = bbox;
                 bbox.reset();
                 float tri_factor = 1 / node.box.area();
                 for (uint32_t i = sz - 1; i >= 1; --i) {
-                    bbox.expand(prim_box(start[i]));
+                    bbox.expand(pbox[start[i]]);
                     float la = left_areas[i - 1], ra = bbox.area();
                     uint32_t pl = i, pr = sz - i;
                     float cost = 2.0f * 1 + tri_factor * (pl * la + pr * ra);
@@ -1211,12 +1239,13 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
                 }
             }
             if (best_index == -1) { node.w0 = 1u | (sz << 1); node.w1 = (uint32_t)(start - base); return; }
-            std::sort(start, end, [&](uint32_t f1, uint32_t f2) { return centroid(f1, (int)best_axis) < centroid(f2, (int)best_axis); });
+            const float *c = cen[best_axis].data();
+            std::sort(start, end, [c](uint32_t f1, uint32_t f2) { return c[f1] < c[f2]; });
             uint32_t lc = (uint32_t)best_index, li = node_idx + 1, ri = node_idx + 2 * lc;
             node.w0 = 0u | ((uint32_t)best_axis << 1);
             node.w1 = ri;
-            serial(li, start, start + lc, tmp);
-            serial(ri, start + lc, end, tmp + lc);
+            fork2(sz, [&, li, start, lc, tmp] { serial(li, start, start + lc, tmp); },
+                  [&, ri, start, lc, end, tmp] { serial(ri, start + lc, end, tmp + lc); });
         };
         auto to_int = [](float x) -> int { if (!(x > -2147483904.0f && x < 2147483648.0f)) return INT32_MIN; return (int)x; };
         std::function<void(uint32_t, uint32_t *, uint32_t *, uint32_t *)> task;
@@ -1232,9 +1261,9 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
             for (auto &b : bb) b.reset();
             for (uint32_t i = 0; i < sz; ++i) {
                 uint32_t f = start[i];
-                int index = std::min(std::max(to_int((centroid(f, axis) - mn) * inv), 0), 15);
+                int index = std::min(std::max(to_int((cen[axis][f] - mn) * inv), 0), 15);
                 counts[index]++;
-                bb[index].expand(prim_box(f));
+                bb[index].expand(pbox[f]);
             }
             Box bl[16];
             bl[0] = bb[0];
@@ -1258,12 +1287,12 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
             uint32_t il = 0, ir = lc;
             for (uint32_t i = 0; i < sz; ++i) {
                 uint32_t f = start[i];
-                int index = to_int((centroid(f, axis) - mn) * inv);
+                int index = to_int((cen[axis][f] - mn) * inv);
                 if (index <= best_index) tmp[il++] = f; else tmp[ir++] = f;
             }
             std::memcpy(start, tmp, sz * sizeof(uint32_t));
-            task(li, start, start + lc, tmp);
-            task(ri, start + lc, end, tmp + lc);
+            fork2(sz, [&, li, start, lc, tmp] { task(li, start, start + lc, tmp); },
+                  [&, ri, start, lc, end, tmp] { task(ri, start + lc, end, tmp + lc); });
         };
         task(0u, base, base + size, temp.data());
         // statistics + compaction (bvh.cpp:354-379)
