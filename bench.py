@@ -1,30 +1,33 @@
 """Benchmark of the MI355X path_mis hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--mode wavefront]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--mode wavefront] [--scaling weak|strong]
 
 Workload (N=1, BASELINE.json configs[1]): Cornell box diffuse-only (C2: both spheres
 diffuse), 1024x1024, 256 spp, path_mis, per-path pcg32 seeding. One step = `--rounds`
 (default 16) sample rounds over the whole image = one nh_render call: the wavefront pipeline
-(generate, then extend / any-hit / shade per bounce until no path is alive) or, with
---mode megakernel, one path-kernel launch; then one ImageBlock splat. The default K=16 steps
-render the full 256 spp. Multi-GPU: one process per GPU (torchrun), 32x32 image blocks dealt
-round-robin to ranks (tile shard); a step is `--rounds` x N sample rounds over each rank's 1/N
-of the blocks, so every GPU traces the same 16.7M samples per step at any N (weak scaling: at N
-GPUs the K steps render N x K x rounds spp of the same image); one RCCL reduce (sum) of the RGBW
-framebuffer to rank 0 inside the timed region.
+(per bounce: closest-hit traversal, any-hit traversal, shade; a tail kernel finishes the last
+paths) or, with --mode megakernel, one path-kernel launch; then the ImageBlock splat. The
+default K=16 steps render the full 256 spp.
+
+Multi-GPU: one process per GPU (torchrun), 32x32 image blocks dealt round-robin to ranks (tile
+shard), one RCCL reduce (sum) of the RGBW framebuffer to rank 0 inside the timed region, max
+time over ranks. --scaling weak (default): a step is N x --rounds sample rounds over each rank's
+1/N of the blocks, so every GPU traces the same 16.7M samples per step at any N. --scaling
+strong: a fixed image (C4, 2048^2, --rounds x --steps spp) split over the ranks by blocks.
+`value` = all ranks' samples / the max-over-ranks time.
 
 The JSON line also carries:
-  roofline      the dominant kernel (largest summed HIP-event time on the context's stream):
-                  wf_shade    path-state bytes loaded + stored (counted by construction from
-                              the queue counts)
-                  wf_extend   BVH nodes x 64 B + primitive tests x 48 B (in-kernel counters in
-                              a calibration launch on the same seeds) + 48 B ray/hit per query
-                  nh_path_kernel (megakernel) nodes x 64 + prims x 48 + 20 B record per path
-                ... / average launch duration, against 8 TB/s HBM; traffic = HBM bytes per
-                launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json)
-                when one exists for this workload, else null
+  roofline      the dominant kernel (largest summed HIP-event time) against the 8 TB/s HBM peak:
+                algorithmic HBM bytes per launch / average launch duration (see roofline()); every
+                stage's figures under `stages` (HBM GB/s, and for an LDS-staged BVH the algorithmic
+                traversal work rate separately, never compared with the HBM peak); `traffic` = HBM
+                bytes per launch from the committed rocprofv3 PMC summary of the same command
+                (profiles/pmc_traffic.json, named in `traffic_source`), else null
+  traversal     the metric's "traversal HBM GB/s": the closest-hit kernel of the timed run
+  traversal_1m  (N=1) the north star's roofline target: the persistent traversal kernel on the
+                ~1M-triangle scene (perf-1M), timed in the same run
   cpu_baseline  the CPU oracle (oracle/, a restatement of the reference's path_mis) timed on
-                this host on a bounded sample of the same workload (rank 0, N=1 only)
+                this host's cores on a bounded sample of the same workload (rank 0, N=1 only)
 """
 import argparse
 import json
@@ -49,7 +52,12 @@ def parse():
     p.add_argument("--steps", type=int, default=16)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--rounds", type=int, default=16, help="sample rounds per step")
-    p.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "bumpy1m"])
+    p.add_argument("--config", default=None, choices=["c1", "c2", "c3", "c4", "c5", "bumpy1m"])
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                   help="weak: N x --rounds rounds per step over each rank's 1/N of the blocks (default); strong: "
+                        "a fixed image (C4 2048^2 unless --config) and --rounds x --steps spp split by blocks")
+    p.add_argument("--traversal-1m-steps", type=int, default=4,
+                   help="N=1: also time the perf-1M traversal kernel (0 = skip)")
     p.add_argument("--width", type=int, default=None)
     p.add_argument("--height", type=int, default=None)
     p.add_argument("--traversal", default="ordered", choices=["ordered", "reference"])
@@ -65,7 +73,15 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (production); gloo = host-side reduce, for rehearsing the "
                         "multi-process flow with several ranks on one GPU")
-    return p.parse_args()
+    a = p.parse_args()
+    a.config_given = a.config is not None
+    a.config = a.config or "c2"
+    return a
+
+
+def scene_dims(args):
+    w = args.width or {"c4": 2048, "c5": 4096}.get(args.config, 1024)
+    return w, args.height or w
 
 
 def build_scene(args, tmp):
@@ -91,83 +107,137 @@ def build_scene(args, tmp):
 
 
 def pmc_traffic(workload_key):
-    """HBM bytes per path-kernel launch from a committed rocprofv3 PMC summary, if any."""
+    """HBM bytes per launch of the roofline kernel from a committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json: FETCH_SIZE x2 + WRITE_SIZE from separate --pmc passes of the same
+    bench command), or (None, None) when none exists for this workload. It is read from the file,
+    not measured in this run: the PMC passes need rocprofv3 around the process."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
-        data = json.load(open(path))
-        return data.get(workload_key, {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+        rec = json.load(open(path)).get(workload_key)
+    except (OSError, ValueError):
+        return None, None
+    if not rec:
+        return None, None
+    return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_traffic.json[{workload_key}]: {rec.get('source', '')}"
+
+
+def stage_work(calib):
+    """Traversal work per stage from the calibration launch's in-kernel counters: the tail kernel
+    counts into its own slots, so extend / shadow are those kernels' own visits."""
+    tq, tn, tp = calib["tail_queries"], calib["tail_nodes_visited"], calib["tail_prims_tested"]
+    tsq, tsn, tsp = calib["tail_shadow_queries"], calib["tail_shadow_nodes_visited"], calib["tail_shadow_prims_tested"]
+    sq, sn, sp = calib["shadow_queries"] - tsq, calib["shadow_nodes_visited"] - tsn, calib["shadow_prims_tested"] - tsp
+    eq = calib["ray_queries"] - calib["shadow_queries"] - (tq - tsq)
+    en = calib["nodes_visited"] - calib["shadow_nodes_visited"] - (tn - tsn)
+    ep = calib["prims_tested"] - calib["shadow_prims_tested"] - (tp - tsp)
+    return {"extend": (eq, en, ep), "shadow": (sq, sn, sp), "tail": (tq, tn, tp)}
 
 
 def roofline(args, calib, st, W, H, R):
-    """Roofline of the dominant kernel. Algorithmic bytes come from the calibration launch's
-    in-kernel counters (same seeds as the first timed step), scaled per sample; the time is the
-    kernel's summed HIP-event duration over the timed region on the context's stream.
-      megakernel: nh_path_kernel -- BVH nodes x 64 B + primitive tests x 48 B (closest, probe and
-                  shadow queries) + 20 B sample record per path
-      wavefront:  the dominant stage -- wf_shade: path-state bytes; wf_extend: the closest-hit
-                  share of nodes/prims + 48 B per query (ray 32 B in, hit 16 B out)"""
+    """Roofline of the dominant kernel (largest summed HIP-event time over the timed kernels).
+
+    Algorithmic bytes per launch = the calibration launch's per-sample bytes x samples per launch,
+    divided by the kernel's average launch duration (HIP events on the stream it runs on):
+      wf_shade     path-state bytes loaded + stored (counted by construction from the queue counts)
+      wf_extend /  BVH nodes x node bytes + primitive tests x 48 B (in-kernel counters) + queue bytes
+      wf_shadow    (ray in, hit / occlusion out). Node and primitive reads are HBM traffic only when the
+                   BVH is read from global memory; a BVH staged in LDS (the Cornell box, < 1 KB) makes
+                   them LDS reads, so `hbm_gbs` counts the queue bytes alone and `work_gbs` the
+                   algorithmic traversal rate (not an HBM figure)
+      wf_tail      traversal + shade work of the last few paths, in place
+      megakernel   nodes x 64 + prims x 48 + 20 B record per path
+    `peak` is the HBM roofline; only `hbm_gbs` figures are compared with it."""
     paths = calib["samples"]
-    NODE_BYTES = calib.get("node_bytes") or 64  # 128 when the 4-wide tree was traversed
+    node_b = calib.get("node_bytes") or 64
+    lds = bool(calib.get("lds_scene"))
+    per_launch = lambda b, launches: b / paths * st["samples"] / max(launches, 1)  # noqa: E731
+    stages = {}
     if args.mode == "wavefront":
-        # dominant stage by measured time
-        stage = max(("extend", "shadow", "shade"), key=lambda k: st[f"kernel_ms_{k}"])
-        q = calib["ray_queries"] - calib["shadow_queries"]
-        nodes = calib["nodes_visited"] - calib["shadow_nodes_visited"]
-        prims = calib["prims_tested"] - calib["shadow_prims_tested"]
-        if stage == "shade":
-            bytes_calib = calib["shade_state_bytes"]
-        elif stage == "extend":
-            bytes_calib = nodes * NODE_BYTES + prims * PRIM_BYTES + calib["extend_queue_bytes"]
-        else:
-            bytes_calib = (calib["shadow_nodes_visited"] * NODE_BYTES + calib["shadow_prims_tested"] * PRIM_BYTES
-                           + calib["shadow_queue_bytes"])
-        launches, ms, kernel = max(st[f"launches_{stage}"], 1), st[f"kernel_ms_{stage}"], f"wf_{stage}"
+        w = stage_work(calib)
+        for k in ("extend", "shadow", "tail"):
+            q, n, p = w[k]
+            trav = n * node_b + p * PRIM_BYTES
+            queue = {"extend": calib["extend_queue_bytes"], "shadow": calib["shadow_queue_bytes"], "tail": 0}[k]
+            stages[k] = {"work_bytes": trav + queue, "hbm_bytes": queue + (0 if lds else trav),
+                         "queries": q, "nodes": n, "prims": p}
+        stages["shade"] = {"work_bytes": calib["shade_state_bytes"], "hbm_bytes": calib["shade_state_bytes"]}
     else:
-        q, nodes, prims = calib["ray_queries"], calib["nodes_visited"], calib["prims_tested"]
-        bytes_calib = nodes * NODE_BYTES + prims * PRIM_BYTES + paths * RECORD_BYTES
-        launches, ms, kernel = max(st["launches_path"], 1), st["kernel_ms_path"], "nh_path_kernel"
-    bytes_per_sample = bytes_calib / paths
-    avg_ms = ms / launches
-    bytes_per_launch = bytes_per_sample * st["samples"] / launches
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        q, n, p = calib["ray_queries"], calib["nodes_visited"], calib["prims_tested"]
+        b = n * 64 + p * PRIM_BYTES + paths * RECORD_BYTES
+        stages["path"] = {"work_bytes": b, "hbm_bytes": b, "queries": q, "nodes": n, "prims": p}
+    report = {}
+    for k, v in stages.items():
+        ms, launches = st[f"kernel_ms_{k}"], st[f"launches_{k}"]
+        if ms <= 0 or launches == 0:
+            continue
+        avg = ms / launches
+        r = {"ms": round(ms, 3), "launches": launches, "avg_launch_ms": round(avg, 4),
+             "hbm_bytes_per_launch": int(per_launch(v["hbm_bytes"], launches)),
+             "hbm_gbs": round(per_launch(v["hbm_bytes"], launches) / (avg * 1e-3) / 1e9, 1)}
+        if v["work_bytes"] != v["hbm_bytes"]:
+            r["work_gbs"] = round(per_launch(v["work_bytes"], launches) / (avg * 1e-3) / 1e9, 1)
+            r["work_note"] = "algorithmic node/primitive bytes read from the LDS copy of the BVH: not HBM traffic"
+        if "queries" in v and v["queries"]:
+            r["nodes_per_query"] = round(v["nodes"] / v["queries"], 3)
+            r["prims_per_query"] = round(v["prims"] / v["queries"], 3)
+        if r["hbm_gbs"] > HBM_PEAK_GBS * 1.02:  # an HBM figure above peak is an accounting bug: say so
+            r["accounting_error"] = "HBM GB/s above the HBM peak"
+        report[k] = r
+    dom = max(report, key=lambda k: report[k]["ms"])
+    kernel = {"shade": "wf_shade", "extend": "wf_extend", "shadow": "wf_shadow", "tail": "wf_tail",
+              "path": "nh_path_kernel"}[dom]
+    d = report[dom]
     key = f"{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}"
-    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            # PMC summaries are recorded for single-GPU runs (per-rank launches are smaller at N > 1)
-            "traffic": pmc_traffic(key) if int(os.environ.get("WORLD_SIZE", "1")) == 1 else None,
-            "kernel": kernel, "avg_launch_ms": round(avg_ms, 4), "launches": launches,
-            "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "bytes_per_sample": round(bytes_per_sample, 1),
-            "node_bytes": NODE_BYTES,
-            "queries_per_sample": round(q / paths, 3),
-            "nodes_per_query": round(nodes / max(q, 1), 3),
-            "prims_per_query": round(prims / max(q, 1), 3),
-            "splat_ms_per_launch": round(st["kernel_ms_splat"] / max(st["launches_splat"], 1), 4)}
-    if args.mode == "wavefront":
-        roof["stage_ms"] = {k: round(st[f"kernel_ms_{k}"], 3) for k in ("extend", "shadow", "shade", "tail", "splat")}
-        # every traversal/shade stage against HBM, algorithmic bytes as above (per-sample from calibration)
-        per = {"shade": calib["shade_state_bytes"],
-               "extend": nodes * NODE_BYTES + prims * PRIM_BYTES + calib["extend_queue_bytes"],
-               "extend_queue_only": calib["extend_queue_bytes"],
-               "shadow": (calib["shadow_nodes_visited"] * NODE_BYTES + calib["shadow_prims_tested"] * PRIM_BYTES
-                          + calib["shadow_queue_bytes"])}
-        roof["stage_gbs"] = {}
-        for k, b in per.items():
-            t = st["kernel_ms_" + k.split("_")[0]]
-            if t > 0:
-                roof["stage_gbs"][k] = round(b / paths * st["samples"] / (t * 1e-3) / 1e9, 1)
+    single = int(os.environ.get("WORLD_SIZE", "1")) == 1
+    traffic, source = pmc_traffic(key) if single else (None, None)
+    achieved = d["hbm_gbs"]
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": source or "not collected for this workload (rocprofv3 PMC runs separately)",
+            "kernel": kernel, "avg_launch_ms": d["avg_launch_ms"], "launches": d["launches"],
+            "algorithmic_bytes_per_launch": d["hbm_bytes_per_launch"],
+            "bytes_per_sample": round(stages[dom]["hbm_bytes"] / paths, 1), "node_bytes": node_b,
+            "lds_scene": lds, "queries_per_sample": round(calib["ray_queries"] / paths, 3),
+            "splat_ms_per_launch": round(st["kernel_ms_splat"] / max(st["launches_splat"], 1), 4),
+            "stages": report}
     return roof
+
+
+def traversal_record(roof):
+    """The metric's "traversal HBM GB/s": the closest-hit traversal kernel of the timed run."""
+    e = roof["stages"].get("extend") or roof["stages"].get("path")
+    if not e:
+        return None
+    out = {"kernel": "wf_extend" if "extend" in roof["stages"] else "nh_path_kernel",
+           "hbm_gbs": e["hbm_gbs"], "frac_of_hbm_peak": round(e["hbm_gbs"] / HBM_PEAK_GBS, 4),
+           "avg_launch_ms": e["avg_launch_ms"]}
+    if "work_gbs" in e:
+        out["work_gbs"] = e["work_gbs"]
+        out["note"] = ("BVH staged in LDS: hbm_gbs is the ray/hit queue stream; work_gbs the algorithmic traversal "
+                       "rate (LDS reads)")
+    return out
+
+
+def cpu_cores():
+    """Host cores this process may run on (affinity mask), and the cgroup CPU quota if one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    return n, quota
 
 
 def cpu_baseline(scene, budget_s, seed):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import nori_oracle as no
-    threads = int(os.environ.get("NH_CPU_THREADS", "16"))
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    n_cpu, quota = cpu_cores()
+    threads = int(os.environ.get("NH_CPU_THREADS", "0")) or n_cpu
     orc = no.OracleScene(scene)
     rgbw = None
     t0 = time.perf_counter()
@@ -179,9 +249,123 @@ def cpu_baseline(scene, budget_s, seed):
             break
     dt = time.perf_counter() - t0
     n = rounds * orc.width * orc.height
+    q = f", cgroup CPU quota {quota:g} cores" if quota else ""
     return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{rounds} spp of the same {orc.width}x{orc.height} image ({n} samples, {dt:.1f} s), "
-                      f"oracle/nori_oracle.cpp restatement of path_mis, {threads} threads"}
+                      f"oracle/nori_oracle.cpp restatement of path_mis, {threads} threads = every core in this "
+                      f"process's affinity mask ({n_cpu}){q}"}
+
+
+def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, rank=0, dist=None):
+    """Scene setup + calibration + warmup + timed steps (+ serialized roofline pass). Returns a dict."""
+    a = argparse.Namespace(**vars(args))
+    a.config = config
+    if config != args.config:
+        a.width = a.height = None
+    tmp = tempfile.mkdtemp(prefix="nh_bench_")
+    xml, W, H, scene_desc = build_scene(a, tmp)
+    scene = nh.Scene(xml)
+    t0 = time.perf_counter()
+    bvh = nh.Bvh(scene, n_threads=16)
+    bvh_s = time.perf_counter() - t0
+    ctx = nh.Context(local)
+    t0 = time.perf_counter()
+    ctx.upload(scene, bvh)
+    upload_s = time.perf_counter() - t0
+    trav = nh.TRAVERSAL_ORDERED if a.traversal == "ordered" else nh.TRAVERSAL_REFERENCE
+    mode = nh.MODE_WAVEFRONT if a.mode == "wavefront" else nh.MODE_MEGAKERNEL
+    if args.scaling == "strong":
+        R = a.rounds  # every rank renders the whole sample budget of its 1/N of the blocks
+    else:
+        R = a.rounds * world  # each rank's 1/N of the image for N x --rounds rounds (weak scaling)
+    os.environ["NH_POOLS"] = str(a.pools)
+    calib = None
+    if not a.no_calibrate:
+        ctx.reset_stats()
+        ctx.render(0, R, seed=a.seed, blocks=blocks, traversal=trav, clear=True, stats=True, mode=mode)
+        calib = ctx.stats()
+    for w in range(warmup):
+        ctx.render(R * (steps + w), R * (steps + w + 1), seed=a.seed, blocks=blocks, traversal=trav,
+                   clear=(w == 0), mode=mode)
+    ctx.synchronize()
+    ctx.reset_stats()
+    ctx.render(0, 0, seed=a.seed, blocks=blocks, traversal=trav, clear=True)
+    ctx.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t_start = time.perf_counter()
+    for s in range(steps):
+        ctx.render(s * R, (s + 1) * R, seed=a.seed, blocks=blocks, traversal=trav, clear=False, mode=mode)
+    if dist is not None:
+        reduce_framebuffer(ctx, dist, args, local)
+    ctx.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        elapsed = max_over_ranks(elapsed, dist, args, local)
+    st = ctx.stats()
+    roof_pass = None
+    if a.mode == "wavefront" and a.pools > 1 and calib is not None and a.roofline_steps > 0:
+        # Kernels of overlapping pools share the GPU, so their event durations are no kernel roofline:
+        # time the kernels in a serialized pass (one pool) over the same workload instead.
+        os.environ["NH_POOLS"] = "1"
+        ctx.reset_stats()
+        base = R * (steps + warmup)
+        for s in range(a.roofline_steps):
+            ctx.render(base + s * R, base + (s + 1) * R, seed=a.seed, blocks=blocks, traversal=trav, mode=mode)
+        ctx.synchronize()
+        st = ctx.stats()
+        roof_pass = f"serialized pass: {a.roofline_steps} steps with one path pool (kernels alone on the GPU)"
+        os.environ["NH_POOLS"] = str(a.pools)
+    # every rank renders its 1/N of the blocks: the whole job is W x H x R samples per step
+    samples = W * H * R * steps
+    roof = None
+    if calib is not None and calib["samples"] > 0:
+        roof = roofline(a, calib, st, W, H, R)
+        roof["timed"] = roof_pass or "the timed region"
+    return {"scene": scene, "W": W, "H": H, "R": R, "desc": scene_desc, "elapsed": elapsed, "samples": samples,
+            "roof": roof, "bvh_s": bvh_s, "upload_s": upload_s, "ctx": ctx}
+
+
+def reduce_framebuffer(ctx, dist, args, local):
+    import torch
+    ptr, n = ctx.framebuffer_device_ptr()  # completes every submitted chunk first
+    if args.dist_backend == "nccl":
+        fb = _wrap_device(ptr, n, local)
+        dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+    else:
+        fb = torch.from_numpy(ctx.framebuffer().reshape(-1))
+        dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+
+
+def max_over_ranks(elapsed, dist, args, local):
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64,
+                     device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def traversal_1m(nh, args, local):
+    """perf-1M: the north star's traversal roofline target is set on the BVH-traversal
+    kernel of the ~1M-triangle scene at 1 GPU; measured here in the same run (a short bench of it)."""
+    r = run_workload(nh, args, "bumpy1m", args.traversal_1m_steps, 1, local)
+    roof = r["roof"]
+    e = roof["stages"]["extend"]
+    traffic, source = pmc_traffic(f"bumpy1m_{r['W']}x{r['H']}_r{r['R']}_{args.traversal}_{args.mode}")
+    out = {"workload": r["desc"], "msamples_s": round(r["samples"] / r["elapsed"] / 1e6, 3),
+           "kernel": "wf_trace_pt (persistent 4-wide closest-hit traversal)" if roof["node_bytes"] == 128 else "wf_extend",
+           "avg_launch_ms": e["avg_launch_ms"], "algorithmic_bytes_per_launch": e["hbm_bytes_per_launch"],
+           "achieved_gbs": e["hbm_gbs"], "frac": round(e["hbm_gbs"] / HBM_PEAK_GBS, 4), "target_frac": 0.40,
+           "nodes_per_query": e.get("nodes_per_query"), "prims_per_query": e.get("prims_per_query"),
+           "node_bytes": roof["node_bytes"],
+           "bytes": "algorithmic: nodes x node_bytes + primitive tests x 48 B + 48 B ray/hit per query",
+           "traffic": traffic, "traffic_source": source or "not collected for this workload",
+           "note": "the ~176 MB tree is resident in the 256 MB MALL: measured HBM traffic (traffic) is well below "
+                   "the algorithmic bytes; this kernel is bound by dependent-load latency",
+           "steps": args.traversal_1m_steps, "spp": r["R"] * args.traversal_1m_steps, "timed": roof["timed"]}
+    r["ctx"].close()
+    return out
 
 
 def main():
@@ -201,89 +385,28 @@ def main():
             dist.init_process_group("gloo")
     import nori_hip as nh
 
-    tmp = tempfile.mkdtemp(prefix="nh_bench_")
-    xml, W, H, scene_desc = build_scene(args, tmp)
-    scene = nh.Scene(xml)
-    t0 = time.perf_counter()
-    bvh = nh.Bvh(scene, n_threads=16)
-    bvh_s = time.perf_counter() - t0
-    ctx = nh.Context(local)
-    t0 = time.perf_counter()
-    ctx.upload(scene, bvh)
-    upload_s = time.perf_counter() - t0
+    if args.scaling == "strong" and args.config == "c2" and not args.config_given:
+        args.config = "c4"  # the north star's scaling target: a fixed C4 image split over the ranks
+    W, H = scene_dims(args)
     blocks = nh.tile_shard(W, H, world, rank) if world > 1 else None
-    trav = nh.TRAVERSAL_ORDERED if args.traversal == "ordered" else nh.TRAVERSAL_REFERENCE
-    mode = nh.MODE_WAVEFRONT if args.mode == "wavefront" else nh.MODE_MEGAKERNEL
-    # rounds per step and rank: each rank's 1/N of the image for N x --rounds rounds (weak scaling)
-    R = args.rounds * world
-    os.environ["NH_POOLS"] = str(args.pools)
-
-    # calibration launch (in-kernel counters; same seeds as the first timed step)
-    calib = None
-    if not args.no_calibrate:
-        ctx.reset_stats()
-        ctx.render(0, R, seed=args.seed, blocks=blocks, traversal=trav, clear=True, stats=True, mode=mode)
-        calib = ctx.stats()
-
-    # warmup (rounds past the timed range, separate framebuffer content)
-    for w in range(args.warmup):
-        ctx.render(R * (args.steps + w), R * (args.steps + w + 1), seed=args.seed, blocks=blocks, traversal=trav,
-                   clear=(w == 0), mode=mode)
-    ctx.synchronize()
-    ctx.reset_stats()
-    if dist is not None:
-        import torch
-        ctx.synchronize()
-        dist.barrier()
-    ctx.render(0, 0, seed=args.seed, blocks=blocks, traversal=trav, clear=True)
-    ctx.synchronize()
-    t_start = time.perf_counter()
-    for s in range(args.steps):
-        ctx.render(s * R, (s + 1) * R, seed=args.seed, blocks=blocks, traversal=trav, clear=False, mode=mode)
-    if dist is not None:
-        ctx.synchronize()
-        if args.dist_backend == "nccl":
-            ptr, n = ctx.framebuffer_device_ptr()
-            fb = _wrap_device(ptr, n, local)
-            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
-            torch.cuda.synchronize()
-        else:
-            fb = torch.from_numpy(ctx.framebuffer().reshape(-1))
-            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
-    ctx.synchronize()
-    t_end = time.perf_counter()
-    elapsed = t_end - t_start
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    st = ctx.stats()
-    total_samples = W * H * R * args.steps
-    roof_pass = None
-    if args.mode == "wavefront" and args.pools > 1 and calib is not None and args.roofline_steps > 0:
-        # Kernels of overlapping pools share the GPU, so their event durations are no kernel roofline:
-        # time the kernels in a serialized pass (one pool) over the same workload instead.
-        os.environ["NH_POOLS"] = "1"
-        ctx.reset_stats()
-        base = R * (args.steps + args.warmup)
-        for s in range(args.roofline_steps):
-            ctx.render(base + s * R, base + (s + 1) * R, seed=args.seed, blocks=blocks, traversal=trav, mode=mode)
-        ctx.synchronize()
-        st = ctx.stats()
-        roof_pass = f"serialized pass: {args.roofline_steps} steps with one path pool (kernels alone on the GPU)"
-        os.environ["NH_POOLS"] = str(args.pools)
-
+    r = run_workload(nh, args, args.config, args.steps, args.warmup, local, blocks=blocks, world=world, rank=rank,
+                     dist=dist)
     if rank == 0:
-        value = total_samples / elapsed / 1e6
-        # roofline of the path megakernel (dominant kernel)
-        roof = None
-        if calib is not None and calib["samples"] > 0:
-            roof = roofline(args, calib, st, W, H, R)
-            roof["timed"] = roof_pass or "the timed region"
+        W, H, R = r["W"], r["H"], r["R"]
+        value = r["samples"] / r["elapsed"] / 1e6
+        roof = r["roof"]
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(scene, args.cpu_seconds, args.seed)
+            cpu = cpu_baseline(r["scene"], args.cpu_seconds, args.seed)
+        t1m = None
+        if world == 1 and args.traversal_1m_steps > 0 and args.config != "bumpy1m":
+            r["ctx"].close()
+            t1m = traversal_1m(nh, args, local)
+        spp = R * args.steps
+        if args.scaling == "strong":
+            par = f"tile-shard x{world}, strong scaling: fixed {W}x{H} image, {spp} spp split by blocks"
+        else:
+            par = f"tile-shard x{world}, weak scaling: each rank {R} rounds per step over its 1/{world} of the blocks"
         line = {
             "metric": "Msamples/sec (whole node) + traversal HBM GB/s, cbox 1024x1024 256spp",
             "value": round(value, 3),
@@ -291,19 +414,21 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (reference Cornell box scene files, per-path pcg32 seeds)",
-            "config": {"workload": f"{scene_desc}, {R * args.steps} spp, path_mis", "config": args.config,
-                       "width": W, "height": H, "spp": R * args.steps, "rounds_per_step": R,
+            "data": "synthetic (reference Cornell box scene files, generated meshes, per-path pcg32 seeds)",
+            "config": {"workload": f"{r['desc']}, {spp} spp, path_mis", "config": args.config,
+                       "width": W, "height": H, "spp": spp, "rounds_per_step": R,
                        "mode": args.mode, "traversal": args.traversal, "pools": args.pools,
-                       "parallelism": (f"tile-shard x{world} + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce"
+                       "parallelism": (f"{par} + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce"
                                        if world > 1 else "single GPU"),
-                       "bvh_build_s": round(bvh_s, 3), "upload_s": round(upload_s, 3)},
+                       "bvh_build_s": round(r["bvh_s"], 3), "upload_s": round(r["upload_s"], 3)},
             "roofline": roof,
+            "traversal": traversal_record(roof) if roof else None,
+            "traversal_1m": t1m,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

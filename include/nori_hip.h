@@ -51,10 +51,11 @@ extern "C" {
 enum { NH_SHAPE_MESH = 0, NH_SHAPE_SPHERE = 1 };
 enum { NH_BSDF_DIFFUSE = 0, NH_BSDF_MIRROR = 1, NH_BSDF_DIELECTRIC = 2, NH_BSDF_MICROFACET = 3 };
 enum { NH_EMITTER_AREA = 0, NH_EMITTER_POINT = 1, NH_EMITTER_ENVMAP = 2 };
-/* path_mis (src/integrators/path_mis.cpp), path_mats (path_mats.cpp), and the single-bounce
- * direct_ems / direct_mats / direct_mis (direct_ems.cpp, direct_mats.cpp, direct_mis.cpp) */
+/* path_mis (src/integrators/path_mis.cpp), path_mats (path_mats.cpp), the single-bounce
+ * direct_ems / direct_mats / direct_mis (direct_ems.cpp, direct_mats.cpp, direct_mis.cpp) and the
+ * point-light `direct` integrator (direct.cpp, scenes/pa1) */
 enum { NH_INTEGRATOR_PATH_MIS = 0, NH_INTEGRATOR_PATH_MATS = 1, NH_INTEGRATOR_DIRECT_EMS = 2,
-       NH_INTEGRATOR_DIRECT_MATS = 3, NH_INTEGRATOR_DIRECT_MIS = 4 };
+       NH_INTEGRATOR_DIRECT_MATS = 3, NH_INTEGRATOR_DIRECT_MIS = 4, NH_INTEGRATOR_DIRECT = 5 };
 
 /* One Nori Shape (src/shapes/mesh.cpp, src/shapes/sphere.cpp). Mesh data lives in
  * the scene-wide concatenated arrays at the given offsets. */
@@ -238,6 +239,13 @@ typedef struct nh_render_stats {
     /* bytes of one BVH node as counted in nodes_visited: 64 (binary tree) or 128 (the 4-wide
        collapse, NH_TRAVERSAL_WIDE), for the last render */
     uint64_t node_bytes;
+    /* the tail kernel's share of ray_queries / nodes_visited / boxes_tested / prims_tested (closest
+       + any hit), and of that its any-hit part (also counted in shadow_*), collect_stats only */
+    uint64_t tail_queries, tail_nodes_visited, tail_boxes_tested, tail_prims_tested;
+    uint64_t tail_shadow_queries, tail_shadow_nodes_visited, tail_shadow_boxes_tested, tail_shadow_prims_tested;
+    /* 1 when the last wavefront render traversed an LDS copy of the BVH (scenes of a few KB): its node
+       and primitive reads then come from LDS, not HBM */
+    uint64_t lds_scene;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;
@@ -285,7 +293,8 @@ int nh_trace_rays(nh_ctx *ctx, const nh_ray_soa *rays, int32_t n, int32_t any_hi
 int nh_render(nh_ctx *ctx, const nh_render_req *req);
 int nh_synchronize(nh_ctx *ctx);
 int nh_get_framebuffer(nh_ctx *ctx, float *rgbw, size_t n_floats);
-/* device pointer of the (W+2b)(H+2b)x4 fp32 framebuffer, for collectives issued by the caller */
+/* device pointer of the (W+2b)(H+2b)x4 fp32 framebuffer, for collectives issued by the caller;
+   completes every submitted render first (the wavefront pipeline advances only inside library calls) */
 int nh_framebuffer_device_ptr(nh_ctx *ctx, void **dptr, size_t *n_floats);
 int nh_get_stats(nh_ctx *ctx, nh_render_stats *out);
 int nh_reset_stats(nh_ctx *ctx);

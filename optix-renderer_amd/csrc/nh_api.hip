@@ -31,6 +31,7 @@ using nhd::DShape;
 // ---- wavefront pipeline state (used by nh_render, see the pipeline section below) ----
 constexpr int kRing = 4;   // bounce-count copies in flight per pool
 constexpr int kPools = 2;  // path pools in flight: one drains its last bounces while the next fills the GPU
+constexpr int kMaxStack = 128;  // deepest per-lane LDS stack of the binary-tree kernels (DEPTH template)
 
 // one chunk of sample rounds of one nh_render call
 struct WfJob {
@@ -327,7 +328,7 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         S.env_b = e.radiance[2];
     }
     S.n_emitters = (int)d->n_emitters;
-    if (d->integrator < NH_INTEGRATOR_PATH_MIS || d->integrator > NH_INTEGRATOR_DIRECT_MIS)
+    if (d->integrator < NH_INTEGRATOR_PATH_MIS || d->integrator > NH_INTEGRATOR_DIRECT)
         return fail(c, "unknown integrator"), NH_ERR_INVALID;
     S.integrator = d->integrator;
     std::memcpy(S.s2c, d->camera.sample_to_camera, sizeof(S.s2c));
@@ -450,6 +451,7 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
 
     std::vector<float4> nodes;
     std::vector<int2> leaves;
+    uint32_t tree_depth = 0;
     nhd::DScene &S = c->S;
     if (b->n_nodes == 0) {
         S.root_kind = 0;
@@ -462,18 +464,23 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
         } else {
             S.root_kind = 1;
             // DFS (left first) over inner nodes assigning GPU ids in visit order
+            // (the tree's depth is measured here, not taken from nh_bvh_desc::max_depth: it sizes the
+            // traversal stacks)
             std::vector<int> gid(b->n_nodes, -1);
-            std::vector<uint32_t> order, st{0u};
+            std::vector<uint32_t> order;
+            std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 0u}};  // (node, level)
             while (!st.empty()) {
-                uint32_t i = st.back();
+                const uint32_t i = st.back().first, lvl = st.back().second;
                 st.pop_back();
+                tree_depth = std::max(tree_depth, lvl);
                 if (N[i].word0 & 1u) continue;
+                if (gid[i] >= 0) return fail(c, "corrupt BVH: node reached twice"), NH_ERR_INVALID;
                 gid[i] = (int)order.size();
                 order.push_back(i);
                 if (N[i].word1 >= b->n_nodes || i + 1 >= b->n_nodes)
                     return fail(c, "corrupt BVH child index"), NH_ERR_INVALID;
-                st.push_back(N[i].word1);
-                st.push_back(i + 1);
+                st.push_back({N[i].word1, lvl + 1});
+                st.push_back({i + 1, lvl + 1});
             }
             nodes.resize(4 * order.size());
             auto child_ref = [&](uint32_t ch) -> int {
@@ -534,6 +541,10 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
             bits |= nhd::kPrimLeafEnd;
             std::memcpy(&w.w, &bits, 4);
         }
+    // The binary-tree kernels keep a per-lane stack of at most kMaxStack entries (the deferred
+    // children of one root-to-leaf path; the reference keeps 64, bvh.cpp:403)
+    if (tree_depth + 2 > (uint32_t)kMaxStack)
+        return fail(c, "BVH deeper than " + std::to_string(kMaxStack - 2) + " levels is not supported"), NH_ERR_UNSUPPORTED;
     int depth4 = 0;
     const std::vector<float4> wide = collapse_wide(nodes, leaves, depth4);
     int rc;
@@ -554,7 +565,7 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     S.prims = c->tv.prims;
     c->bvh_indices.assign(b->indices, b->indices + b->n_indices);
     c->shape_offset = off;
-    c->depth = (int)b->max_depth + 2;
+    c->depth = (int)tree_depth + 2;
     if (!c->d_scene) HIP_TRY(c, hipMalloc(&c->d_scene, sizeof(nhd::DScene)));
     HIP_TRY(c, hipMemcpyAsync(c->d_scene, &c->S, sizeof(nhd::DScene), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -641,13 +652,17 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
 constexpr size_t kWfBytesPerPath = 2 * (16 * 6 + 8 + 1) + 36;  // two buffers + shadow queue
 
 static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t staging_f4) {
-    if (!p.stream) {
-        HIP_TRY(c, hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));
-        if (hipHostMalloc(reinterpret_cast<void **>(&p.h_counts),
-                          (kRing * 2 * kCountGroup + kCountSlot) * sizeof(unsigned)) != hipSuccess)
+    if (!p.stream) {  // the stream is created last: a pool with a stream has all of these
+        if (!p.h_counts && hipHostMalloc(reinterpret_cast<void **>(&p.h_counts),
+                                         (kRing * 2 * kCountGroup + kCountSlot) * sizeof(unsigned)) != hipSuccess) {
+            p.h_counts = nullptr;
             return fail(c, "hipHostMalloc failed"), NH_ERR_DEVICE;
-        for (hipEvent_t &e : p.copy_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        for (hipEvent_t *e : {&p.ev_begin, &p.ev_path, &p.ev_splat0, &p.ev_splat}) HIP_TRY(c, hipEventCreate(e));
+        }
+        for (hipEvent_t &e : p.copy_ev)
+            if (!e) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (hipEvent_t *e : {&p.ev_begin, &p.ev_path, &p.ev_splat0, &p.ev_splat})
+            if (!*e) HIP_TRY(c, hipEventCreate(e));
+        HIP_TRY(c, hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));
     }
     if (p.cap < n) {
         free_all(p.bufs);
@@ -680,8 +695,9 @@ static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t staging_f4) {
     if (p.staging_cap < staging_f4) {
         (void)hipFree(p.staging);
         p.staging = nullptr;
-        p.staging_cap = staging_f4;
+        p.staging_cap = 0;
         HIP_TRY(c, hipMalloc(&p.staging, staging_f4 * sizeof(float4)));
+        p.staging_cap = staging_f4;
     }
     return NH_OK;
 }
@@ -769,10 +785,12 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
         HIP_TRY(c, hipStreamSynchronize(p.stream));
         (void)hipFree(p.spill);
         p.spill = nullptr;
-        p.spill_words = spill_words;
+        p.spill_words = 0;
         HIP_TRY(c, hipMalloc(&p.spill, (size_t)kPersistentBlocks * 128 * spill_words * sizeof(uint32_t)));
+        p.spill_words = spill_words;
     }
     c->stats.node_bytes = p.wide ? 16 * nhd::kWideF4 : 64;
+    c->stats.lds_scene = small && !p.persistent && c->depth <= 16 ? 1 : 0;  // the SMALL instantiations (DEPTH 16)
     L.trav_spill = p.spill;
     L.spill_depth = p.spill_words;
     // measured on 16.7M-path chunks: C2 3025 / 3030 / 2692 Msamples/s at 64k / 262k / 1M,
@@ -1083,6 +1101,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     rc = ensure_pixel_list(c, q);
     if (rc) return rc;
     c->stats.node_bytes = 64;  // binary tree unless a wavefront pool picks the 4-wide one
+    c->stats.lds_scene = 0;
     if (q->clear) {
         HIP_TRY(c, hipMemsetAsync(c->fb, 0, c->fb_floats * sizeof(float), c->stream));
         HIP_TRY(c, hipEventRecord(c->fb_ev, c->stream));  // pools' splats wait for it
@@ -1120,15 +1139,19 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
             (void)hipFree(c->rec_jy);
             c->rec = nullptr;
             c->rec_jy = nullptr;
-            c->rec_cap = (size_t)chunk * per_round;
-            HIP_TRY(c, hipMalloc(&c->rec, c->rec_cap * sizeof(float4)));
-            HIP_TRY(c, hipMalloc(&c->rec_jy, c->rec_cap * sizeof(float)));
+            c->rec_cap = 0;
+            const size_t cap = (size_t)chunk * per_round;
+            HIP_TRY(c, hipMalloc(&c->rec, cap * sizeof(float4)));
+            HIP_TRY(c, hipMalloc(&c->rec_jy, cap * sizeof(float)));
+            c->rec_cap = cap;
         }
         if (c->staging_cap < (size_t)chunk * c->n_blocks * block_px(c)) {
             (void)hipFree(c->staging);
             c->staging = nullptr;
-            c->staging_cap = (size_t)chunk * c->n_blocks * block_px(c);
-            HIP_TRY(c, hipMalloc(&c->staging, c->staging_cap * sizeof(float4)));
+            c->staging_cap = 0;
+            const size_t cap = (size_t)chunk * c->n_blocks * block_px(c);
+            HIP_TRY(c, hipMalloc(&c->staging, cap * sizeof(float4)));
+            c->staging_cap = cap;
         }
         struct Ev {
             hipEvent_t a, b, d;
@@ -1176,19 +1199,28 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         c->stats.samples += (uint64_t)rounds * (uint64_t)c->n_list;
     }
     if (q->collect_stats) {
-        unsigned long long hs[kStatShards * kStatStride], h[16] = {};
+        unsigned long long hs[kStatShards * kStatStride], h[kStatStride] = {};
         HIP_TRY(c, hipMemcpy(hs, c->counters, sizeof(hs), hipMemcpyDeviceToHost));
         for (int sh = 0; sh < kStatShards; ++sh)
-            for (int j = 0; j < 16; ++j) h[j] += hs[sh * kStatStride + j];
-        c->stats.ray_queries += h[0] + h[8];
-        c->stats.nodes_visited += h[1] + h[9];
-        c->stats.boxes_tested += h[2] + h[10];
-        c->stats.prims_tested += h[3] + h[11];
+            for (int j = 0; j < kStatStride; ++j) h[j] += hs[sh * kStatStride + j];
+        const unsigned long long *cl = h, *an = h + kStatAny, *tc = h + kStatTail, *ta = h + kStatTailAny;
+        c->stats.ray_queries += cl[0] + an[0] + tc[0] + ta[0];
+        c->stats.nodes_visited += cl[1] + an[1] + tc[1] + ta[1];
+        c->stats.boxes_tested += cl[2] + an[2] + tc[2] + ta[2];
+        c->stats.prims_tested += cl[3] + an[3] + tc[3] + ta[3];
         c->stats.invalid_samples += h[4];
-        c->stats.shadow_queries += h[8];
-        c->stats.shadow_nodes_visited += h[9];
-        c->stats.shadow_boxes_tested += h[10];
-        c->stats.shadow_prims_tested += h[11];
+        c->stats.shadow_queries += an[0] + ta[0];
+        c->stats.shadow_nodes_visited += an[1] + ta[1];
+        c->stats.shadow_boxes_tested += an[2] + ta[2];
+        c->stats.shadow_prims_tested += an[3] + ta[3];
+        c->stats.tail_queries += tc[0] + ta[0];
+        c->stats.tail_nodes_visited += tc[1] + ta[1];
+        c->stats.tail_boxes_tested += tc[2] + ta[2];
+        c->stats.tail_prims_tested += tc[3] + ta[3];
+        c->stats.tail_shadow_queries += ta[0];
+        c->stats.tail_shadow_nodes_visited += ta[1];
+        c->stats.tail_shadow_boxes_tested += ta[2];
+        c->stats.tail_shadow_prims_tested += ta[3];
     }
     return NH_OK;
 }
@@ -1217,6 +1249,12 @@ int nh_get_framebuffer(nh_ctx *c, float *rgbw, size_t n) {
 int nh_framebuffer_device_ptr(nh_ctx *c, void **dptr, size_t *n) {
     if (!c || !dptr || !n) return NH_ERR_INVALID;
     if (!c->has_scene) return fail(c, "no scene"), NH_ERR_STATE;
+    // The pipeline advances only inside library calls (the host reads queue counts to enqueue the
+    // next bounce): run every submitted chunk to completion first, so a caller that hands the
+    // pointer to its own stream or collective (RCCL reduce) reads the finished image.
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc = pipeline_drain(c)) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     *dptr = c->fb;
     *n = c->fb_floats;
     return NH_OK;

@@ -41,9 +41,10 @@ struct SplatLaunch {
 };
 
 // In-kernel work counters (collect_stats): kStatShards copies of [0-3] queries, nodes, boxes, prims,
-// [4] invalid samples, [8-11] the any-hit share, one copy per XCD (workgroup b adds to copy b % 8)
-// so the per-wave atomics of concurrent workgroups do not serialise on one address.
-constexpr int kStatShards = 8, kStatStride = 32;
+// [4] invalid samples, [8-11] the any-hit share, [16-19] / [20-23] the closest / any-hit work of
+// the tail kernel, one copy per XCD (workgroup b adds to copy b % 8) so the per-wave atomics of
+// concurrent workgroups do not serialise on one address.
+constexpr int kStatShards = 8, kStatStride = 32, kStatAny = 8, kStatTail = 16, kStatTailAny = 20;
 __device__ __forceinline__ unsigned long long *stat_shard(unsigned long long *c) {
     return c + (blockIdx.x & (kStatShards - 1)) * kStatStride;
 }

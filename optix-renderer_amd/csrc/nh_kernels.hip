@@ -371,6 +371,37 @@ __device__ F3 li_direct_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o
 }
 #undef NH_DIRECT_PROLOGUE
 
+// DirectIntegrator::Li (src/integrators/direct.cpp:17-63, the point-light integrator of scenes/pa1):
+// every emitter sampled once in scene order (its own 2D sample), its shadow ray always traced;
+// unoccluded samples add li * |wi . n| / |wi| * f(wi = toward the light, wo = toward the ray
+// origin). No emitter-hit term.
+template <int DEPTH, bool ORDERED, bool STATS>
+__device__ F3 li_direct_simple(const DScene &S, const Traversal &tv, Rng &rng, F3 o, F3 d, float mint, float maxt,
+                               uint32_t *stk, int stride, TravStats &st, uint32_t &queries) {
+    Hit h;
+    if (STATS) queries++;
+    if (!trace<DEPTH, ORDERED, false, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st))
+        return S.envmap >= 0 ? env_eval(S, d) : f3(0, 0, 0);
+    Its its;
+    hit_info(S, tv, h, o, d, its);
+    const DBsdf bsdf = S.bsdfs[S.shapes[its.shape].bsdf];
+    const F3 wo = to_local(its.sh, normalized(sub(o, its.p)));
+    F3 result = f3(0, 0, 0);
+    for (int l = 0; l < S.n_emitters; ++l) {
+        const float ex = rng.next1d(), ey = rng.next1d();
+        ESample es;
+        const F3 li = emitter_sample(S, S.emitters[l], its.p, ex, ey, es);
+        const F3 wi = to_local(its.sh, es.wi);
+        Hit hs;
+        if (STATS) queries++;
+        if (trace<DEPTH, ORDERED, true, STATS>(tv, S, es.so, es.sd, es.smint, es.smaxt, hs, stk, stride, st)) continue;
+        const F3 f = bsdf_eval(bsdf, wi, wo, M_SOLID_ANGLE);
+        const float cs = fabsf(dot(es.wi, its.sh.n)) / f_sqrt(dot(es.wi, es.wi));
+        result = add(result, mulc(scl(cs, li), f));
+    }
+    return result;
+}
+
 template <int BLOCK, int DEPTH, bool ORDERED, bool STATS, int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__restrict__ Sp, Traversal tv, PathLaunch L) {
     __shared__ uint32_t stk[DEPTH * BLOCK];
@@ -398,6 +429,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
             case 2: li = li_direct_ems<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
             case 3: li = li_direct_mats<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
             case 4: li = li_direct_mis<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
+            case 5: li = li_direct_simple<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
             default: li = li_path_mis<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
         }
         const size_t r = (size_t)k * L.n_list + i;

@@ -633,9 +633,9 @@ __global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Tr
             }
         }
     }
-    if (STATS) {
-        flush_trav_stats(stat_shard(L.counters), q_e, st_e);
-        flush_trav_stats(stat_shard(L.counters) + 8, q_s, st_s);
+    if (STATS) {  // the tail's own counter slots (kStatTail*), so stage rates stay per kernel
+        flush_trav_stats(stat_shard(L.counters) + kStatTail, q_e, st_e);
+        flush_trav_stats(stat_shard(L.counters) + kStatTailAny, q_s, st_s);
     }
 }
 

@@ -30,6 +30,9 @@ int paeth(int a, int b, int c) {
 
 }  // namespace
 
+// 2^28 pixels: 1 GiB of RGBA8 output, at most 2 GiB of raw 64-bit scanlines (< 2^32 for zlib's uInt)
+constexpr uint64_t kMaxPngPixels = (uint64_t)1 << 28;
+
 bool png_decode_rgba8(const std::string &path, std::vector<uint8_t> &out, unsigned &width, unsigned &height,
                       std::string &err) {
     std::ifstream is(path, std::ios::binary);
@@ -66,6 +69,10 @@ bool png_decode_rgba8(const std::string &path, std::vector<uint8_t> &out, unsign
         pos += 12 + (size_t)len;
     }
     if (!seen_ihdr || width == 0 || height == 0) return err = path + ": missing IHDR", false;
+    // the PNG spec limits each dimension to 2^31-1; the decoded RGBA8 image (and the 16-bit raw
+    // scanlines, up to 8 bytes per pixel) must also fit the size_t / zlib uInt arithmetic below
+    if (width > 0x7fffffffu || height > 0x7fffffffu || (uint64_t)width * height > kMaxPngPixels)
+        return err = path + ": image too large", false;
     if (interlace != 0) return err = path + ": interlaced PNG is not supported", false;
     int channels;
     switch (ctype) {

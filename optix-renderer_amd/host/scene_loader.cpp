@@ -832,6 +832,7 @@ void build_scene(const Obj &scene, const std::string &base_dir, SceneData &sd) {
             else if (ch.type == "direct_ems") sd.integrator = NH_INTEGRATOR_DIRECT_EMS;
             else if (ch.type == "direct_mats") sd.integrator = NH_INTEGRATOR_DIRECT_MATS;
             else if (ch.type == "direct_mis") sd.integrator = NH_INTEGRATOR_DIRECT_MIS;
+            else if (ch.type == "direct") sd.integrator = NH_INTEGRATOR_DIRECT;
             else throw SceneError("integrator \"" + ch.type + "\" is not supported by the HIP path");
         } else if (ch.tag == "camera") {
             if (have_camera) throw SceneError("there can only be one camera per scene");
@@ -1084,7 +1085,7 @@ int nh_scene_set_bsdf(nh_scene *scene, uint32_t shape, const nh_bsdf *bsdf) {
 }
 
 int nh_scene_set_integrator(nh_scene *scene, int32_t integrator) {
-    if (!scene || integrator < NH_INTEGRATOR_PATH_MIS || integrator > NH_INTEGRATOR_DIRECT_MIS) {
+    if (!scene || integrator < NH_INTEGRATOR_PATH_MIS || integrator > NH_INTEGRATOR_DIRECT) {
         nh::set_host_error("invalid integrator");
         return NH_ERR_INVALID;
     }

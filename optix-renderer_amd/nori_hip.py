@@ -30,6 +30,7 @@ SHAPE_MESH, SHAPE_SPHERE = 0, 1
 BSDF_DIFFUSE, BSDF_MIRROR, BSDF_DIELECTRIC, BSDF_MICROFACET = 0, 1, 2, 3
 EMITTER_AREA, EMITTER_POINT, EMITTER_ENVMAP = 0, 1, 2
 INTEGRATOR_PATH_MIS, INTEGRATOR_PATH_MATS, INTEGRATOR_DIRECT_EMS, INTEGRATOR_DIRECT_MATS, INTEGRATOR_DIRECT_MIS = 0, 1, 2, 3, 4
+INTEGRATOR_DIRECT = 5  # the point-light `direct` integrator of scenes/pa1 (direct.cpp)
 MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1
 TRAVERSAL_REFERENCE, TRAVERSAL_ORDERED, TRAVERSAL_WIDE = 0, 1, 2
 
@@ -118,7 +119,10 @@ class nh_render_stats(C.Structure):
                 ("shadow_prims_tested", C.c_uint64), ("shade_state_bytes", C.c_uint64),
                 ("extend_queue_bytes", C.c_uint64), ("shadow_queue_bytes", C.c_uint64),
                 ("paths_shaded", C.c_uint64), ("kernel_ms_tail", C.c_double), ("launches_tail", C.c_uint64),
-                ("node_bytes", C.c_uint64)]
+                ("node_bytes", C.c_uint64)] + [
+        (n, C.c_uint64) for n in ("tail_queries", "tail_nodes_visited", "tail_boxes_tested", "tail_prims_tested",
+                                  "tail_shadow_queries", "tail_shadow_nodes_visited", "tail_shadow_boxes_tested",
+                                  "tail_shadow_prims_tested", "lds_scene")]
 
 
 def _sig(name, res, *args):

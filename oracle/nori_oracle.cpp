@@ -966,6 +966,35 @@ V3 li_direct_mis(const no_scene &s, Sampler &smp, const Ray &ray) {  // direct_m
     return result + w_ems * result_ems + w_mat * result_mats;
 }
 
+// DirectIntegrator::Li (direct.cpp:17-63, the point-light integrator of scenes/pa1): every emitter is
+// sampled once (its own next2D) and its shadow ray traced; unoccluded samples add
+// li * |wi . n| / |wi| * f(wi = light, wo = toward the ray origin). No emitter-hit term.
+V3 li_direct(const no_scene &s, Sampler &smp, const Ray &ray) {
+    Its its;
+    if (!bvh_intersect(s, ray, its, false)) return s.envmap >= 0 ? env_eval(s, ray.d) : mk(0, 0, 0);
+    V3 result = mk(0, 0, 0);
+    const nh_bsdf &bsdf = s.bsdfs[s.shapes[its.shape].bsdf];
+    const V3 wo = its.sh.to_local(normalized(ray.o - its.p));
+    for (const nh_emitter &l : s.emitters) {
+        ERec rec;
+        rec.ref = its.p;
+        float ex, ey;
+        smp.next2d(ex, ey);
+        const V3 li = emitter_sample(s, l, rec, ex, ey);
+        const V3 wi = its.sh.to_local(rec.wi);
+        Its dummy;
+        if (bvh_intersect(s, rec.shadow, dummy, true)) continue;
+        BRec bq;
+        bq.wi = wi;
+        bq.wo = wo;
+        bq.measure = ESolidAngle;
+        const V3 f = bsdf_eval(bsdf, bq);
+        const float cs = std::abs(dot(rec.wi, its.sh.n)) / norm(rec.wi);
+        result = result + cmul(li * cs, f);
+    }
+    return result;
+}
+
 // PerspectiveCamera::sampleRay (perspective.cpp:97-141), no depth of field
 Ray camera_ray(const nh_camera &c, float px, float py) {
     const float *m = c.sample_to_camera;
@@ -1006,6 +1035,7 @@ V3 li(const no_scene &s, Sampler &smp, const Ray &r) {
         case NH_INTEGRATOR_DIRECT_EMS: return li_direct_ems(s, smp, r);
         case NH_INTEGRATOR_DIRECT_MATS: return li_direct_mats(s, smp, r);
         case NH_INTEGRATOR_DIRECT_MIS: return li_direct_mis(s, smp, r);
+        case NH_INTEGRATOR_DIRECT: return li_direct(s, smp, r);
         default: return li_path_mis(s, smp, r);
     }
 }

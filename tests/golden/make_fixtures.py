@@ -8,8 +8,8 @@ Writes (all data, no reference source):
                           own pcg32-demo.cpp when that binary exists
   reference_scenes.json   scene inputs the reference's own tests and benchmarks use: the Cornell
                           box (scenes/pa4/cbox), the path-integrator known-answer tests
-                          (scenes/pa4/tests) and the microfacet BSDF tests (scenes/pa3/tests
-                          ttest/chi2test XML). Stored as {relative path: file text}; tests write
+                          (scenes/pa4/tests), the microfacet BSDF tests (scenes/pa3/tests
+                          ttest/chi2test XML) and the point-light tests (scenes/pa1/test-direct.xml). Stored as {relative path: file text}; tests write
                           them to a temporary directory and load them through nh_scene_load_xml.
 """
 import json
@@ -48,6 +48,9 @@ SCENE_FILES = [
     "scenes/pa3/tests/polylum3.obj",
     "scenes/pa3/tests/polylum4.obj",
     "scenes/pa3/tests/polylum5.obj",
+    # point-light known-answer scenes of the `direct` integrator (PointLight, pointlight.cpp:47-78)
+    "scenes/pa1/test-direct.xml",
+    "scenes/pa1/disk.obj",
 ]
 
 

@@ -45,7 +45,11 @@ def secondary_rays(oracle, n, seed):
     o, d, mint, maxt = random_rays(n, -1.0, 2.0, seed)
     h = oracle.trace(o, d, mint, maxt)
     m = h["hit"] == 1
-    p = o[m] + h["t"][m][:, None] * d[m]
+    with np.errstate(invalid="ignore", over="ignore"):
+        p = o[m] + h["t"][m][:, None] * d[m]
+    # a hit at t = inf is legal for an unbounded ray (t <= maxt, mesh.cpp:138) but has no surface point
+    p = p[np.isfinite(p).all(axis=1)]
+    assert len(p) > 0.9 * m.sum()
     rng = np.random.default_rng(seed + 1)
     d2 = rng.normal(size=p.shape).astype(np.float32)
     d2 /= np.linalg.norm(d2, axis=1, keepdims=True)
@@ -161,9 +165,10 @@ def test_render_parity_direct(gpu, tmp_path, scene, integrator):
 
 def test_direct_ttest_scenes_match_oracle(gpu, scene_dir):
     """The reference's direct-integrator known-answer scenes (scenes/pa3/tests/test-mesh*.xml, 1x1
-    pixel cameras): GPU render equals the oracle's bit for bit at 64 spp."""
-    for name in ("test-mesh.xml", "test-mesh-furnace.xml"):
-        path = os.path.join(scene_dir, "scenes/pa3/tests", name)
+    pixel cameras) and the point-light scenes of the `direct` integrator (scenes/pa1/test-direct.xml,
+    PointLight::sample/eval, pointlight.cpp:47-78): GPU render equals the oracle's bit for bit at 64 spp."""
+    for name in ("pa3/tests/test-mesh.xml", "pa3/tests/test-mesh-furnace.xml", "pa1/test-direct.xml"):
+        path = os.path.join(scene_dir, "scenes", name)
         for i in range(len(scenegen.test_references(path))):
             s = nh.Scene(path, i)
             b = nh.Bvh(s)
@@ -306,8 +311,10 @@ def test_framebuffer_device_pointer_wraps_in_torch(gpu, tmp_path):
     spec.loader.exec_module(bench)
     s, b, ctx = setup(scenegen.cbox_xml(str(tmp_path), "c2"), 64, 48)
     ctx.render(0, 4, seed=2, clear=True, mode=nh.MODE_WAVEFRONT)
+    # no nh_synchronize: the pointer call itself completes the submitted chunks (the pipeline only
+    # advances inside library calls), so a torch-side device sync is enough
     ptr, n = ctx.framebuffer_device_ptr()
-    ctx.synchronize()
+    torch.cuda.synchronize()
     t = bench._wrap_device(ptr, n, 0)
     np.testing.assert_array_equal(t.cpu().numpy(), ctx.framebuffer().reshape(-1))
     orig = ctx.framebuffer().reshape(-1).copy()

@@ -87,9 +87,11 @@ def students_t_test(mean, variance, reference, n, alpha, num_tests):
 
 
 @pytest.mark.parametrize("name", ["pa4/tests/test-furnace.xml", "pa4/tests/test-direct.xml",
-                                  "pa3/tests/test-mesh.xml", "pa3/tests/test-mesh-furnace.xml"])
+                                  "pa3/tests/test-mesh.xml", "pa3/tests/test-mesh-furnace.xml",
+                                  "pa1/test-direct.xml"])
 def test_scene_ttests(scene_dir, name):
-    """pa4: path_mats / path_mis; pa3: direct_ems / direct_mats / direct_mis (5 + 2 scenes each)."""
+    """pa4: path_mats / path_mis; pa3: direct_ems / direct_mats / direct_mis (5 + 2 scenes each);
+    pa1: the point-light `direct` integrator (4 scenes: visible, visible, hidden, all three lights)."""
     path = os.path.join(scene_dir, "scenes", name)
     refs = scenegen.test_references(path)
     rng = no.Pcg32()  # Independent sampler created once, never prepare()d (ttest.cpp:193-194)
