@@ -237,7 +237,10 @@ def cpu_baseline(scene, budget_s, seed):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import nori_oracle as no
     n_cpu, quota = cpu_cores()
-    threads = int(os.environ.get("NH_CPU_THREADS", "0")) or n_cpu
+    # every core this process may use: the affinity mask, capped by the cgroup CPU quota (the GPU box
+    # grants a 16-core share of a larger host; more threads than the quota only time-slice)
+    usable = min(n_cpu, max(1, int(quota + 0.999))) if quota else n_cpu
+    threads = int(os.environ.get("NH_CPU_THREADS", "0")) or usable
     orc = no.OracleScene(scene)
     rgbw = None
     t0 = time.perf_counter()
@@ -252,8 +255,8 @@ def cpu_baseline(scene, budget_s, seed):
     q = f", cgroup CPU quota {quota:g} cores" if quota else ""
     return {"value": round(n / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{rounds} spp of the same {orc.width}x{orc.height} image ({n} samples, {dt:.1f} s), "
-                      f"oracle/nori_oracle.cpp restatement of path_mis, {threads} threads = every core in this "
-                      f"process's affinity mask ({n_cpu}){q}"}
+                      f"oracle/nori_oracle.cpp restatement of path_mis, {threads} threads = every core this process "
+                      f"may use (affinity mask {n_cpu} CPUs{q})"}
 
 
 def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, rank=0, dist=None):
