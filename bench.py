@@ -154,7 +154,19 @@ def roofline(args, calib, st, W, H, R):
     lds = bool(calib.get("lds_scene"))
     per_launch = lambda b, launches: b / paths * st["samples"] / max(launches, 1)  # noqa: E731
     stages = {}
-    if args.mode == "wavefront":
+    fused = args.mode == "wavefront" and bool(calib.get("fused_bounce"))
+    if fused:
+        # one wf_bounce kernel per bounce (shade + any-hit + closest hit over the LDS copy of the BVH):
+        # its HBM bytes are the path state; the traversal work is LDS reads
+        w = stage_work(calib)
+        (eq, en, ep), (sq, sn, sp) = w["extend"], w["shadow"]
+        trav = (en + sn) * node_b + (ep + sp) * PRIM_BYTES
+        stages["bounce"] = {"work_bytes": calib["shade_state_bytes"] + trav, "hbm_bytes": calib["shade_state_bytes"],
+                            "queries": eq + sq, "nodes": en + sn, "prims": ep + sp, "ms": "shade"}
+        q, n, p = w["tail"]
+        trav = n * node_b + p * PRIM_BYTES
+        stages["tail"] = {"work_bytes": trav, "hbm_bytes": 0 if lds else trav, "queries": q, "nodes": n, "prims": p}
+    elif args.mode == "wavefront":
         w = stage_work(calib)
         for k in ("extend", "shadow", "tail"):
             q, n, p = w[k]
@@ -169,7 +181,8 @@ def roofline(args, calib, st, W, H, R):
         stages["path"] = {"work_bytes": b, "hbm_bytes": b, "queries": q, "nodes": n, "prims": p}
     report = {}
     for k, v in stages.items():
-        ms, launches = st[f"kernel_ms_{k}"], st[f"launches_{k}"]
+        src = v.get("ms", k)  # the fused bounce kernel's time is recorded in the shade slot
+        ms, launches = st[f"kernel_ms_{src}"], st[f"launches_{src}"]
         if ms <= 0 or launches == 0:
             continue
         avg = ms / launches
@@ -178,7 +191,8 @@ def roofline(args, calib, st, W, H, R):
              "hbm_gbs": round(per_launch(v["hbm_bytes"], launches) / (avg * 1e-3) / 1e9, 1)}
         if v["work_bytes"] != v["hbm_bytes"]:
             r["work_gbs"] = round(per_launch(v["work_bytes"], launches) / (avg * 1e-3) / 1e9, 1)
-            r["work_note"] = "algorithmic node/primitive bytes read from the LDS copy of the BVH: not HBM traffic"
+            r["work_note"] = ("algorithmic node/primitive bytes read from the LDS copy of the BVH: not HBM traffic"
+                              if lds else "algorithmic bytes")
         if "queries" in v and v["queries"]:
             r["nodes_per_query"] = round(v["nodes"] / v["queries"], 3)
             r["prims_per_query"] = round(v["prims"] / v["queries"], 3)
@@ -187,7 +201,7 @@ def roofline(args, calib, st, W, H, R):
         report[k] = r
     dom = max(report, key=lambda k: report[k]["ms"])
     kernel = {"shade": "wf_shade", "extend": "wf_extend", "shadow": "wf_shadow", "tail": "wf_tail",
-              "path": "nh_path_kernel"}[dom]
+              "path": "nh_path_kernel", "bounce": "wf_bounce (shade + any-hit + closest-hit, fused)"}[dom]
     d = report[dom]
     key = f"{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}"
     single = int(os.environ.get("WORLD_SIZE", "1")) == 1
@@ -206,17 +220,19 @@ def roofline(args, calib, st, W, H, R):
 
 
 def traversal_record(roof):
-    """The metric's "traversal HBM GB/s": the closest-hit traversal kernel of the timed run."""
-    e = roof["stages"].get("extend") or roof["stages"].get("path")
-    if not e:
+    """The metric's "traversal HBM GB/s": the closest-hit traversal kernel of the timed run (the fused
+    bounce kernel when the BVH is traversed inside it)."""
+    name = next((k for k in ("extend", "bounce", "path") if k in roof["stages"]), None)
+    if name is None:
         return None
-    out = {"kernel": "wf_extend" if "extend" in roof["stages"] else "nh_path_kernel",
+    e = roof["stages"][name]
+    out = {"kernel": {"extend": "wf_extend", "bounce": "wf_bounce", "path": "nh_path_kernel"}[name],
            "hbm_gbs": e["hbm_gbs"], "frac_of_hbm_peak": round(e["hbm_gbs"] / HBM_PEAK_GBS, 4),
            "avg_launch_ms": e["avg_launch_ms"]}
     if "work_gbs" in e:
         out["work_gbs"] = e["work_gbs"]
-        out["note"] = ("BVH staged in LDS: hbm_gbs is the ray/hit queue stream; work_gbs the algorithmic traversal "
-                       "rate (LDS reads)")
+        out["note"] = ("BVH staged in LDS: hbm_gbs is the HBM stream of that kernel (ray/hit queues, or the path state "
+                       "of the fused bounce kernel); work_gbs adds the algorithmic traversal bytes read from LDS")
     return out
 
 

@@ -246,6 +246,9 @@ typedef struct nh_render_stats {
     /* 1 when the last wavefront render traversed an LDS copy of the BVH (scenes of a few KB): its node
        and primitive reads then come from LDS, not HBM */
     uint64_t lds_scene;
+    /* 1 when the last wavefront render ran one fused bounce kernel per bounce (shade + any-hit +
+       closest-hit, LDS-staged BVHs): its time is in kernel_ms_shade, extend/shadow times are 0 */
+    uint64_t fused_bounce;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;

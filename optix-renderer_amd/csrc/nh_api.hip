@@ -64,6 +64,7 @@ struct WfPool {
     WfJob job{};
     WfLaunch L{};
     bool persistent = false, wide = false, tail = false, draining = false;
+    bool fused = false, sorted = false;  // one wf_bounce kernel per bounce (LDS-staged BVH); material-sorted queue
     int64_t tail_at = 0, drain_at = 0;
     int it = 0;
     std::vector<uint64_t> in_e, in_s;  // live paths / shadow rays entering each bounce
@@ -88,6 +89,8 @@ struct nh_ctx {
     int depth_wide = 0;  // stack bound of the 4-wide traversal
     int n_node_f4 = 0, n_leaves = 0, n_prim_f4 = 0;  // GPU BVH sizes (float4 / int2 entries)
     std::vector<uint32_t> bvh_indices, shape_offset;
+    std::vector<int> shape_bsdf_type;  // BSDF type of each shape (material key of the sorted queues)
+    int n_bsdf_types = 0;              // distinct BSDF types in the scene
     float *fb = nullptr;
     size_t fb_floats = 0;
     float4 *rec = nullptr;
@@ -345,6 +348,14 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     std::memcpy(S.table, d->filter.table, sizeof(S.table));
 
     c->shapes.assign(d->shapes, d->shapes + d->n_shapes);
+    c->shape_bsdf_type.clear();
+    unsigned types = 0;
+    for (uint32_t i = 0; i < d->n_shapes; ++i) {
+        const int t = d->bsdfs[d->shapes[i].bsdf].type & 3;
+        c->shape_bsdf_type.push_back(t);
+        types |= 1u << t;
+    }
+    c->n_bsdf_types = __builtin_popcount(types);
     c->V.assign(d->V, d->V + 3 * nv);
     c->F.assign(d->F, d->F + 3 * (size_t)d->n_faces);
     c->width = d->camera.width;
@@ -516,11 +527,15 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
         std::memcpy(&fs, &si, 4);
         std::memcpy(&f1, &one, 4);
         std::memcpy(&f0, &zero, 4);
+        const int mat = c->shape_bsdf_type[s] << nhd::kPrimMatShift;
         if (sh.type == NH_SHAPE_SPHERE) {
+            const int flags = 1 | mat;
+            std::memcpy(&f1, &flags, 4);
             p[0] = make_float4(sh.center[0], sh.center[1], sh.center[2], sh.radius);
             p[1] = make_float4(0, 0, 0, fs);
             p[2] = make_float4(0, 0, 0, f1);
         } else {
+            std::memcpy(&f0, &mat, 4);
             const uint32_t *f = &c->F[3 * ((size_t)sh.f_offset + local)];
             const float *p0 = &c->V[3 * ((size_t)sh.v_offset + f[0])], *p1 = &c->V[3 * ((size_t)sh.v_offset + f[1])],
                         *p2 = &c->V[3 * ((size_t)sh.v_offset + f[2])];
@@ -789,6 +804,13 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
         HIP_TRY(c, hipMalloc(&p.spill, (size_t)kPersistentBlocks * 128 * spill_words * sizeof(uint32_t)));
         p.spill_words = spill_words;
     }
+    // BVHs staged in LDS: one fused bounce kernel instead of extend + any-hit + shade, its output queue
+    // sorted by the next hit's BSDF type when the scene mixes BSDF types
+    p.fused = small && !p.persistent && c->depth <= 16;
+    if (const char *e = std::getenv("NH_FUSED")) p.fused = p.fused && e[0] != '0';
+    p.sorted = p.fused && c->n_bsdf_types > 1;
+    if (const char *e = std::getenv("NH_SORT")) p.sorted = p.fused && e[0] == '1';
+    c->stats.fused_bounce = p.fused ? 1 : 0;
     c->stats.node_bytes = p.wide ? 16 * nhd::kWideF4 : 64;
     c->stats.lds_scene = small && !p.persistent && c->depth <= 16 ? 1 : 0;  // the SMALL instantiations (DEPTH 16)
     L.trav_spill = p.spill;
@@ -836,6 +858,28 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
     const bool ordered = p.job.ordered, stats = p.job.stats;
     HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), p.stream));
     HIP_TRY(c, hipEventRecord(ev[0], p.stream));
+    if (p.fused) {  // one kernel per bounce: its input already carries the hits (and no pending light samples)
+        HIP_TRY(c, hipEventRecord(ev[1], p.stream));
+        HIP_TRY(c, hipEventRecord(ev[2], p.stream));
+        if (it > 0 && (int64_t)bound <= p.tail_at) {
+            nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, false, bound, c->depth, p.stream);
+            HIP_TRY(c, hipGetLastError());
+            HIP_TRY(c, hipEventRecord(ev[3], p.stream));
+            p.tail = true;
+            p.draining = true;
+            p.state = WfPool::SPLAT;
+            return NH_OK;
+        }
+        nh::launch_wf_bounce(c->d_scene, c->tv, L, ordered, stats, p.sorted, bound, p.stream);
+        HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipEventRecord(ev[3], p.stream));
+        unsigned *h = p.h_counts + (size_t)(it % kRing) * 2 * kCountGroup;
+        HIP_TRY(c, hipMemcpyAsync(h, slot[in ^ 1], 2 * kCountGroup * sizeof(unsigned), hipMemcpyDeviceToHost, p.stream));
+        HIP_TRY(c, hipEventRecord(p.copy_ev[it % kRing], p.stream));
+        if (it == 0) p.it = 1;
+        else p.state = WfPool::COUNTS;
+        return NH_OK;
+    }
     nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, p.persistent, p.wide, bound, c->depth, p.stream);
     HIP_TRY(c, hipEventRecord(ev[1], p.stream));
     // bounce 0 has no shadow rays (the launch still runs: the kernels read the count on the device)
@@ -956,8 +1000,13 @@ static int pool_finish(nh_ctx *c, WfPool &p) {
         // rng 8 B) + hit in, the occlusion byte of a queued light sample (its 16-B pending term is
         // read only when unoccluded, not counted); out: survivors' state, the pending term + shadow
         // ray of each queued light sample, the radiance of each finished path
-        const uint64_t loads = b == 0 ? shaded * (16 + 20) : shaded * (72 + 16) + nsh * 1;
         c->stats.paths_shaded += shaded;
+        if (p.fused) {  // wf_bounce: state + hit in (none at bounce 0), survivors' state + hit out, records
+            const uint64_t loads = b == 0 ? 0 : shaded * (72 + 16);
+            c->stats.shade_state_bytes += loads + (b == 0 ? shaded * 20 : 0) + ne * (72 + 16) + (shaded - ne) * 12;
+            continue;
+        }
+        const uint64_t loads = b == 0 ? shaded * (16 + 20) : shaded * (72 + 16) + nsh * 1;
         c->stats.shade_state_bytes += loads + ne * 72 + ns * (16 + 36) + (shaded - ne) * 12;
         c->stats.extend_queue_bytes += shaded * (b == 0 ? 16 : 48);
         c->stats.shadow_queue_bytes += nsh * 37;  // ray in, path slot, occlusion byte out
@@ -1102,6 +1151,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     if (rc) return rc;
     c->stats.node_bytes = 64;  // binary tree unless a wavefront pool picks the 4-wide one
     c->stats.lds_scene = 0;
+    c->stats.fused_bounce = 0;
     if (q->clear) {
         HIP_TRY(c, hipMemsetAsync(c->fb, 0, c->fb_floats * sizeof(float), c->stream));
         HIP_TRY(c, hipEventRecord(c->fb_ev, c->stream));  // pools' splats wait for it

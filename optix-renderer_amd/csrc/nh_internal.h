@@ -120,6 +120,9 @@ namespace nh {
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                      bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st);
 void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, int bound, hipStream_t st);
+// fused shade + any-hit + closest-hit bounce for LDS-staged BVHs; sort = material-sorted output queue
+void launch_wf_bounce(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
+                      bool sort, int bound, hipStream_t st);
 void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                     bool wide, int bound, int depth, hipStream_t st);
 }  // namespace nh

@@ -144,9 +144,11 @@ struct Traversal {
     const float4 *wnodes;  // 4-wide collapse of the same tree (kWideF4 float4 per node), see Tracer4
 };
 
-// primitive record type / leaf-end bits (word 2 .w of the record)
-constexpr int kPrimSphere = 1, kPrimLeafEnd = 2;
+// primitive record type / leaf-end bits (word 2 .w of the record), and the BSDF type of the owning
+// shape in bits 2-3 (the material key of the sorted shade queues)
+constexpr int kPrimSphere = 1, kPrimLeafEnd = 2, kPrimMatShift = 2;
 NHD bool prim_is_tri(float4 c) { return (__float_as_int(c.w) & kPrimSphere) == 0; }
+NHD int prim_material(float4 c) { return (__float_as_int(c.w) >> kPrimMatShift) & 3; }
 
 // Test the primitives of one leaf. Returns true when an any-hit query is answered.
 template <bool ANY, bool STATS>

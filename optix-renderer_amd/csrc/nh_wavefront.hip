@@ -373,8 +373,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
 // next state in o); sets nee when it sampled a light (shadow ray in so/sd). A terminated path
 // writes its radiance to its sample record.
 __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv, const WfLaunch &L, const WfBuf &B,
-                                           int s, PState &o, bool &nee, float4 &so, float4 &sd) {
-    const float4 hv = B.hit[s];
+                                           int s, const float4 hv, PState &o, bool &nee, float4 &so, float4 &sd) {
     float4 ro, rd, li4, th4;
     int flags, pid;
     Rng rng;
@@ -573,7 +572,11 @@ __global__ __launch_bounds__(256, NH_SHADE_WAVES) void wf_shade(const DScene *__
     bool cont = false, nee = false;
     PState o;
     float4 so, sd;
-    if (q < qv.n) cont = shade_path(S, tv, L, L.st.buf[L.in_q], queue_slot(qv.pre, L.seg_cap, q), o, nee, so, sd);
+    if (q < qv.n) {
+        const WfBuf &B = L.st.buf[L.in_q];
+        const int s = queue_slot(qv.pre, L.seg_cap, q);
+        cont = shade_path(S, tv, L, B, s, B.hit[s], o, nee, so, sd);
+    }
     const int le = wave_append(&s_n[0], cont);
     const int ls = wave_append(&s_n[1], cont && nee);
     __syncthreads();
@@ -591,6 +594,124 @@ __global__ __launch_bounds__(256, NH_SHADE_WAVES) void wf_shade(const DScene *__
             L.st.sh_d[ss] = sd;
             L.st.sh_slot[ss] = slot;
         }
+    }
+}
+
+// Fused bounce for BVHs staged in LDS (the Cornell-box configurations, < 16 KB of nodes and
+// primitives): traversal there is ALU work on an LDS copy, so extend / any-hit / shade as three
+// kernels only add queue round trips through HBM and two launches per bounce. One thread per live
+// path runs the bounce end to end -- shade (shade_path), the any-hit query of the light sample it
+// queued, the closest hit of the next ray -- and stores the path state with that hit. The same
+// operations on the same values as the split kernels: the unoccluded light term is added to Li
+// where the next shade would have added it (before that bounce's emitter term), so the image is
+// bit-identical.
+//
+// Material-sorted queue: survivors are ranked within the workgroup by the BSDF type of their next
+// hit (kPrimMatShift bits of the primitive record; misses last), so the next bounce's waves shade
+// runs of one material instead of interleaving the diffuse, mirror, dielectric and microfacet
+// code paths lane by lane (SURVEY.md north star: material-sorted shade queues).
+constexpr int kMatClasses = 5;  // 4 BSDF types + rays that leave the scene
+#ifndef NH_BOUNCE_WAVES
+#define NH_BOUNCE_WAVES 4
+#endif
+template <bool ORDERED, bool STATS, bool SORT>
+__global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce(const DScene *__restrict__ Sp, Traversal tv_g,
+                                                                  WfLaunch L) {
+    __shared__ uint32_t stk[16 * 256];
+    __shared__ unsigned s_n[kMatClasses], s_off[kMatClasses], s_base;
+    extern __shared__ float4 lds_scene[];
+    const DScene &S = *Sp;
+    const QView qv = queue_view(L.cnt_in);
+    const int base = blockIdx.x * 256;
+    if (base >= qv.n) return;  // whole workgroup
+    if (threadIdx.x < kMatClasses) s_n[threadIdx.x] = 0u;  // visible after the staging barrier
+    const Traversal tv = stage_small_scene(tv_g, L, lds_scene);
+    // gridDim.x is a multiple of kQueueShards: shard s receives the chunks c = s (mod 8), at most
+    // seg_cap entries (as wf_shade)
+    const int shard = blockIdx.x & (kQueueShards - 1);
+    const int q = base + (int)threadIdx.x;
+    const WfBuf &B = L.st.buf[L.in_q];
+    uint32_t *my_stk = stk + threadIdx.x;
+    TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
+    unsigned long long q_e = 0, q_s = 0;
+    bool cont = false;
+    PState o;
+    float4 hit_out = make_float4(0.f, 0.f, 0.f, 0.f);
+    int cls = kMatClasses - 1;
+    if (q < qv.n) {
+        const int s = queue_slot(qv.pre, L.seg_cap, q);
+        float4 hv;
+        if (L.first) {  // the camera ray's closest hit (wf_extend at bounce 0)
+            float4 ro, rd;
+            load_ray(S, L, B, q, s, ro, rd);
+            Hit h;
+            const bool live = rd.w >= ro.w;
+            q_e += live ? 1 : 0;
+            const bool found = live && trace<16, ORDERED, false, STATS>(tv, S, xyz(ro), xyz(rd), ro.w, rd.w, h,
+                                                                        my_stk, 256, st_e);
+            hv = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
+        } else {
+            hv = B.hit[s];
+        }
+        bool nee = false;
+        float4 so, sd;
+        cont = shade_path(S, tv, L, B, s, hv, o, nee, so, sd);
+        if (cont) {
+            if (nee) {  // the light sample's any-hit query (wf_shadow), its outcome applied as shade_path would
+                Hit hs;
+                ++q_s;
+                if (!trace<16, ORDERED, true, STATS>(tv, S, xyz(so), xyz(sd), so.w, sd.w, hs, my_stk, 256, st_s)) {
+                    o.li.x = o.li.x + o.pe.x;
+                    o.li.y = o.li.y + o.pe.y;
+                    o.li.z = o.li.z + o.pe.z;
+                    o.thr.w = o.pe.w;
+                } else if (o.flags & F_ZNAN) {
+                    o.li.x = o.li.x + NAN;
+                    o.li.y = o.li.y + NAN;
+                    o.li.z = o.li.z + NAN;
+                }
+                o.flags &= ~(F_NEE | F_ZNAN);
+            }
+            Hit h;  // the next ray's closest hit (wf_extend)
+            const bool live = o.rd.w >= o.ro.w;
+            q_e += live ? 1 : 0;
+            const bool found = live && trace<16, ORDERED, false, STATS>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h,
+                                                                        my_stk, 256, st_e);
+            hit_out = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
+            if (found) cls = prim_material(tv.prims[3 * h.k + 2]);
+        }
+    }
+    // rank survivors: by material class (sorted queue) or in lane order
+    int rank = 0;
+    if (SORT) {
+#pragma unroll
+        for (int c = 0; c < kMatClasses; ++c) {
+            const int r = wave_append(&s_n[c], cont && cls == c);
+            if (cls == c) rank = r;
+        }
+    } else {
+        cls = 0;
+        rank = wave_append(&s_n[0], cont);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned tot = 0;
+        for (int c = 0; c < kMatClasses; ++c) {
+            s_off[c] = tot;
+            tot += s_n[c];
+        }
+        s_base = tot ? atomicAdd(&L.cnt_out[shard * kCountStride], tot) : 0u;
+    }
+    __syncthreads();
+    if (cont) {
+        const WfBuf &Bo = L.st.buf[1 - L.in_q];
+        const int slot = shard * L.seg_cap + (int)(s_base + s_off[cls]) + rank;
+        store_state(Bo, slot, o);
+        Bo.hit[slot] = hit_out;
+    }
+    if (STATS) {
+        flush_trav_stats(stat_shard(L.counters), q_e, st_e);
+        flush_trav_stats(stat_shard(L.counters) + kStatAny, q_s, st_s);
     }
 }
 
@@ -615,7 +736,7 @@ __global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Tr
             PState o;
             bool nee = false;
             float4 so, sd;
-            if (!shade_path(S, tv, L, B, s, o, nee, so, sd)) break;
+            if (!shade_path(S, tv, L, B, s, B.hit[s], o, nee, so, sd)) break;
             store_state(B, s, o);
             Hit h;
             const bool live = o.rd.w >= o.ro.w;
@@ -731,6 +852,22 @@ void launch_wf_tail(const DScene *S, const Traversal &tv, const WfLaunch &L, boo
     else launch_wf_tail_d<128>(S, tv, L, ordered, stats, wide, bound, st);
 }
 
+
+void launch_wf_bounce(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
+                      int bound, hipStream_t st) {
+    int blocks = std::max(1, (bound + 255) / 256);
+    blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
+    const size_t lds = 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves;
+#define NH_FB(O, T, SO) hipLaunchKernelGGL((wf_bounce<O, T, SO>), dim3(blocks), dim3(256), lds, st, S, tv, L)
+    if (ordered) {
+        if (stats) { if (sort) NH_FB(true, true, true); else NH_FB(true, true, false); }
+        else { if (sort) NH_FB(true, false, true); else NH_FB(true, false, false); }
+    } else {
+        if (stats) { if (sort) NH_FB(false, true, true); else NH_FB(false, true, false); }
+        else { if (sort) NH_FB(false, false, true); else NH_FB(false, false, false); }
+    }
+#undef NH_FB
+}
 
 void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, int bound, hipStream_t st) {
     // one 256-entry chunk per workgroup up to the bound; a multiple of kQueueShards (see wf_shade)

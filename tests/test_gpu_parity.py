@@ -257,7 +257,8 @@ def test_render_parity_envmap(gpu, tmp_path, texture, integrator, mode):
 
 
 @pytest.mark.parametrize("knob", ["NH_PERSISTENT=1", "NH_PERSISTENT=1,NH_WIDE=0", "NH_PERSISTENT=0",
-                                  "NH_LDS_SCENE=0", "NH_TAIL=0", "NH_TAIL=1000000", "NH_PERSISTENT=1,NH_TAIL=1000000"])
+                                  "NH_LDS_SCENE=0", "NH_TAIL=0", "NH_TAIL=1000000", "NH_PERSISTENT=1,NH_TAIL=1000000",
+                                  "NH_FUSED=0", "NH_SORT=0", "NH_SORT=1", "NH_FUSED=1,NH_TAIL=0"])
 def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
     """The traversal variants the wavefront picks per scene (persistent ray-fetching traversal for
     deep BVHs over the binary or the 4-wide tree, per-lane traversal, LDS-staged small BVHs) all give
@@ -281,6 +282,8 @@ def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
         np.testing.assert_array_equal(ref.framebuffer(), ctx.framebuffer())
         wide = ctx.stats()["node_bytes"] == 128
         env = dict(knobs)
+        small = b.desc.max_depth + 2 <= 16 and env.get("NH_LDS_SCENE") != "0" and env.get("NH_PERSISTENT") != "1"
+        assert ctx.stats()["fused_bounce"] == int(small and env.get("NH_FUSED") != "0"), xml
         persistent = env["NH_PERSISTENT"] == "1" if "NH_PERSISTENT" in env else b.desc.max_depth + 2 > 20
         assert wide == (persistent and env.get("NH_WIDE") != "0"), xml
         for k in ("ray_queries",) if wide else ("ray_queries", "nodes_visited", "prims_tested"):
