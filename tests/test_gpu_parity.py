@@ -282,8 +282,10 @@ def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
         np.testing.assert_array_equal(ref.framebuffer(), ctx.framebuffer())
         wide = ctx.stats()["node_bytes"] == 128
         env = dict(knobs)
-        small = b.desc.max_depth + 2 <= 16 and env.get("NH_LDS_SCENE") != "0" and env.get("NH_PERSISTENT") != "1"
-        assert ctx.stats()["fused_bounce"] == int(small and env.get("NH_FUSED") != "0"), xml
+        # the fused bounce kernel runs exactly when the BVH is traversed from LDS, unless NH_FUSED=0
+        assert ctx.stats()["fused_bounce"] == int(ctx.stats()["lds_scene"] == 1 and env.get("NH_FUSED") != "0"), xml
+        if "cbox" in xml and not any(k in env for k in ("NH_LDS_SCENE", "NH_PERSISTENT")):
+            assert ctx.stats()["lds_scene"] == 1
         persistent = env["NH_PERSISTENT"] == "1" if "NH_PERSISTENT" in env else b.desc.max_depth + 2 > 20
         assert wide == (persistent and env.get("NH_WIDE") != "0"), xml
         for k in ("ray_queries",) if wide else ("ray_queries", "nodes_visited", "prims_tested"):
