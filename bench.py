@@ -65,8 +65,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-calibrate", action="store_true")
-    p.add_argument("--pools", type=int, default=2,
-                   help="wavefront path pools in flight (2: a chunk's last bounces overlap the next chunk)")
+    p.add_argument("--pools", type=int, default=0,
+                   help="wavefront path pools in flight (0: the library default; >1: a chunk's last bounces overlap "
+                        "the next chunks)")
     p.add_argument("--roofline-steps", type=int, default=4,
                    help="with --pools > 1: steps of the serialized pass that times the kernels for the roofline")
     p.add_argument("--seed", type=int, default=1234)
@@ -297,7 +298,8 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
         R = a.rounds  # every rank renders the whole sample budget of its 1/N of the blocks
     else:
         R = a.rounds * world  # each rank's 1/N of the image for N x --rounds rounds (weak scaling)
-    os.environ["NH_POOLS"] = str(a.pools)
+    if a.pools:
+        os.environ["NH_POOLS"] = str(a.pools)
     calib = None
     if not a.no_calibrate:
         ctx.reset_stats()
@@ -323,7 +325,8 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
         elapsed = max_over_ranks(elapsed, dist, args, local)
     st = ctx.stats()
     roof_pass = None
-    if a.mode == "wavefront" and a.pools > 1 and calib is not None and a.roofline_steps > 0:
+    if a.mode == "wavefront" and a.pools != 1 and calib is not None and a.roofline_steps > 0:
+        pools_env = os.environ.get("NH_POOLS")
         # Kernels of overlapping pools share the GPU, so their event durations are no kernel roofline:
         # time the kernels in a serialized pass (one pool) over the same workload instead.
         os.environ["NH_POOLS"] = "1"
@@ -334,7 +337,10 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
         ctx.synchronize()
         st = ctx.stats()
         roof_pass = f"serialized pass: {a.roofline_steps} steps with one path pool (kernels alone on the GPU)"
-        os.environ["NH_POOLS"] = str(a.pools)
+        if pools_env is None:
+            del os.environ["NH_POOLS"]
+        else:
+            os.environ["NH_POOLS"] = pools_env
     # every rank renders its 1/N of the blocks: the whole job is W x H x R samples per step
     samples = W * H * R * steps
     roof = None
@@ -441,7 +447,8 @@ def main():
             "data": "synthetic (reference Cornell box scene files, generated meshes, per-path pcg32 seeds)",
             "config": {"workload": f"{r['desc']}, {spp} spp, path_mis", "config": args.config,
                        "width": W, "height": H, "spp": spp, "rounds_per_step": R,
-                       "mode": args.mode, "traversal": args.traversal, "pools": args.pools,
+                       "mode": args.mode, "traversal": args.traversal,
+                       "pools": args.pools or int(os.environ.get("NH_POOLS", "0")) or "library default (4)",
                        "parallelism": (f"{par} + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce"
                                        if world > 1 else "single GPU"),
                        "bvh_build_s": round(r["bvh_s"], 3), "upload_s": round(r["upload_s"], 3)},

@@ -30,7 +30,12 @@ using nhd::DShape;
 
 // ---- wavefront pipeline state (used by nh_render, see the pipeline section below) ----
 constexpr int kRing = 4;   // bounce-count copies in flight per pool
-constexpr int kPools = 2;  // path pools in flight: one drains its last bounces while the next fills the GPU
+// path pools in flight: while one drains its last bounces (long specular chains are a latency chain of
+// hundreds of bounces) the next ones fill the GPU; NH_POOLS=1..kPools overrides the default
+constexpr int kPools = 4;
+#ifndef NH_DEFAULT_POOLS
+#define NH_DEFAULT_POOLS 4
+#endif
 constexpr int kMaxStack = 128;  // deepest per-lane LDS stack of the binary-tree kernels (DEPTH template)
 
 // one chunk of sample rounds of one nh_render call
@@ -1029,7 +1034,7 @@ static void pipeline_reset(nh_ctx *c) {
 // submitted chunk has started and every busy pool is draining.
 static int pipeline_run(nh_ctx *c, bool all) {
     const char *np = std::getenv("NH_POOLS");  // 1 = no overlap (A/B and tests)
-    const int n_pools = np ? std::max(1, std::min(kPools, std::atoi(np))) : kPools;
+    const int n_pools = std::max(1, std::min(kPools, np ? std::atoi(np) : NH_DEFAULT_POOLS));
     for (;;) {
         bool progress = false;
         for (WfPool &p : c->pools) {

@@ -284,7 +284,7 @@ def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
         env = dict(knobs)
         # the fused bounce kernel runs exactly when the BVH is traversed from LDS, unless NH_FUSED=0
         assert ctx.stats()["fused_bounce"] == int(ctx.stats()["lds_scene"] == 1 and env.get("NH_FUSED") != "0"), xml
-        if "cbox" in xml and not any(k in env for k in ("NH_LDS_SCENE", "NH_PERSISTENT")):
+        if s.desc.n_faces < 100 and not any(k in env for k in ("NH_LDS_SCENE", "NH_PERSISTENT")):  # the Cornell box
             assert ctx.stats()["lds_scene"] == 1
         persistent = env["NH_PERSISTENT"] == "1" if "NH_PERSISTENT" in env else b.desc.max_depth + 2 > 20
         assert wide == (persistent and env.get("NH_WIDE") != "0"), xml
