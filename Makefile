@@ -32,7 +32,14 @@ HOSTLIB  := $(LIBDIR)/libnori_host.so
 ORACLE   := oracle/_build/libnori_oracle.so
 CLI      := $(LIBDIR)/nori_hip
 
-all: $(LIB) $(HOSTLIB) $(ORACLE) $(CLI)
+RCPCHECK := tools/bin/rcp_exhaustive
+
+all: $(LIB) $(HOSTLIB) $(ORACLE) $(CLI) $(RCPCHECK)
+
+# exhaustive check of the fast reciprocal the traversal kernels use (run by the GPU tests)
+$(RCPCHECK): tools/rcp_exhaustive.hip $(HIP_DEPS)
+	@mkdir -p tools/bin
+	$(HIPCC) $(HIP_FLAGS) -o $@ $<
 
 $(OBJDIR)/host_%.o: $(PKG)/host/%.cpp $(wildcard $(PKG)/host/*.h) include/nori_hip.h
 	@mkdir -p $(OBJDIR)

@@ -972,6 +972,19 @@ static int pool_finish(nh_ctx *c, WfPool &p) {
         p.in_e.push_back(ne);
         p.in_s.push_back(ns);
     }
+    static const bool trace_counts = std::getenv("NH_TRACE_COUNTS") != nullptr;  // diagnostics: per-bounce profile
+    if (trace_counts) {
+        float t_all = 0.f;
+        (void)hipEventElapsedTime(&t_all, p.ev_begin, p.ev_path);
+        std::fprintf(stderr, "[nh] chunk seq %llu: %d paths, %d bounces%s, %.3f ms, live/bounce(ms):",
+                     (unsigned long long)p.job.seq, p.L.n_paths, p.it + 1, p.tail ? " (last = tail kernel)" : "", t_all);
+        for (int b = 0; b <= p.it && b < (int)p.in_e.size(); ++b) {
+            float d = 0.f;
+            (void)hipEventElapsedTime(&d, p.events[(size_t)b * 4], p.events[(size_t)b * 4 + 3]);
+            std::fprintf(stderr, " %llu(%.3f)", (unsigned long long)p.in_e[b], d);
+        }
+        std::fprintf(stderr, "\n");
+    }
     for (int b = 0; b <= p.it; ++b) {
         hipEvent_t *ev = &p.events[(size_t)b * 4];
         float a = 0.f, sh = 0.f, d = 0.f;

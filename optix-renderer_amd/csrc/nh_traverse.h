@@ -71,13 +71,30 @@ NHD bool box_test(float mnx, float mny, float mnz, float mxx, float mxy, float m
     return mint <= far_t && near_t <= maxt;
 }
 
+// Correctly rounded 1/x (what `1.0f / x` gives) in 3 instructions: the hardware estimate (within 1 ulp)
+// and one FMA Newton step. Checked against the correctly rounded division for all 2^32 inputs on gfx950
+// (tools/rcp_exhaustive.hip, tests/test_gpu_parity.py::test_fast_reciprocal_exhaustive): identical for
+// |x| in [2^-125, 2^126); outside that range the caller must use the division.
+NHD float rcp_rn(float x) {
+    const float r = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+}
+// 1/det of Mesh::rayIntersect: every det the test does not reject (|det| >= 1e-8 or NaN) takes rcp_rn
+// unless it is >= 2^126 in magnitude (then the division); rejected dets may get any value
+NHD float tri_inv_det(float det) {
+    float r = rcp_rn(det);
+    if (__builtin_expect(fabsf(det) >= 0x1p126f, 0)) r = 1.0f / det;
+    return r;
+}
+
 // Mesh::rayIntersect (mesh.cpp:101-139): edges from the vertices, as the reference computes them
 NHD bool tri_test(float4 a, float4 b, float4 c, F3 o, F3 d, float mint, float maxt, float &t, float &u, float &v) {
     const F3 p0 = f3(a.x, a.y, a.z), e1 = sub(f3(b.x, b.y, b.z), p0), e2 = sub(f3(c.x, c.y, c.z), p0);
     F3 pvec = cross(d, e2);
     float det = dot(e1, pvec);
     if (det > -1e-8f && det < 1e-8f) return false;
-    float inv_det = 1.0f / det;
+    float inv_det = tri_inv_det(det);
     F3 tvec = sub(o, p0);
     u = dot(tvec, pvec) * inv_det;
     if (u < 0.0f || u > 1.0f) return false;
@@ -88,6 +105,40 @@ NHD bool tri_test(float4 a, float4 b, float4 c, F3 o, F3 d, float mint, float ma
     return t >= mint && t <= maxt;
 }
 
+// Two Moller-Trumbore tests at once, one per component of packed-FP32 pairs (v_pk_mul_f32 /
+// v_pk_add_f32: each component is the IEEE single-precision result of the same operation, so the
+// pair computes exactly what two tri_test_nb calls compute, in half the VALU issue slots). Returns
+// the hit predicates without the maxt bound (t_ok: t >= mint; the caller applies t <= maxt in
+// primitive order, since a hit of the first shrinks maxt for the second).
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct P3 {
+    f2 x, y, z;
+};
+NHD P3 psub(P3 a, P3 b) { return P3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+NHD P3 pcross(P3 a, P3 b) { return P3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+NHD f2 pdot(P3 a, P3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
+NHD void tri_test_pair(float4 a0, float4 b0, float4 c0, float4 a1, float4 b1, float4 c1, F3 o, F3 d, float mint,
+                       f2 &t, f2 &u, f2 &v, bool &ok0, bool &ok1) {
+    const P3 p0{f2{a0.x, a1.x}, f2{a0.y, a1.y}, f2{a0.z, a1.z}};
+    const P3 p1{f2{b0.x, b1.x}, f2{b0.y, b1.y}, f2{b0.z, b1.z}};
+    const P3 p2{f2{c0.x, c1.x}, f2{c0.y, c1.y}, f2{c0.z, c1.z}};
+    const P3 po{f2{o.x, o.x}, f2{o.y, o.y}, f2{o.z, o.z}}, pd{f2{d.x, d.x}, f2{d.y, d.y}, f2{d.z, d.z}};
+    const P3 e1 = psub(p1, p0), e2 = psub(p2, p0);
+    const P3 pvec = pcross(pd, e2);
+    const f2 det = pdot(e1, pvec);
+    const f2 inv_det = f2{tri_inv_det(det.x), tri_inv_det(det.y)};
+    const P3 tvec = psub(po, p0);
+    u = pdot(tvec, pvec) * inv_det;
+    const P3 qvec = pcross(tvec, e1);
+    v = pdot(pd, qvec) * inv_det;
+    t = pdot(e2, qvec) * inv_det;
+    const f2 uv = u + v;
+    ok0 = !(det.x > -1e-8f && det.x < 1e-8f) & !(u.x < 0.0f || u.x > 1.0f) & !(v.x < 0.0f || uv.x > 1.0f) &
+          (t.x >= mint);
+    ok1 = !(det.y > -1e-8f && det.y < 1e-8f) & !(u.y < 0.0f || u.y > 1.0f) & !(v.y < 0.0f || uv.y > 1.0f) &
+          (t.y >= mint);
+}
+
 // tri_test without early exits: the same predicates on the same values (so the same answer, NaNs
 // included), evaluated in full. In SIMT code an early return only skips work when every lane of
 // the wave takes it; otherwise it costs a branch and exec-mask bookkeeping per test.
@@ -95,7 +146,7 @@ NHD bool tri_test_nb(float4 a, float4 b, float4 c, F3 o, F3 d, float mint, float
     const F3 p0 = f3(a.x, a.y, a.z), e1 = sub(f3(b.x, b.y, b.z), p0), e2 = sub(f3(c.x, c.y, c.z), p0);
     const F3 pvec = cross(d, e2);
     const float det = dot(e1, pvec);
-    const float inv_det = 1.0f / det;
+    const float inv_det = tri_inv_det(det);
     const F3 tvec = sub(o, p0);
     u = dot(tvec, pvec) * inv_det;
     const F3 qvec = cross(tvec, e1);
@@ -155,21 +206,38 @@ template <bool ANY, bool STATS>
 NHD bool leaf_test(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float &maxt, Hit &best, bool &found,
                    TravStats &st) {
     const int2 lf = tv.leaves[leaf];
-    for (int k = lf.x, e = lf.x + lf.y; k < e; ++k) {
-        const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
-        if (STATS) st.prims++;
-        float t, u = 0.f, v = 0.f;
-        bool hit = prim_is_tri(c) ? tri_test(a, b, c, o, d, mint, maxt, t, u, v)
-                                              : sphere_test(a, o, d, mint, maxt, t);
-        if (!hit) continue;
-        if (ANY) return true;
-        if (t < maxt || k > best.k) {
-            found = true;
-            maxt = t;
-            best.t = t;
-            best.u = u;
-            best.v = v;
-            best.k = k;
+    // primitives in pairs: both triangle tests in packed FP32 (tri_test_pair), then accepted in
+    // order -- a hit of the first shrinks maxt before the second is bounded by it
+    for (int k = lf.x, e = lf.x + lf.y; k < e; k += 2) {
+        const int k1 = k + 1 < e ? k + 1 : k;
+        const float4 a0 = tv.prims[3 * k], b0 = tv.prims[3 * k + 1], c0 = tv.prims[3 * k + 2];
+        const float4 a1 = tv.prims[3 * k1], b1 = tv.prims[3 * k1 + 1], c1 = tv.prims[3 * k1 + 2];
+        f2 pt, pu, pv;
+        bool ok0, ok1;
+        tri_test_pair(a0, b0, c0, a1, b1, c1, o, d, mint, pt, pu, pv, ok0, ok1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (j == 1 && k1 == k) break;
+            const float4 &a = j ? a1 : a0, &c = j ? c1 : c0;
+            if (STATS) st.prims++;
+            float t = j ? pt.y : pt.x, u = j ? pu.y : pu.x, v = j ? pv.y : pv.x;
+            bool hit;
+            if (prim_is_tri(c)) {
+                hit = (j ? ok1 : ok0) && t <= maxt;
+            } else {
+                u = v = 0.f;
+                hit = sphere_test(a, o, d, mint, maxt, t);
+            }
+            if (!hit) continue;
+            if (ANY) return true;
+            if (t < maxt || k + j > best.k) {
+                found = true;
+                maxt = t;
+                best.t = t;
+                best.u = u;
+                best.v = v;
+                best.k = k + j;
+            }
         }
     }
     return false;
@@ -427,6 +495,10 @@ constexpr int kWideF4 = 8;
 #endif
 
 constexpr int kWideEmpty = (int)0x80000000;
+// the two primitive records of a step tested as a packed pair (tri_test_pair) or one after the other
+#ifndef NH_WIDE_PAIR
+#define NH_WIDE_PAIR 1
+#endif
 
 // Traversal stack of one lane, (ref, entry distance) pairs: the top K entries live in LDS
 // (lane-interleaved, `stride` words apart), deeper entries spill to the lane's own global area.
@@ -598,23 +670,42 @@ struct Tracer4 {
                 enter((v0 && !rk0) ? ref.x : (v1 && !rk1) ? ref.y : (v2 && !rk2) ? ref.z : ref.w);
             }
         }
-        if (k >= 0) {  // up to two primitives of the current leaf, both records fetched at once
+        if (k >= 0) {  // up to two primitives of the current leaf: records fetched together, tested as a pair
             const float4 a0 = tv.prims[3 * k], b0 = tv.prims[3 * k + 1], c0 = tv.prims[3 * k + 2];
             const float4 a1 = tv.prims[3 * k + 3], b1 = tv.prims[3 * k + 4], c1 = tv.prims[3 * k + 5];
-            if (prim(a0, b0, c0, st)) return;
+#if NH_WIDE_PAIR
+            f2 pt, pu, pv;
+            bool ok0, ok1;
+            tri_test_pair(a0, b0, c0, a1, b1, c1, o, d, mint, pt, pu, pv, ok0, ok1);
+            if (prim(a0, c0, pt.x, pu.x, pv.x, ok0, st)) return;
             if (k >= 0) {
-                if (prim(a1, b1, c1, st)) return;
+                if (prim(a1, c1, pt.y, pu.y, pv.y, ok1, st)) return;
             }
+#else
+            float t0, u0 = 0.f, v0 = 0.f;
+            const bool ok0 = prim_is_tri(c0) && tri_test_nb(a0, b0, c0, o, d, mint, INFINITY, t0, u0, v0);
+            if (prim(a0, c0, t0, u0, v0, ok0, st)) return;
+            if (k >= 0) {
+                float t1, u1 = 0.f, v1 = 0.f;
+                const bool ok1 = prim_is_tri(c1) && tri_test_nb(a1, b1, c1, o, d, mint, INFINITY, t1, u1, v1);
+                if (prim(a1, c1, t1, u1, v1, ok1, st)) return;
+            }
+#endif
         }
         if (k < 0 && cur < 0 && sp == 0) done = true;
     }
 
-    // test record k (a, b, c) and advance k; true when an any-hit query is answered
-    NHD bool prim(const float4 &a, const float4 &b, const float4 &c, TravStats &st) {
+    // record k (a, c; for a triangle its pair-test results t, u, v, ok) against the current maxt, then
+    // advance k; true when an any-hit query is answered
+    NHD bool prim(const float4 &a, const float4 &c, float t, float u, float v, bool ok, TravStats &st) {
         if (STATS) st.prims++;
-        float t, u = 0.f, v = 0.f;
-        const bool hit = prim_is_tri(c) ? tri_test_nb(a, b, c, o, d, mint, maxt, t, u, v)
-                                        : sphere_test(a, o, d, mint, maxt, t);
+        bool hit;
+        if (prim_is_tri(c)) {
+            hit = ok & (t <= maxt);
+        } else {
+            u = v = 0.f;
+            hit = sphere_test(a, o, d, mint, maxt, t);
+        }
         if (hit) {
             if (ANY) {
                 found = true;

@@ -369,10 +369,42 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
     if (STATS) flush_trav_stats(stat_shard(L.counters) + (ANY ? 8 : 0), queries, st);
 }
 
-// One shade step of the path in slot s of buffer B. Returns whether the path continues (its
-// next state in o); sets nee when it sampled a light (shadow ray in so/sd). A terminated path
-// writes its radiance to its sample record.
-__device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv, const WfLaunch &L, const WfBuf &B,
+// Where shade_path reads a path's state from: slot s of a path buffer (MemState), or the registers
+// of the previous shade step of the same thread (RegState, the tail kernel: no store -> load round
+// trip through memory per bounce on its latency-bound chains). Both hand shade_path the same values.
+struct MemState {
+    const WfBuf &B;
+    int s;
+    __device__ __forceinline__ void load(float4 &ro, float4 &rd, float4 &li, float4 &thr, uint64_t &rng) const {
+        ro = B.ray_o[s];
+        rd = B.ray_d[s];
+        li = B.li[s];
+        thr = B.thr[s];
+        rng = B.rng[s];
+    }
+    __device__ __forceinline__ bool occluded() const { return B.occl[s] != 0; }
+    __device__ __forceinline__ float4 pending() const { return B.pend[s]; }
+};
+struct RegState {
+    const PState &o;
+    bool occl;
+    __device__ __forceinline__ void load(float4 &ro, float4 &rd, float4 &li, float4 &thr, uint64_t &rng) const {
+        ro = make_float4(o.ro.x, o.ro.y, o.ro.z, o.pdfmat);
+        rd = make_float4(o.rd.x, o.rd.y, o.rd.z,
+                         __int_as_float((int)(((unsigned)o.flags << kPidBits) | (unsigned)o.pid)));
+        li = o.li;
+        thr = o.thr;
+        rng = o.rng;
+    }
+    __device__ __forceinline__ bool occluded() const { return occl; }
+    __device__ __forceinline__ float4 pending() const { return o.pe; }
+};
+
+// One shade step of the path whose state src holds (slot s of the input queue), hv = the hit of its
+// ray. Returns whether the path continues (its next state in o); sets nee when it sampled a light
+// (shadow ray in so/sd). A terminated path writes its radiance to its sample record.
+template <class Src>
+__device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv, const WfLaunch &L, const Src &src,
                                            int s, const float4 hv, PState &o, bool &nee, float4 &so, float4 &sd) {
     float4 ro, rd, li4, th4;
     int flags, pid;
@@ -387,14 +419,10 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
         L.rec_rgbx[pid] = make_float4(0.f, 0.f, 0.f, jx);
         L.rec_jy[pid] = jy;
     } else {
-        ro = B.ray_o[s];
-        rd = B.ray_d[s];
-        li4 = B.li[s];
-        th4 = B.thr[s];
+        src.load(ro, rd, li4, th4, rng.state);
         const int bits = __float_as_int(rd.w);
         flags = (int)((unsigned)bits >> kPidBits);
         pid = bits & ((1 << kPidBits) - 1);
-        rng.state = B.rng[s];
         rng.inc = ((uint64_t)(L.s0 + pid / L.n_list) << 1u) | 1u;
     }
     const F3 org = xyz(ro), d = xyz(rd);
@@ -445,8 +473,8 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
             // the light sample counts unless occluded: its MIS-weighted term was computed by that
             // bounce, Li += w_ems * t * Li_ems (:142), and w_ems is the unoccluded weight (:103-106)
             if (flags & F_NEE) {
-                if (!B.occl[s]) {
-                    const float4 pe = B.pend[s];
+                if (!src.occluded()) {
+                    const float4 pe = src.pending();
                     li = add(li, xyz(pe));
                     w_ems = pe.w;
                 } else if (flags & F_ZNAN) {
@@ -575,7 +603,7 @@ __global__ __launch_bounds__(256, NH_SHADE_WAVES) void wf_shade(const DScene *__
     if (q < qv.n) {
         const WfBuf &B = L.st.buf[L.in_q];
         const int s = queue_slot(qv.pre, L.seg_cap, q);
-        cont = shade_path(S, tv, L, B, s, B.hit[s], o, nee, so, sd);
+        cont = shade_path(S, tv, L, MemState{B, s}, s, B.hit[s], o, nee, so, sd);
     }
     const int le = wave_append(&s_n[0], cont);
     const int ls = wave_append(&s_n[1], cont && nee);
@@ -655,7 +683,7 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce(const DScene *
         }
         bool nee = false;
         float4 so, sd;
-        cont = shade_path(S, tv, L, B, s, hv, o, nee, so, sd);
+        cont = shade_path(S, tv, L, MemState{B, s}, s, hv, o, nee, so, sd);
         if (cont) {
             if (nee) {  // the light sample's any-hit query (wf_shadow), its outcome applied as shade_path would
                 Hit hs;
@@ -720,8 +748,11 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce(const DScene *
 // of a bounce whose extend / any-hit traversals are done and finishes every path in place, one
 // thread per path: shade, then its next closest-hit and shadow traversals, until it terminates --
 // the same operations in the same order as further wavefront bounces.
+#ifndef NH_TAIL_WAVES
+#define NH_TAIL_WAVES 1
+#endif
 template <int DEPTH, bool ORDERED, bool STATS, bool SMALL, bool WIDE>
-__global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAVES))) void wf_tail(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
     extern __shared__ float4 lds_scene[];
     const DScene &S = *Sp;
@@ -732,26 +763,28 @@ __global__ __launch_bounds__(128) void wf_tail(const DScene *__restrict__ Sp, Tr
     unsigned long long q_e = 0, q_s = 0;
     for (int q = blockIdx.x * 128 + threadIdx.x; q < qv.n; q += gridDim.x * 128) {
         const int s = queue_slot(qv.pre, L.seg_cap, q);
+        // the first step reads the path from the buffer; later steps take the previous step's state,
+        // hit and occlusion straight from registers (nothing else reads them: the chunk ends here)
+        PState o;
+        bool nee = false, occ = false;
+        float4 so, sd;
+        if (!shade_path(S, tv, L, MemState{B, s}, s, B.hit[s], o, nee, so, sd)) continue;
         for (;;) {
-            PState o;
-            bool nee = false;
-            float4 so, sd;
-            if (!shade_path(S, tv, L, B, s, B.hit[s], o, nee, so, sd)) break;
-            store_state(B, s, o);
             Hit h;
             const bool live = o.rd.w >= o.ro.w;
             q_e += live ? 1 : 0;
             const bool found = live && trace_lane<WIDE, DEPTH, ORDERED, false, STATS>(tv, S, L, xyz(o.ro), xyz(o.rd),
                                                                                       o.ro.w, o.rd.w, h, stk, st_e);
-            B.hit[s] = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
+            const float4 hv = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
+            occ = false;
             if (nee) {
                 ++q_s;
                 Hit hs;
-                B.occl[s] = trace_lane<WIDE, DEPTH, ORDERED, true, STATS>(tv, S, L, xyz(so), xyz(sd), so.w, sd.w, hs,
-                                                                          stk, st_s)
-                                ? 1
-                                : 0;
+                occ = trace_lane<WIDE, DEPTH, ORDERED, true, STATS>(tv, S, L, xyz(so), xyz(sd), so.w, sd.w, hs, stk, st_s);
             }
+            const PState prev = o;
+            nee = false;
+            if (!shade_path(S, tv, L, RegState{prev, occ}, s, hv, o, nee, so, sd)) break;
         }
     }
     if (STATS) {  // the tail's own counter slots (kStatTail*), so stage rates stay per kernel

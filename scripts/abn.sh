@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for i in $(seq 1 $n); do
   for v in $libs; do
     export NH_LIB_PATH=$PWD/optix-renderer_amd/$v/libnori_hip.so
-    timeout -k 10 300 python bench.py --no-cpu --no-calibrate "$@" > gpurun_out/ab_$v.$i.log 2>&1 || { echo "fail $v $i"; tail -3 gpurun_out/ab_$v.$i.log; exit 99; }
+    timeout -k 10 300 python bench.py --no-cpu --no-calibrate --traversal-1m-steps 0 --roofline-steps 0 "$@" > gpurun_out/ab_$v.$i.log 2>&1 || { echo "fail $v $i"; tail -3 gpurun_out/ab_$v.$i.log; exit 99; }
     python3 -c "
 import json
 d=json.loads(open('gpurun_out/ab_$v.$i.log').read().strip().splitlines()[-1])

@@ -319,8 +319,8 @@ def test_framebuffer_device_pointer_wraps_in_torch(gpu, tmp_path):
     # no nh_synchronize: the pointer call itself completes the submitted chunks (the pipeline only
     # advances inside library calls), so a torch-side device sync is enough
     ptr, n = ctx.framebuffer_device_ptr()
-    torch.cuda.synchronize()
     t = bench._wrap_device(ptr, n, 0)
+    torch.cuda.synchronize()
     np.testing.assert_array_equal(t.cpu().numpy(), ctx.framebuffer().reshape(-1))
     orig = ctx.framebuffer().reshape(-1).copy()
     t.mul_(2.0)  # writes through to the context's buffer
@@ -396,3 +396,15 @@ def test_pipelined_chunks_match_one_pool(gpu, tmp_path, monkeypatch):
     np.testing.assert_array_equal(out[0], out[1])
     r = no.OracleScene(s).render(0, 12, seed=9)
     assert rel_l2(out[0], r) < TOL_REL_L2
+
+
+def test_fast_reciprocal_exhaustive(gpu):
+    """nhd::rcp_rn (hardware estimate + one FMA Newton step), which the triangle tests use for 1/det,
+    equals the correctly rounded 1.0f / x for every one of the 2^32 float inputs in the range the
+    kernels use it for (tools/rcp_exhaustive.hip, built by `make`)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "bin", "rcp_exhaustive")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=90)
+    print(r.stdout.strip())
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "in_range_mismatches 0 " in r.stdout
