@@ -296,7 +296,7 @@ __device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S,
 #define NH_REFILL_MIN 32
 #endif
 #ifndef NH_PT_WAVES
-#define NH_PT_WAVES 6
+#define NH_PT_WAVES 5
 #endif
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool WIDE>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES))) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {

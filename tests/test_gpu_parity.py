@@ -305,27 +305,50 @@ def test_render_parity_c5_small(gpu, tmp_path, mode):
     assert e < TOL_REL_L2
 
 
+_TORCH_WRAP = r"""
+import os, sys
+import numpy as np
+import torch                      # first: the library then shares torch's HIP runtime (one per process)
+torch.zeros(1, device="cuda:0")   # torch initialises the device before the library, as bench.py at N > 1
+sys.path[:0] = [os.path.join(sys.argv[1], "optix-renderer_amd"), sys.argv[1]]
+import importlib.util
+import nori_hip as nh
+import scenegen
+spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(sys.argv[1], "bench.py"))
+bench = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(bench)
+s = nh.Scene(scenegen.cbox_xml(sys.argv[2], "c2", width=64, height=48))
+b = nh.Bvh(s)
+ctx = nh.Context(0)
+ctx.upload(s, b)
+ctx.render(0, 4, seed=2, clear=True, mode=nh.MODE_WAVEFRONT, traversal=nh.TRAVERSAL_ORDERED)
+# no nh_synchronize: the pointer call completes the submitted chunks (the pipeline advances only
+# inside library calls), so a torch-side device sync is enough
+ptr, n = ctx.framebuffer_device_ptr()
+t = bench._wrap_device(ptr, n, 0)
+torch.cuda.synchronize()
+host = ctx.framebuffer().reshape(-1)
+assert np.array_equal(t.cpu().numpy(), host)
+t.mul_(2.0)  # writes through to the context's buffer
+torch.cuda.synchronize()
+assert np.array_equal(ctx.framebuffer().reshape(-1), host * np.float32(2.0))
+print("torch-wrap ok", float(host.sum()))
+"""
+
+
 def test_framebuffer_device_pointer_wraps_in_torch(gpu, tmp_path):
     """bench.py hands the device framebuffer to torch.distributed (RCCL) through
-    __cuda_array_interface__; the wrapped tensor must alias the context's framebuffer."""
-    import importlib.util
-    import torch
-    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(
-        os.path.dirname(os.path.abspath(__file__))), "bench.py"))
-    bench = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(bench)
-    s, b, ctx = setup(scenegen.cbox_xml(str(tmp_path), "c2"), 64, 48)
-    ctx.render(0, 4, seed=2, clear=True, mode=nh.MODE_WAVEFRONT)
-    # no nh_synchronize: the pointer call itself completes the submitted chunks (the pipeline only
-    # advances inside library calls), so a torch-side device sync is enough
-    ptr, n = ctx.framebuffer_device_ptr()
-    t = bench._wrap_device(ptr, n, 0)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(t.cpu().numpy(), ctx.framebuffer().reshape(-1))
-    orig = ctx.framebuffer().reshape(-1).copy()
-    t.mul_(2.0)  # writes through to the context's buffer
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(ctx.framebuffer().reshape(-1), orig * np.float32(2.0))
+    __cuda_array_interface__; the wrapped tensor must alias the context's framebuffer. Run in a fresh
+    process that imports and initialises torch first, as bench.py's multi-GPU path does: the library
+    then binds to torch's HIP runtime (two HIP runtimes in one process do not coexist)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "wrap.py"
+    script.write_text(_TORCH_WRAP)
+    r = subprocess.run([sys.executable, str(script), repo, str(tmp_path)], capture_output=True, text=True, timeout=240)
+    print(r.stdout[-2000:], r.stderr[-2000:])
+    assert r.returncode == 0 and "torch-wrap ok" in r.stdout
 
 
 def test_persistent_traversal_deep_tree_spills(gpu, tmp_path, monkeypatch):
