@@ -34,7 +34,16 @@ CLI      := $(LIBDIR)/nori_hip
 
 RCPCHECK := tools/bin/rcp_exhaustive
 
-all: $(LIB) $(HOSTLIB) $(ORACLE) $(CLI) $(RCPCHECK)
+MANUAL   := tests/c/bin/manual_scene
+
+all: $(LIB) $(HOSTLIB) $(ORACLE) $(CLI) $(RCPCHECK) $(MANUAL)
+
+# C test: a scene description filled field by field (no XML loader), rendered through the C-ABI and
+# compared with the oracle (run by tests/test_gpu_parity.py)
+$(MANUAL): tests/c/manual_scene.c $(LIB) $(ORACLE) include/nori_hip.h oracle/nori_oracle.h
+	@mkdir -p tests/c/bin
+	$(CC) -std=c99 -O2 -Wall -Iinclude -Ioracle -o $@ $< -L$(LIBDIR) -lnori_hip -Loracle/_build -lnori_oracle \
+	    -lm -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../../oracle/_build'
 
 # exhaustive check of the fast reciprocal the traversal kernels use (run by the GPU tests)
 $(RCPCHECK): tools/rcp_exhaustive.hip $(HIP_DEPS)

@@ -249,6 +249,9 @@ typedef struct nh_render_stats {
     /* 1 when the last wavefront render ran one fused bounce kernel per bounce (shade + any-hit +
        closest-hit, LDS-staged BVHs): its time is in kernel_ms_shade, extend/shadow times are 0 */
     uint64_t fused_bounce;
+    /* RCCL communicator cliques created by nh_reduce_framebuffers with this context as root (a clique
+       is reused while the same contexts reduce again) */
+    uint64_t comm_inits;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;
@@ -301,7 +304,9 @@ int nh_get_framebuffer(nh_ctx *ctx, float *rgbw, size_t n_floats);
 int nh_framebuffer_device_ptr(nh_ctx *ctx, void **dptr, size_t *n_floats);
 int nh_get_stats(nh_ctx *ctx, nh_render_stats *out);
 int nh_reset_stats(nh_ctx *ctx);
-/* single-process multi-GPU: RCCL sum of the framebuffers of n contexts into ctxs[root] */
+/* single-process multi-GPU: RCCL sum of the framebuffers of n contexts into ctxs[root] (n = 1 included:
+   a one-rank reduce). The communicator clique is created on the first call for a set of contexts and
+   reused by later calls with the same contexts in the same order; it is destroyed with the contexts. */
 int nh_reduce_framebuffers(nh_ctx **ctxs, int32_t n, int32_t root);
 const char *nh_last_error(const nh_ctx *ctx);
 

@@ -10,7 +10,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <deque>
+#include <memory>
 #include <thread>
 #include <functional>
 #include <cmath>
@@ -75,7 +77,23 @@ struct WfPool {
     std::vector<uint64_t> in_e, in_s;  // live paths / shadow rays entering each bounce
 };
 
+// RCCL communicators of one set of contexts (nh_reduce_framebuffers), created once and reused while the
+// same contexts (by creation id, in the same order) reduce again; destroyed with the last holder.
+struct CommSet {
+    std::vector<uint64_t> ids;  // nh_ctx::id of the members, in rank order
+    std::vector<int> devices;
+    std::vector<ncclComm_t> comms;
+    ~CommSet() {
+        for (size_t i = 0; i < comms.size(); ++i) {
+            (void)hipSetDevice(devices[i]);
+            (void)ncclCommDestroy(comms[i]);
+        }
+    }
+};
+
 struct nh_ctx {
+    uint64_t id = 0;  // unique per context (process lifetime): identifies comm-set members
+    std::shared_ptr<CommSet> comms;
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
@@ -118,6 +136,7 @@ struct nh_ctx {
     uint64_t job_seq = 0, splat_seq = 0;  // chunks are splatted into fb in submission order
     hipEvent_t fb_ev = nullptr;           // the last enqueued write of fb (clear or splat)
     bool fb_ev_set = false;
+    uint64_t stats_comm_inits = 0;  // communicator cliques this context created as reduce root
 };
 
 extern "C" {
@@ -203,6 +222,8 @@ int nh_create(int device, nh_ctx **out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return NH_ERR_DEVICE;
     auto *c = new nh_ctx();
+    static std::atomic<uint64_t> next_id{1};
+    c->id = next_id++;
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->counters, kStatShards * kStatStride * sizeof(unsigned long long)) != hipSuccess ||
@@ -234,6 +255,7 @@ void nh_destroy(nh_ctx *c) {
     (void)hipFree(c->counters);
     (void)hipFree(c->d_scene);
     for (WfPool &p : c->pools) pool_free(p);
+    c->comms.reset();  // the communicators go with the last context of their set
     if (c->fb_ev) (void)hipEventDestroy(c->fb_ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1334,6 +1356,7 @@ int nh_get_stats(nh_ctx *c, nh_render_stats *out) {
     int rc = pipeline_drain(c);  // kernel times of chunks still in flight
     if (rc) return rc;
     *out = c->stats;
+    out->comm_inits = c->stats_comm_inits;
     return NH_OK;
 }
 
@@ -1354,27 +1377,41 @@ int nh_reduce_framebuffers(nh_ctx **ctxs, int32_t n, int32_t root) {
         (void)hipSetDevice(ctxs[i]->device);
         if (pipeline_drain(ctxs[i])) return NH_ERR_DEVICE;
     }
-    if (n == 1) return NH_OK;
-    std::vector<ncclComm_t> comms(n);
-    std::vector<int> devs(n);
-    for (int i = 0; i < n; ++i) devs[i] = ctxs[i]->device;
-    if (ncclCommInitAll(comms.data(), n, devs.data()) != ncclSuccess) {
-        ctxs[root]->err = "ncclCommInitAll failed";
-        return NH_ERR_DEVICE;
+    // one communicator clique per set of contexts, reused across calls (ncclCommInitAll costs far more
+    // than the reduce of a framebuffer); any change of members or order builds a new one
+    std::vector<uint64_t> ids(n);
+    for (int i = 0; i < n; ++i) ids[i] = ctxs[i]->id;
+    std::shared_ptr<CommSet> cs = ctxs[0]->comms;
+    if (!cs || cs->ids != ids) {
+        for (int i = 0; i < n; ++i) ctxs[i]->comms.reset();
+        cs = std::make_shared<CommSet>();
+        cs->ids = ids;
+        cs->devices.resize(n);
+        cs->comms.resize(n);
+        for (int i = 0; i < n; ++i) cs->devices[i] = ctxs[i]->device;
+        if (ncclCommInitAll(cs->comms.data(), n, cs->devices.data()) != ncclSuccess) {
+            cs->comms.clear();
+            ctxs[root]->err = "ncclCommInitAll failed";
+            return NH_ERR_DEVICE;
+        }
+        for (int i = 0; i < n; ++i) ctxs[i]->comms = cs;
+        ctxs[root]->stats_comm_inits++;
     }
-    ncclGroupStart();
-    for (int i = 0; i < n; ++i) {
+    ncclResult_t r = ncclGroupStart();
+    for (int i = 0; i < n && r == ncclSuccess; ++i) {
         (void)hipSetDevice(ctxs[i]->device);
-        ncclReduce(ctxs[i]->fb, ctxs[i]->fb, ctxs[i]->fb_floats, ncclFloat, ncclSum, root, comms[i], ctxs[i]->stream);
+        r = ncclReduce(ctxs[i]->fb, ctxs[i]->fb, ctxs[i]->fb_floats, ncclFloat, ncclSum, root, cs->comms[i],
+                       ctxs[i]->stream);
     }
-    ncclResult_t r = ncclGroupEnd();
+    const ncclResult_t g = ncclGroupEnd();
+    if (r == ncclSuccess) r = g;
     for (int i = 0; i < n; ++i) {
         (void)hipSetDevice(ctxs[i]->device);
         (void)hipStreamSynchronize(ctxs[i]->stream);
-        ncclCommDestroy(comms[i]);
     }
     if (r != ncclSuccess) {
-        ctxs[root]->err = "ncclReduce failed";
+        ctxs[root]->err = std::string("ncclReduce failed: ") + ncclGetErrorString(r);
+        for (int i = 0; i < n; ++i) ctxs[i]->comms.reset();
         return NH_ERR_DEVICE;
     }
     return NH_OK;

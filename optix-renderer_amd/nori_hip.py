@@ -122,7 +122,7 @@ class nh_render_stats(C.Structure):
                 ("node_bytes", C.c_uint64)] + [
         (n, C.c_uint64) for n in ("tail_queries", "tail_nodes_visited", "tail_boxes_tested", "tail_prims_tested",
                                   "tail_shadow_queries", "tail_shadow_nodes_visited", "tail_shadow_boxes_tested",
-                                  "tail_shadow_prims_tested", "lds_scene", "fused_bounce")]
+                                  "tail_shadow_prims_tested", "lds_scene", "fused_bounce", "comm_inits")]
 
 
 def _sig(name, res, *args):

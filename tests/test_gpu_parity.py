@@ -431,3 +431,38 @@ def test_fast_reciprocal_exhaustive(gpu):
     print(r.stdout.strip())
     assert r.returncode == 0, r.stdout + r.stderr
     assert "in_range_mismatches 0 " in r.stdout
+
+
+def test_reduce_framebuffers_reuses_communicator(gpu, tmp_path):
+    """nh_reduce_framebuffers (single-process RCCL reduce of per-GPU framebuffers): one box GPU, so a
+    one-rank clique -- the sum over one rank is the framebuffer itself; the communicator is created on
+    the first call and reused by the next, and a different context set gets its own."""
+    s, b, ctx = setup(scenegen.cbox_xml(str(tmp_path), "c2"), 48, 40)
+    ctx.render(0, 4, seed=2, clear=True, mode=nh.MODE_WAVEFRONT, traversal=nh.TRAVERSAL_ORDERED)
+    ref = ctx.framebuffer()
+    nh.reduce_framebuffers([ctx], root=0)
+    nh.reduce_framebuffers([ctx], root=0)
+    np.testing.assert_array_equal(ctx.framebuffer(), ref)
+    assert ctx.stats()["comm_inits"] == 1
+    other = nh.Context(0)
+    other.upload(s, b)
+    other.render(0, 4, seed=2, clear=True, mode=nh.MODE_WAVEFRONT, traversal=nh.TRAVERSAL_ORDERED)
+    nh.reduce_framebuffers([other], root=0)
+    assert other.stats()["comm_inits"] == 1
+    np.testing.assert_array_equal(other.framebuffer(), ref)
+    other.close()
+    nh.reduce_framebuffers([ctx], root=0)  # the first set's clique is still alive
+    assert ctx.stats()["comm_inits"] == 1
+
+
+def test_manual_scene_description_through_cabi(gpu):
+    """The binding path that needs no XML re-parse: a C program fills nh_scene_desc field by field
+    (camera matrices, filter table, meshes with area CDFs, two spheres with microfacet / mirror BSDFs,
+    an area light -- what per-plugin getHipRecord hooks would export), builds the BVH, renders through
+    nh_render and compares with the oracle on the same description (tests/c/manual_scene.c)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "bin", "manual_scene")
+    r = subprocess.run([exe, "8"], capture_output=True, text=True, timeout=120)
+    print(r.stdout.strip(), r.stderr.strip())
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bit-identical 1" in r.stdout
