@@ -16,3 +16,9 @@ mkdir -p "$OUT"
 # -include supplies that standard header, no reference file is altered or stubbed.
 g++ -O2 -std=c++11 -include algorithm -I"$REF/ext/pcg32" "$REF/ext/pcg32/pcg32-demo.cpp" -o "$OUT/pcg32-demo"
 echo "built $OUT/pcg32-demo"
+# Eigen evaluation-order probe (oracle/eigen_probe.cpp, test infrastructure) against the reference's
+# vendored Eigen 3.3.8, x86-64 SSE2 without FMA contraction as the reference is built
+if [ -d "$REF/ext/eigen/Eigen" ]; then
+  g++ -O2 -std=c++17 -ffp-contract=off -I"$REF/ext/eigen" "$(dirname "$0")/eigen_probe.cpp" -o "$OUT/eigen_probe"
+  echo "built $OUT/eigen_probe"
+fi

@@ -1354,6 +1354,41 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
 
 void no_scene_free(no_scene *s) { delete s; }
 
+// The oracle's restated Eigen arithmetic on the probe's cases (oracle/eigen_probe.cpp layout): the same
+// helpers the path uses (dot, normalized, max_coeff, sqnorm, norm, cross, cwise chains; camera_ray's
+// 3x3 direction product and 4x4 point product)
+int no_eigen_ops(int32_t n, const float *in, float *out) {
+    for (int32_t i = 0; i < n; ++i) {
+        const float *p = in + 36 * (size_t)i;
+        const V3 a = mk(p[0], p[1], p[2]), b = mk(p[3], p[4], p[5]), c = mk(p[6], p[7], p[8]);
+        const float s = p[9], *m3 = p + 10, *m4 = p + 20;
+        float *o = out + 24 * (size_t)i;
+        o[0] = dot(a, b);
+        const V3 an = normalized(a);
+        o[1] = an.x; o[2] = an.y; o[3] = an.z;
+        o[4] = max_coeff(a);
+        for (int r = 0; r < 3; ++r) o[5 + r] = m3[3 * r] * b.x + (m3[3 * r + 1] * b.y + m3[3 * r + 2] * b.z);
+        const float v4[4] = {b.x, b.y, b.z, 1.0f};
+        for (int r = 0; r < 4; ++r) {
+            float acc = m4[4 * r + 0] * v4[0];
+            acc = acc + m4[4 * r + 1] * v4[1];
+            acc = acc + m4[4 * r + 2] * v4[2];
+            acc = acc + m4[4 * r + 3] * v4[3];
+            o[8 + r] = acc;
+        }
+        o[12] = sqnorm(a);
+        o[13] = norm(a);
+        const V3 ch = cmul(a * s, b);
+        o[14] = ch.x; o[15] = ch.y; o[16] = ch.z;
+        const V3 ch2 = cmul(cmul(a, b), c);
+        o[17] = ch2.x; o[18] = ch2.y; o[19] = ch2.z;
+        const V3 x = cross(a, b);
+        o[20] = x.x; o[21] = x.y; o[22] = x.z;
+        o[23] = norm(a - b);
+    }
+    return NH_OK;
+}
+
 int no_bvh_info(const no_scene *s, uint32_t *n_nodes, uint32_t *n_indices) {
     *n_nodes = (uint32_t)s->nodes.size();
     *n_indices = (uint32_t)s->indices.size();

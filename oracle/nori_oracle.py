@@ -50,6 +50,7 @@ _sig("no_ttest_bsdf", _i32, C.POINTER(nh.nh_bsdf), C.c_float, _u64p, _u64p, _i32
 _sig("no_bsdf_sample", _i32, C.POINTER(nh.nh_bsdf), _fp, _fp, _fp, _fp, _fp, C.POINTER(_i32))
 _sig("no_bsdf_pdf", C.c_float, C.POINTER(nh.nh_bsdf), _fp, _fp)
 _sig("no_bsdf_pdf_batch", _i32, C.POINTER(nh.nh_bsdf), _fp, _i32, _fp, _fp)
+_sig("no_eigen_ops", _i32, _i32, _fp, _fp)
 _sig("no_chi2_histogram", _i32, C.POINTER(nh.nh_bsdf), _fp, _u64p, _u64p, _i32, _i32, _i32, C.POINTER(C.c_double))
 
 
@@ -186,3 +187,11 @@ def chi2_histogram(bsdf, wi, rng: Pcg32, n, res_theta, res_phi):
     _lib.no_chi2_histogram(C.byref(bsdf), wi.ctypes.data_as(_fp), C.byref(rng.state), C.byref(rng.inc), n, res_theta,
                            res_phi, obs.ctypes.data_as(C.POINTER(C.c_double)))
     return obs
+
+
+def eigen_ops(cases):
+    """The oracle's restated Eigen arithmetic (no_eigen_ops) on (n, 36) float32 cases -> (n, 24)."""
+    cases = np.ascontiguousarray(cases, np.float32)
+    out = np.zeros((len(cases), 24), np.float32)
+    _lib.no_eigen_ops(len(cases), cases.ctypes.data_as(_fp), out.ctypes.data_as(_fp))
+    return out

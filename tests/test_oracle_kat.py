@@ -196,3 +196,36 @@ def test_microfacet_chi2(scene_dir):
             exp = expected_frequencies(b, wi, res_t, res_p, n)
             passed += chi2_test(obs, exp, n, 5, 0.01, tests_per_bsdf * len(bsdfs))
     assert passed == tests_per_bsdf * len(bsdfs), passed
+
+
+def test_oracle_arithmetic_matches_reference_eigen(tmp_path):
+    """The oracle's restated Eigen arithmetic (dot = x0*y0 + (x1*y1 + x2*y2), normalized, maxCoeff,
+    squaredNorm/norm, cross, 3x3 and 4x4 matrix-vector products, Color3f cwise chains) is bit-identical
+    to the reference's own vendored Eigen 3.3.8 (ext/eigen, compiled unmodified into
+    oracle/_ref/eigen_probe by oracle/build_ref.sh) on random inputs, including wide exponent ranges,
+    signed zeros and denormals. Only where the reference checkout is present (this container)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(no.__file__), "_ref", "eigen_probe")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/eigen_probe not built (needs /root/reference/ext/eigen)")
+    rng = np.random.default_rng(2024)
+    n = 200000
+    cases = rng.normal(size=(n, 36)).astype(np.float32)
+    scale = (2.0 ** rng.integers(-20, 21, size=(n, 36))).astype(np.float32)
+    cases[n // 2:] *= scale[n // 2:]          # wide exponent ranges
+    cases[::97, 0] = 0.0                       # exact zeros / signed zeros
+    cases[1::97, 1] = -0.0
+    cases[2::89, 2] = np.float32(1e-40)        # denormals
+    cases[3::83, 3:6] = cases[3::83, 0:3]      # a == b (zero differences)
+    inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
+    cases.tofile(inp)
+    subprocess.run([exe, str(inp), str(out)], check=True, timeout=120)
+    ref = np.fromfile(out, np.float32).reshape(n, 24)
+    mine = no.eigen_ops(cases)
+    names = ["dot"] + ["normalized"] * 3 + ["maxCoeff"] + ["mat3*v"] * 3 + ["mat4*v"] * 4 + ["squaredNorm", "norm"] + \
+            ["(a*s)*b"] * 3 + ["a*b*c"] * 3 + ["cross"] * 3 + ["(a-b).norm"]
+    for j, name in enumerate(names):
+        r, m = ref[:, j].view(np.uint32), mine[:, j].view(np.uint32)
+        nan_both = np.isnan(ref[:, j]) & np.isnan(mine[:, j])
+        bad = (r != m) & ~nan_both
+        assert not bad.any(), f"{name} (column {j}): {bad.sum()} mismatches, e.g. case {np.argmax(bad)}"
