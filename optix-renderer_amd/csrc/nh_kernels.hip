@@ -93,7 +93,16 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
         const F3 nd = to_world(its.sh, wo);
         const F3 no = its.p;
 
-        if (nee) {  // shadow ray (path_mis.cpp:89): occluded -> no contribution, pdfs stay 0
+        // A discrete BSDF sample zeroes w_ems (path_mis.cpp:136-140): the light term (0 * t) * li_ems then
+        // adds exactly zero whether or not the shadow ray is occluded, as long as it is finite (Li never
+        // holds -0, so +-0 leaves it unchanged) -- that query is not traced (same draws, same result;
+        // the wavefront shade makes the same decision)
+        bool trace_shadow = nee;
+        if (nee && measure == M_DISCRETE) {
+            const F3 c = mulc(scl(0.f, t), li_ems), z = mulc(scl(0.f, t), f3(0, 0, 0));
+            if (c.x == 0.f && c.y == 0.f && c.z == 0.f && z.x == 0.f && z.y == 0.f && z.z == 0.f) trace_shadow = false;
+        }
+        if (trace_shadow) {  // shadow ray (path_mis.cpp:89): occluded -> no contribution, pdfs stay 0
             Hit hs;
             if (STATS) queries++;
             if (trace<DEPTH, ORDERED, true, STATS>(tv, S, es.so, es.sd, es.smint, es.smaxt, hs, stk, stride, st)) {

@@ -546,6 +546,15 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
                 if (nee && (pdfems_mats + pdfems) > kEps) w_un = pdfems / (pdfems_mats + pdfems);
                 if (discrete) w_occ = w_un = 0.f;
                 int fl = (discrete ? F_DISCRETE : 0) | (is_zero(bsdf_col) ? F_ZERO_COL : 0);
+                if (nee && discrete) {
+                    // the discrete sample zeroes both weights: a finite term (0 * t) * li_ems adds exactly zero
+                    // occluded or not (Li never holds -0), so no shadow ray is queued (as the megakernel)
+                    const F3 c = mulc(scl(w_un, t), li_ems), z = mulc(scl(w_occ, t), f3(0, 0, 0));
+                    if (c.x == 0.f && c.y == 0.f && c.z == 0.f && z.x == 0.f && z.y == 0.f && z.z == 0.f) {
+                        nee = false;
+                        li_ems = f3(0, 0, 0);  // the unoccluded term is +-0: Li is unchanged either way
+                    }
+                }
                 if (nee) {
                     // Li += w_ems * t * Li_ems (:142) once the shadow ray is known to be unoccluded
                     const F3 c = mulc(scl(w_un, t), li_ems);
