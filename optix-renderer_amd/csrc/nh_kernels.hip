@@ -454,80 +454,14 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
 // gives each block-array pixel the ordered sum of its contributions, in the reference's
 // getSampleIndices order (x outer, y inner), starting from the cleared block (0).
 constexpr int kSplatMaxCols = 40;  // 32 + 2*border, border <= 4
-__global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
-    // sample (lx, ly) lives at lx*33 + ly: neighbouring lanes step lx, the odd stride keeps
-    // them on distinct LDS banks
-    __shared__ float s_val[3][32 * 33];
-    __shared__ float s_pos[2][32 * 33];
-    __shared__ int s_box[32 * 33];  // x0 | x1<<8 | y0<<16 | y1<<24 (block-array coords), x1 < x0: empty
-    __shared__ float s_tab[33];
-    const int slot = blockIdx.x, k = blockIdx.y;
-    const int bid = P.blocks[slot];
-    const int by = bid / P.nbx, bx = bid - by * P.nbx;
-    const int ox = bx * 32, oy = by * 32;
-    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    const int cols = 32 + 2 * P.border;
-    const float r = P.radius;
-    if (threadIdx.x < 33) s_tab[threadIdx.x] = P.table[threadIdx.x];
-    const size_t rbase = (size_t)k * P.n_list;
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-        const int lx = i >> 5, ly = i & 31;  // sample index i = lx*32 + ly: x-major order
-        int box = 0xff;                      // x0 = 255 > x1 = 0: empty
-        float vx = 0.f, vy = 0.f, vz = 0.f, px = 0.f, py = 0.f;
-        if (lx < sxb && ly < syb) {
-            const int li = P.pixel_map[(oy + ly) * P.width + (ox + lx)];
-            if (li >= 0) {
-                const float4 rec = P.rec_rgbx[rbase + li];
-                if (is_valid(f3(rec.x, rec.y, rec.z))) {  // invalid samples drop with their weight
-                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li];
-                    px = spx - 0.5f - (float)(ox - P.border);
-                    py = spy - 0.5f - (float)(oy - P.border);
-                    int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
-                    int x1 = min((int)floorf(px + r), cols - 1), y1 = min((int)floorf(py + r), cols - 1);
-                    box = x0 | (x1 << 8) | (y0 << 16) | (y1 << 24);
-                    vx = rec.x; vy = rec.y; vz = rec.z;
-                }
-            }
-        }
-        const int j = lx * 33 + ly;
-        s_val[0][j] = vx; s_val[1][j] = vy; s_val[2][j] = vz;
-        s_pos[0][j] = px; s_pos[1][j] = py;
-        s_box[j] = box;
-    }
-    __syncthreads();
-    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
-    const int R = P.reach, bd = P.border;
-    for (int q = threadIdx.x; q < cols * cols; q += 256) {
-        const int yt = q / cols, xt = q - yt * cols;
-        float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
-        const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
-        const int ly0 = max(yt - bd - R, 0), ly1 = min(yt - bd + R, syb - 1);
-        for (int lx = lx0; lx <= lx1; ++lx)
-            for (int ly = ly0; ly <= ly1; ++ly) {
-                const int i = lx * 33 + ly;
-                const int box = s_box[i];
-                const int x0 = box & 0xff, x1 = (box >> 8) & 0xff, y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
-                if (xt < x0 || xt > x1 || yt < y0 || yt > y1) continue;
-                const float wx = s_tab[(int)(fabsf((float)xt - s_pos[0][i]) * P.lookup)];
-                const float wy = s_tab[(int)(fabsf((float)yt - s_pos[1][i]) * P.lookup)];
-                ar += s_val[0][i] * wx * wy;
-                ag += s_val[1][i] * wx * wy;
-                ab += s_val[2][i] * wx * wy;
-                aw += 1.0f * wx * wy;
-            }
-        out[q] = make_float4(ar, ag, ab, aw);
-    }
-}
+constexpr int kAccumPx = (kSplatMaxCols * kSplatMaxCols + 255) / 256;  // block-array pixels per thread
 
-// ImageBlock::put(ImageBlock&) into the master (src/utils/block.cpp:125-134): per master
-// pixel, per round, the overlapping rendered blocks in BlockGenerator spiral order.
-__global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
-    const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
-    const int mx = blockIdx.x * 16 + (threadIdx.x & 15), my = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (mx >= mcols || my >= mrows) return;
+// Rendered blocks whose merged region ((sx+2b) x (sy+2b) at offset (ox, oy) in master coordinates)
+// covers master pixel (mx, my), in BlockGenerator spiral order: the order ImageBlock::put(ImageBlock&)
+// adds them (src/utils/block.cpp:125-134). Returns their number (<= 4) and slots.
+__device__ __forceinline__ int covering_blocks(const SplatLaunch &P, int mx, int my, int *slot) {
     const int cols = 32 + 2 * P.border;
-    // blocks whose merged region (sx+2b)x(sy+2b) at offset (ox, oy) covers (mx, my)
-    int blk[4], slot[4], nb = 0;
+    int blk[4], nb = 0;
     const int bx_lo = max((mx - cols + 1 + 31) >> 5, 0), bx_hi = min(mx >> 5, P.nbx - 1);
     const int nby = (P.height + 31) >> 5;
     const int by_lo = max((my - cols + 1 + 31) >> 5, 0), by_hi = min(my >> 5, nby - 1);
@@ -543,15 +477,143 @@ __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
             slot[nb] = sl;
             ++nb;
         }
-    if (nb == 0) return;
     for (int a = 1; a < nb; ++a)
         for (int b = a; b > 0 && P.block_rank[blk[b]] < P.block_rank[blk[b - 1]]; --b) {
             int t = blk[b]; blk[b] = blk[b - 1]; blk[b - 1] = t;
             t = slot[b]; slot[b] = slot[b - 1]; slot[b - 1] = t;
         }
+    return nb;
+}
+
+// ImageBlock::put(pos, value) for every round of a chunk of one rendered block, then ImageBlock::put(block)
+// into the master (src/utils/render.cpp:421-458, src/utils/block.cpp:93-134). One workgroup per block runs
+// the chunk's rounds in order. Per round: the block's <= 1024 sample footprints go to LDS once (odd-stride
+// layout, no bank conflicts), then each block-array pixel sums its contributions in getSampleIndices
+// order (x outer, y inner) from a cleared block (0). Master pixels that no other rendered block's region
+// covers (the 28x28 interior at border 2) take the rounds' sums straight into a register accumulator
+// (master + round 0 + round 1 ..., the serial reference's order) and are written once; pixels in the
+// bands shared with neighbouring blocks go to the staging array for nh_merge_kernel, which adds them in
+// (round, spiral rank) order. Interior pixels thus never touch the staging array in HBM.
+__global__ __launch_bounds__(256) void nh_block_accum_kernel(SplatLaunch P) {
+    // sample (lx, ly) lives at lx*33 + ly: neighbouring lanes step lx, the odd stride keeps
+    // them on distinct LDS banks
+    __shared__ float s_val[3][32 * 33];
+    __shared__ float s_pos[2][32 * 33];
+    __shared__ int s_box[32 * 33];  // x0 | x1<<8 | y0<<16 | y1<<24 (block-array coords), x1 < x0: empty
+    __shared__ float s_tab[33];
+    const int slot = blockIdx.x;
+    const int bid = P.blocks[slot];
+    const int by = bid / P.nbx, bx = bid - by * P.nbx;
+    const int ox = bx * 32, oy = by * 32;
+    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+    const int cols = 32 + 2 * P.border, mcols = P.width + 2 * P.border;
+    const float r = P.radius;
+    const int R = P.reach, bd = P.border;
+    if (threadIdx.x < 33) s_tab[threadIdx.x] = P.table[threadIdx.x];
+    // this thread's samples (list entries, fixed over the rounds) and block-array pixels
+    int li_of[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int i = threadIdx.x + 256 * j, lx = i >> 5, ly = i & 31;
+        li_of[j] = (lx < sxb && ly < syb) ? P.pixel_map[(oy + ly) * P.width + (ox + lx)] : -1;
+    }
+    float4 acc[kAccumPx];
+    bool excl[kAccumPx];  // the master pixel is covered by this block only
+#pragma unroll
+    for (int j = 0; j < kAccumPx; ++j) {
+        const int q = threadIdx.x + 256 * j;
+        const int yt = q / cols, xt = q - yt * cols;
+        excl[j] = false;
+        acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (q < cols * cols && xt < sxb + 2 * bd && yt < syb + 2 * bd) {
+            int sl[4];
+            excl[j] = covering_blocks(P, ox + xt, oy + yt, sl) == 1;
+            if (excl[j]) acc[j] = reinterpret_cast<const float4 *>(P.fb)[(size_t)(oy + yt) * mcols + (ox + xt)];
+        }
+    }
+    for (int k = 0; k < P.n_rounds; ++k) {
+        const size_t rbase = (size_t)k * P.n_list;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = threadIdx.x + 256 * j, lx = i >> 5, ly = i & 31;
+            int box = 0xff;  // x0 = 255 > x1 = 0: empty
+            float vx = 0.f, vy = 0.f, vz = 0.f, px = 0.f, py = 0.f;
+            if (li_of[j] >= 0) {
+                const float4 rec = P.rec_rgbx[rbase + li_of[j]];
+                if (is_valid(f3(rec.x, rec.y, rec.z))) {  // invalid samples drop with their weight
+                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li_of[j]];
+                    px = spx - 0.5f - (float)(ox - P.border);
+                    py = spy - 0.5f - (float)(oy - P.border);
+                    int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
+                    int x1 = min((int)floorf(px + r), cols - 1), y1 = min((int)floorf(py + r), cols - 1);
+                    box = x0 | (x1 << 8) | (y0 << 16) | (y1 << 24);
+                    vx = rec.x; vy = rec.y; vz = rec.z;
+                }
+            }
+            const int s = lx * 33 + ly;
+            s_val[0][s] = vx; s_val[1][s] = vy; s_val[2][s] = vz;
+            s_pos[0][s] = px; s_pos[1][s] = py;
+            s_box[s] = box;
+        }
+        __syncthreads();
+        float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+#pragma unroll
+        for (int j = 0; j < kAccumPx; ++j) {
+            const int q = threadIdx.x + 256 * j;
+            if (q >= cols * cols) break;
+            const int yt = q / cols, xt = q - yt * cols;
+            float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
+            const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
+            const int ly0 = max(yt - bd - R, 0), ly1 = min(yt - bd + R, syb - 1);
+            for (int lx = lx0; lx <= lx1; ++lx)
+                for (int ly = ly0; ly <= ly1; ++ly) {
+                    const int i = lx * 33 + ly;
+                    const int box = s_box[i];
+                    const int x0 = box & 0xff, x1 = (box >> 8) & 0xff, y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
+                    if (xt < x0 || xt > x1 || yt < y0 || yt > y1) continue;
+                    const float wx = s_tab[(int)(fabsf((float)xt - s_pos[0][i]) * P.lookup)];
+                    const float wy = s_tab[(int)(fabsf((float)yt - s_pos[1][i]) * P.lookup)];
+                    ar += s_val[0][i] * wx * wy;
+                    ag += s_val[1][i] * wx * wy;
+                    ab += s_val[2][i] * wx * wy;
+                    aw += 1.0f * wx * wy;
+                }
+            if (excl[j]) {
+                acc[j].x += ar;
+                acc[j].y += ag;
+                acc[j].z += ab;
+                acc[j].w += aw;
+            } else {
+                out[q] = make_float4(ar, ag, ab, aw);
+            }
+        }
+        __syncthreads();  // the next round overwrites the footprints
+    }
+#pragma unroll
+    for (int j = 0; j < kAccumPx; ++j) {
+        const int q = threadIdx.x + 256 * j;
+        if (q < cols * cols && excl[j]) {
+            const int yt = q / cols, xt = q - yt * cols;
+            reinterpret_cast<float4 *>(P.fb)[(size_t)(oy + yt) * mcols + (ox + xt)] = acc[j];
+        }
+    }
+}
+
+// ImageBlock::put(ImageBlock&) into the master (src/utils/block.cpp:125-134) for the master pixels in the
+// bands several rendered blocks cover: per round, the overlapping blocks in BlockGenerator spiral
+// order. Pixels covered by one block only were written by nh_block_accum_kernel.
+__global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
+    const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
+    const int mx = blockIdx.x * 16 + (threadIdx.x & 15), my = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (mx >= mcols || my >= mrows) return;
+    const int cols = 32 + 2 * P.border;
+    int slot[4];
+    const int nb = covering_blocks(P, mx, my, slot);
+    if (nb <= 1) return;
     int off[4];
     for (int q = 0; q < nb; ++q) {
-        const int by = blk[q] / P.nbx, bx = blk[q] - by * P.nbx;
+        const int bid = P.blocks[slot[q]];
+        const int by = bid / P.nbx, bx = bid - by * P.nbx;
         off[q] = (my - by * 32) * cols + (mx - bx * 32);
     }
     float4 *mp = reinterpret_cast<float4 *>(P.fb) + (size_t)my * mcols + mx;
@@ -672,7 +734,7 @@ void launch_path(const DScene *S, const Traversal &tv, const PathLaunch &L, bool
 }
 
 void launch_splat(const SplatLaunch &P, hipStream_t st) {
-    hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(nh_block_accum_kernel, dim3(P.n_blocks), dim3(256), 0, st, P);
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     dim3 grid((mcols + 15) / 16, (mrows + 15) / 16);
     hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, P);
