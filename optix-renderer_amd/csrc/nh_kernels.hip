@@ -454,7 +454,70 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
 // gives each block-array pixel the ordered sum of its contributions, in the reference's
 // getSampleIndices order (x outer, y inner), starting from the cleared block (0).
 constexpr int kSplatMaxCols = 40;  // 32 + 2*border, border <= 4
-constexpr int kAccumPx = (kSplatMaxCols * kSplatMaxCols + 255) / 256;  // block-array pixels per thread
+__global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
+    // sample (lx, ly) lives at lx*33 + ly: neighbouring lanes step lx, the odd stride keeps
+    // them on distinct LDS banks
+    __shared__ float s_val[3][32 * 33];
+    __shared__ float s_pos[2][32 * 33];
+    __shared__ int s_box[32 * 33];  // x0 | x1<<8 | y0<<16 | y1<<24 (block-array coords), x1 < x0: empty
+    __shared__ float s_tab[33];
+    const int slot = blockIdx.x, k = blockIdx.y;
+    const int bid = P.blocks[slot];
+    const int by = bid / P.nbx, bx = bid - by * P.nbx;
+    const int ox = bx * 32, oy = by * 32;
+    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+    const int cols = 32 + 2 * P.border;
+    const float r = P.radius;
+    if (threadIdx.x < 33) s_tab[threadIdx.x] = P.table[threadIdx.x];
+    const size_t rbase = (size_t)k * P.n_list;
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        const int lx = i >> 5, ly = i & 31;  // sample index i = lx*32 + ly: x-major order
+        int box = 0xff;                      // x0 = 255 > x1 = 0: empty
+        float vx = 0.f, vy = 0.f, vz = 0.f, px = 0.f, py = 0.f;
+        if (lx < sxb && ly < syb) {
+            const int li = P.pixel_map[(oy + ly) * P.width + (ox + lx)];
+            if (li >= 0) {
+                const float4 rec = P.rec_rgbx[rbase + li];
+                if (is_valid(f3(rec.x, rec.y, rec.z))) {  // invalid samples drop with their weight
+                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li];
+                    px = spx - 0.5f - (float)(ox - P.border);
+                    py = spy - 0.5f - (float)(oy - P.border);
+                    int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
+                    int x1 = min((int)floorf(px + r), cols - 1), y1 = min((int)floorf(py + r), cols - 1);
+                    box = x0 | (x1 << 8) | (y0 << 16) | (y1 << 24);
+                    vx = rec.x; vy = rec.y; vz = rec.z;
+                }
+            }
+        }
+        const int j = lx * 33 + ly;
+        s_val[0][j] = vx; s_val[1][j] = vy; s_val[2][j] = vz;
+        s_pos[0][j] = px; s_pos[1][j] = py;
+        s_box[j] = box;
+    }
+    __syncthreads();
+    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+    const int R = P.reach, bd = P.border;
+    for (int q = threadIdx.x; q < cols * cols; q += 256) {
+        const int yt = q / cols, xt = q - yt * cols;
+        float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
+        const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
+        const int ly0 = max(yt - bd - R, 0), ly1 = min(yt - bd + R, syb - 1);
+        for (int lx = lx0; lx <= lx1; ++lx)
+            for (int ly = ly0; ly <= ly1; ++ly) {
+                const int i = lx * 33 + ly;
+                const int box = s_box[i];
+                const int x0 = box & 0xff, x1 = (box >> 8) & 0xff, y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
+                if (xt < x0 || xt > x1 || yt < y0 || yt > y1) continue;
+                const float wx = s_tab[(int)(fabsf((float)xt - s_pos[0][i]) * P.lookup)];
+                const float wy = s_tab[(int)(fabsf((float)yt - s_pos[1][i]) * P.lookup)];
+                ar += s_val[0][i] * wx * wy;
+                ag += s_val[1][i] * wx * wy;
+                ab += s_val[2][i] * wx * wy;
+                aw += 1.0f * wx * wy;
+            }
+        out[q] = make_float4(ar, ag, ab, aw);
+    }
+}
 
 // Rendered blocks whose merged region ((sx+2b) x (sy+2b) at offset (ox, oy) in master coordinates)
 // covers master pixel (mx, my), in BlockGenerator spiral order: the order ImageBlock::put(ImageBlock&)
@@ -485,123 +548,85 @@ __device__ __forceinline__ int covering_blocks(const SplatLaunch &P, int mx, int
     return nb;
 }
 
-// ImageBlock::put(pos, value) for every round of a chunk of one rendered block, then ImageBlock::put(block)
-// into the master (src/utils/render.cpp:421-458, src/utils/block.cpp:93-134). One workgroup per block runs
-// the chunk's rounds in order. Per round: the block's <= 1024 sample footprints go to LDS once (odd-stride
-// layout, no bank conflicts), then each block-array pixel sums its contributions in getSampleIndices
-// order (x outer, y inner) from a cleared block (0). Master pixels that no other rendered block's region
-// covers (the 28x28 interior at border 2) take the rounds' sums straight into a register accumulator
-// (master + round 0 + round 1 ..., the serial reference's order) and are written once; pixels in the
-// bands shared with neighbouring blocks go to the staging array for nh_merge_kernel, which adds them in
-// (round, spiral rank) order. Interior pixels thus never touch the staging array in HBM.
-__global__ __launch_bounds__(256) void nh_block_accum_kernel(SplatLaunch P) {
-    // sample (lx, ly) lives at lx*33 + ly: neighbouring lanes step lx, the odd stride keeps
-    // them on distinct LDS banks
-    __shared__ float s_val[3][32 * 33];
-    __shared__ float s_pos[2][32 * 33];
-    __shared__ int s_box[32 * 33];  // x0 | x1<<8 | y0<<16 | y1<<24 (block-array coords), x1 < x0: empty
+// The same splat for the default filter reach (radius 2, border 2: 36x36 block arrays, every sample's
+// footprint inside the 5x5 pixels starting at (lx, ly)). Phase 1 tabulates each sample's x and y weights
+// for those 5 columns and rows once -- filter[(int)(|x - pos| * lookup)] inside its footprint, 0 outside
+// (ImageBlock::put's m_weightsX / m_weightsY, block.cpp:105-117) -- so phase 2 adds (value * wx) * wy
+// without per-pair box tests or table lookups. A zero weight adds +0 (or -0), which leaves the sum
+// unchanged: values are finite and non-negative (invalid samples are dropped) and a sum never holds -0,
+// so the result equals the footprint-tested sum bit for bit.
+constexpr int kSplatStride = 33;  // sample (lx, ly) at lx*33 + ly: neighbouring lanes on distinct banks
+__global__ __launch_bounds__(256) void nh_block_splat_r2_kernel(SplatLaunch P) {
+    __shared__ float4 s_val[32 * kSplatStride];   // (r, g, b, 1); weights 0 for empty / dropped samples
+    __shared__ float s_wx[5][32 * kSplatStride];  // weight of column lx + d
+    __shared__ float s_wy[5][32 * kSplatStride];  // weight of row ly + d
     __shared__ float s_tab[33];
-    const int slot = blockIdx.x;
+    const int slot = blockIdx.x, k = blockIdx.y;
     const int bid = P.blocks[slot];
     const int by = bid / P.nbx, bx = bid - by * P.nbx;
     const int ox = bx * 32, oy = by * 32;
     const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    const int cols = 32 + 2 * P.border, mcols = P.width + 2 * P.border;
+    constexpr int cols = 36;
     const float r = P.radius;
-    const int R = P.reach, bd = P.border;
     if (threadIdx.x < 33) s_tab[threadIdx.x] = P.table[threadIdx.x];
-    // this thread's samples (list entries, fixed over the rounds) and block-array pixels
-    int li_of[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int i = threadIdx.x + 256 * j, lx = i >> 5, ly = i & 31;
-        li_of[j] = (lx < sxb && ly < syb) ? P.pixel_map[(oy + ly) * P.width + (ox + lx)] : -1;
-    }
-    float4 acc[kAccumPx];
-    bool excl[kAccumPx];  // the master pixel is covered by this block only
-#pragma unroll
-    for (int j = 0; j < kAccumPx; ++j) {
-        const int q = threadIdx.x + 256 * j;
-        const int yt = q / cols, xt = q - yt * cols;
-        excl[j] = false;
-        acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (q < cols * cols && xt < sxb + 2 * bd && yt < syb + 2 * bd) {
-            int sl[4];
-            excl[j] = covering_blocks(P, ox + xt, oy + yt, sl) == 1;
-            if (excl[j]) acc[j] = reinterpret_cast<const float4 *>(P.fb)[(size_t)(oy + yt) * mcols + (ox + xt)];
-        }
-    }
-    for (int k = 0; k < P.n_rounds; ++k) {
-        const size_t rbase = (size_t)k * P.n_list;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = threadIdx.x + 256 * j, lx = i >> 5, ly = i & 31;
-            int box = 0xff;  // x0 = 255 > x1 = 0: empty
-            float vx = 0.f, vy = 0.f, vz = 0.f, px = 0.f, py = 0.f;
-            if (li_of[j] >= 0) {
-                const float4 rec = P.rec_rgbx[rbase + li_of[j]];
+    __syncthreads();
+    const size_t rbase = (size_t)k * P.n_list;
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        const int lx = i >> 5, ly = i & 31;  // sample index i = lx*32 + ly: x-major order
+        float4 v = make_float4(0.f, 0.f, 0.f, 1.f);
+        float wx[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, wy[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+        if (lx < sxb && ly < syb) {
+            const int li = P.pixel_map[(oy + ly) * P.width + (ox + lx)];
+            if (li >= 0) {
+                const float4 rec = P.rec_rgbx[rbase + li];
                 if (is_valid(f3(rec.x, rec.y, rec.z))) {  // invalid samples drop with their weight
-                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li_of[j]];
-                    px = spx - 0.5f - (float)(ox - P.border);
-                    py = spy - 0.5f - (float)(oy - P.border);
-                    int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
-                    int x1 = min((int)floorf(px + r), cols - 1), y1 = min((int)floorf(py + r), cols - 1);
-                    box = x0 | (x1 << 8) | (y0 << 16) | (y1 << 24);
-                    vx = rec.x; vy = rec.y; vz = rec.z;
-                }
-            }
-            const int s = lx * 33 + ly;
-            s_val[0][s] = vx; s_val[1][s] = vy; s_val[2][s] = vz;
-            s_pos[0][s] = px; s_pos[1][s] = py;
-            s_box[s] = box;
-        }
-        __syncthreads();
-        float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li];
+                    const float px = spx - 0.5f - (float)(ox - 2), py = spy - 0.5f - (float)(oy - 2);
+                    const int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
+                    const int x1 = min((int)floorf(px + r), cols - 1), y1 = min((int)floorf(py + r), cols - 1);
 #pragma unroll
-        for (int j = 0; j < kAccumPx; ++j) {
-            const int q = threadIdx.x + 256 * j;
-            if (q >= cols * cols) break;
-            const int yt = q / cols, xt = q - yt * cols;
-            float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
-            const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
-            const int ly0 = max(yt - bd - R, 0), ly1 = min(yt - bd + R, syb - 1);
-            for (int lx = lx0; lx <= lx1; ++lx)
-                for (int ly = ly0; ly <= ly1; ++ly) {
-                    const int i = lx * 33 + ly;
-                    const int box = s_box[i];
-                    const int x0 = box & 0xff, x1 = (box >> 8) & 0xff, y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
-                    if (xt < x0 || xt > x1 || yt < y0 || yt > y1) continue;
-                    const float wx = s_tab[(int)(fabsf((float)xt - s_pos[0][i]) * P.lookup)];
-                    const float wy = s_tab[(int)(fabsf((float)yt - s_pos[1][i]) * P.lookup)];
-                    ar += s_val[0][i] * wx * wy;
-                    ag += s_val[1][i] * wx * wy;
-                    ab += s_val[2][i] * wx * wy;
-                    aw += 1.0f * wx * wy;
+                    for (int d = 0; d < 5; ++d) {
+                        const int xt = lx + d, yt = ly + d;
+                        wx[d] = (xt >= x0 && xt <= x1) ? s_tab[(int)(fabsf((float)xt - px) * P.lookup)] : 0.f;
+                        wy[d] = (yt >= y0 && yt <= y1) ? s_tab[(int)(fabsf((float)yt - py) * P.lookup)] : 0.f;
+                    }
+                    v = make_float4(rec.x, rec.y, rec.z, 1.f);
                 }
-            if (excl[j]) {
-                acc[j].x += ar;
-                acc[j].y += ag;
-                acc[j].z += ab;
-                acc[j].w += aw;
-            } else {
-                out[q] = make_float4(ar, ag, ab, aw);
             }
         }
-        __syncthreads();  // the next round overwrites the footprints
+        const int j = lx * kSplatStride + ly;
+        s_val[j] = v;
+#pragma unroll
+        for (int d = 0; d < 5; ++d) {
+            s_wx[d][j] = wx[d];
+            s_wy[d][j] = wy[d];
+        }
     }
-#pragma unroll
-    for (int j = 0; j < kAccumPx; ++j) {
-        const int q = threadIdx.x + 256 * j;
-        if (q < cols * cols && excl[j]) {
-            const int yt = q / cols, xt = q - yt * cols;
-            reinterpret_cast<float4 *>(P.fb)[(size_t)(oy + yt) * mcols + (ox + xt)] = acc[j];
+    __syncthreads();
+    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+    for (int q = threadIdx.x; q < cols * cols; q += 256) {
+        const int yt = q / cols, xt = q - yt * cols;
+        float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
+        const int lx0 = max(xt - 4, 0), lx1 = min(xt, sxb - 1);
+        const int ly0 = max(yt - 4, 0), ly1 = min(yt, syb - 1);
+        for (int lx = lx0; lx <= lx1; ++lx) {
+            const int dx = xt - lx;
+            for (int ly = ly0; ly <= ly1; ++ly) {
+                const int i = lx * kSplatStride + ly;
+                const float wxs = s_wx[dx][i], wys = s_wy[yt - ly][i];
+                const float4 v = s_val[i];
+                ar += v.x * wxs * wys;
+                ag += v.y * wxs * wys;
+                ab += v.z * wxs * wys;
+                aw += v.w * wxs * wys;
+            }
         }
+        out[q] = make_float4(ar, ag, ab, aw);
     }
 }
 
-// ImageBlock::put(ImageBlock&) into the master (src/utils/block.cpp:125-134) for the master pixels in the
-// bands several rendered blocks cover: per round, the overlapping blocks in BlockGenerator spiral
-// order. Pixels covered by one block only were written by nh_block_accum_kernel.
+// ImageBlock::put(ImageBlock&) into the master (src/utils/block.cpp:125-134): per master
+// pixel, per round, the overlapping rendered blocks in BlockGenerator spiral order.
 __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     const int mx = blockIdx.x * 16 + (threadIdx.x & 15), my = blockIdx.y * 16 + (threadIdx.x >> 4);
@@ -609,7 +634,7 @@ __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
     const int cols = 32 + 2 * P.border;
     int slot[4];
     const int nb = covering_blocks(P, mx, my, slot);
-    if (nb <= 1) return;
+    if (nb == 0) return;
     int off[4];
     for (int q = 0; q < nb; ++q) {
         const int bid = P.blocks[slot[q]];
@@ -734,7 +759,10 @@ void launch_path(const DScene *S, const Traversal &tv, const PathLaunch &L, bool
 }
 
 void launch_splat(const SplatLaunch &P, hipStream_t st) {
-    hipLaunchKernelGGL(nh_block_accum_kernel, dim3(P.n_blocks), dim3(256), 0, st, P);
+    if (P.reach == 2 && P.border == 2)  // the default Gaussian (radius 2): tabulated per-sample weights
+        hipLaunchKernelGGL(nh_block_splat_r2_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
+    else
+        hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     dim3 grid((mcols + 15) / 16, (mrows + 15) / 16);
     hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, P);
