@@ -548,83 +548,6 @@ __device__ __forceinline__ int covering_blocks(const SplatLaunch &P, int mx, int
     return nb;
 }
 
-// The same splat for the default filter reach (radius 2, border 2: 36x36 block arrays, every sample's
-// footprint inside the 5x5 pixels starting at (lx, ly)). Phase 1 tabulates each sample's x and y weights
-// for those 5 columns and rows once -- filter[(int)(|x - pos| * lookup)] inside its footprint, 0 outside
-// (ImageBlock::put's m_weightsX / m_weightsY, block.cpp:105-117) -- so phase 2 adds (value * wx) * wy
-// without per-pair box tests or table lookups. A zero weight adds +0 (or -0), which leaves the sum
-// unchanged: values are finite and non-negative (invalid samples are dropped) and a sum never holds -0,
-// so the result equals the footprint-tested sum bit for bit.
-constexpr int kSplatStride = 33;  // sample (lx, ly) at lx*33 + ly: neighbouring lanes on distinct banks
-__global__ __launch_bounds__(256) void nh_block_splat_r2_kernel(SplatLaunch P) {
-    __shared__ float4 s_val[32 * kSplatStride];   // (r, g, b, 1); weights 0 for empty / dropped samples
-    __shared__ float s_wx[5][32 * kSplatStride];  // weight of column lx + d
-    __shared__ float s_wy[5][32 * kSplatStride];  // weight of row ly + d
-    __shared__ float s_tab[33];
-    const int slot = blockIdx.x, k = blockIdx.y;
-    const int bid = P.blocks[slot];
-    const int by = bid / P.nbx, bx = bid - by * P.nbx;
-    const int ox = bx * 32, oy = by * 32;
-    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    constexpr int cols = 36;
-    const float r = P.radius;
-    if (threadIdx.x < 33) s_tab[threadIdx.x] = P.table[threadIdx.x];
-    __syncthreads();
-    const size_t rbase = (size_t)k * P.n_list;
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-        const int lx = i >> 5, ly = i & 31;  // sample index i = lx*32 + ly: x-major order
-        float4 v = make_float4(0.f, 0.f, 0.f, 1.f);
-        float wx[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, wy[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-        if (lx < sxb && ly < syb) {
-            const int li = P.pixel_map[(oy + ly) * P.width + (ox + lx)];
-            if (li >= 0) {
-                const float4 rec = P.rec_rgbx[rbase + li];
-                if (is_valid(f3(rec.x, rec.y, rec.z))) {  // invalid samples drop with their weight
-                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li];
-                    const float px = spx - 0.5f - (float)(ox - 2), py = spy - 0.5f - (float)(oy - 2);
-                    const int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
-                    const int x1 = min((int)floorf(px + r), cols - 1), y1 = min((int)floorf(py + r), cols - 1);
-#pragma unroll
-                    for (int d = 0; d < 5; ++d) {
-                        const int xt = lx + d, yt = ly + d;
-                        wx[d] = (xt >= x0 && xt <= x1) ? s_tab[(int)(fabsf((float)xt - px) * P.lookup)] : 0.f;
-                        wy[d] = (yt >= y0 && yt <= y1) ? s_tab[(int)(fabsf((float)yt - py) * P.lookup)] : 0.f;
-                    }
-                    v = make_float4(rec.x, rec.y, rec.z, 1.f);
-                }
-            }
-        }
-        const int j = lx * kSplatStride + ly;
-        s_val[j] = v;
-#pragma unroll
-        for (int d = 0; d < 5; ++d) {
-            s_wx[d][j] = wx[d];
-            s_wy[d][j] = wy[d];
-        }
-    }
-    __syncthreads();
-    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
-    for (int q = threadIdx.x; q < cols * cols; q += 256) {
-        const int yt = q / cols, xt = q - yt * cols;
-        float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
-        const int lx0 = max(xt - 4, 0), lx1 = min(xt, sxb - 1);
-        const int ly0 = max(yt - 4, 0), ly1 = min(yt, syb - 1);
-        for (int lx = lx0; lx <= lx1; ++lx) {
-            const int dx = xt - lx;
-            for (int ly = ly0; ly <= ly1; ++ly) {
-                const int i = lx * kSplatStride + ly;
-                const float wxs = s_wx[dx][i], wys = s_wy[yt - ly][i];
-                const float4 v = s_val[i];
-                ar += v.x * wxs * wys;
-                ag += v.y * wxs * wys;
-                ab += v.z * wxs * wys;
-                aw += v.w * wxs * wys;
-            }
-        }
-        out[q] = make_float4(ar, ag, ab, aw);
-    }
-}
-
 // ImageBlock::put(ImageBlock&) into the master (src/utils/block.cpp:125-134): per master
 // pixel, per round, the overlapping rendered blocks in BlockGenerator spiral order.
 __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
@@ -759,10 +682,7 @@ void launch_path(const DScene *S, const Traversal &tv, const PathLaunch &L, bool
 }
 
 void launch_splat(const SplatLaunch &P, hipStream_t st) {
-    if (P.reach == 2 && P.border == 2)  // the default Gaussian (radius 2): tabulated per-sample weights
-        hipLaunchKernelGGL(nh_block_splat_r2_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
-    else
-        hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     dim3 grid((mcols + 15) / 16, (mrows + 15) / 16);
     hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, P);
