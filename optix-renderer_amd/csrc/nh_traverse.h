@@ -173,6 +173,24 @@ NHD bool box_test_finite(float mnx, float mny, float mnz, float mxx, float mxy, 
     return (near_t <= far_t) & (mint <= far_t) & (near_t <= maxt);
 }
 
+// box_test_finite for two boxes at once: the slab products in packed FP32 (component i = box i, the
+// same IEEE operations), the min / max reductions per box as box_test_finite does them
+NHD void box_test_finite_pair(f2 mnx, f2 mny, f2 mnz, f2 mxx, f2 mxy, f2 mxz, F3 o, F3 r, float mint, float maxt,
+                              bool &hit0, bool &hit1, float &near0, float &near1) {
+    const f2 ox{o.x, o.x}, oy{o.y, o.y}, oz{o.z, o.z}, rx{r.x, r.x}, ry{r.y, r.y}, rz{r.z, r.z};
+    const f2 ax = (mnx - ox) * rx, bx = (mxx - ox) * rx;
+    const f2 ay = (mny - oy) * ry, by = (mxy - oy) * ry;
+    const f2 az = (mnz - oz) * rz, bz = (mxz - oz) * rz;
+    const float n0 = fmaxf(fmaxf(fminf(ax.x, bx.x), fminf(ay.x, by.x)), fminf(az.x, bz.x));
+    const float f0 = fminf(fminf(fmaxf(ax.x, bx.x), fmaxf(ay.x, by.x)), fmaxf(az.x, bz.x));
+    const float n1 = fmaxf(fmaxf(fminf(ax.y, bx.y), fminf(ay.y, by.y)), fminf(az.y, bz.y));
+    const float f1 = fminf(fminf(fmaxf(ax.y, bx.y), fmaxf(ay.y, by.y)), fmaxf(az.y, bz.y));
+    near0 = n0;
+    near1 = n1;
+    hit0 = (n0 <= f0) & (mint <= f0) & (n0 <= maxt);
+    hit1 = (n1 <= f1) & (mint <= f1) & (n1 <= maxt);
+}
+
 // Sphere::rayIntersect (sphere.cpp:67-94)
 NHD bool sphere_test(float4 a, F3 o, F3 d, float mint, float maxt, float &t) {
     F3 L = sub(o, f3(a.x, a.y, a.z));
@@ -499,6 +517,10 @@ constexpr int kWideEmpty = (int)0x80000000;
 #ifndef NH_WIDE_PAIR
 #define NH_WIDE_PAIR 1
 #endif
+// the four child boxes of a wide node tested as two packed pairs (box_test_finite_pair)
+#ifndef NH_WIDE_PACKED_BOX
+#define NH_WIDE_PACKED_BOX 1
+#endif
 
 // Traversal stack of one lane, (ref, entry distance) pairs: the top K entries live in LDS
 // (lane-interleaved, `stride` words apart), deeper entries spill to the lane's own global area.
@@ -630,10 +652,21 @@ struct Tracer4 {
             float n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f;
             bool v0, v1, v2, v3;
             if (finite_r) {
+#if NH_WIDE_PACKED_BOX
+                box_test_finite_pair(f2{mnx.x, mnx.y}, f2{mny.x, mny.y}, f2{mnz.x, mnz.y}, f2{mxx.x, mxx.y},
+                                     f2{mxy.x, mxy.y}, f2{mxz.x, mxz.y}, o, r, mint, maxt, v0, v1, n0, n1);
+                box_test_finite_pair(f2{mnx.z, mnx.w}, f2{mny.z, mny.w}, f2{mnz.z, mnz.w}, f2{mxx.z, mxx.w},
+                                     f2{mxy.z, mxy.w}, f2{mxz.z, mxz.w}, o, r, mint, maxt, v2, v3, n2, n3);
+                v0 &= ref.x != kWideEmpty;
+                v1 &= ref.y != kWideEmpty;
+                v2 &= ref.z != kWideEmpty;
+                v3 &= ref.w != kWideEmpty;
+#else
                 v0 = box_test_finite(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, r, mint, maxt, n0) & (ref.x != kWideEmpty);
                 v1 = box_test_finite(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, r, mint, maxt, n1) & (ref.y != kWideEmpty);
                 v2 = box_test_finite(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, r, mint, maxt, n2) & (ref.z != kWideEmpty);
                 v3 = box_test_finite(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, r, mint, maxt, n3) & (ref.w != kWideEmpty);
+#endif
             } else {
                 v0 = ref.x != kWideEmpty && box_test(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, d, r, mint, maxt, n0);
                 v1 = ref.y != kWideEmpty && box_test(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, d, r, mint, maxt, n1);
