@@ -517,9 +517,10 @@ constexpr int kWideEmpty = (int)0x80000000;
 #ifndef NH_WIDE_PAIR
 #define NH_WIDE_PAIR 1
 #endif
-// the four child boxes of a wide node tested as two packed pairs (box_test_finite_pair)
+// the four child boxes of a wide node tested as two packed pairs (box_test_finite_pair): off, the
+// extra live registers spill at 5 waves/SIMD (bumpy-1M 1260 vs 1404 Msamples/s)
 #ifndef NH_WIDE_PACKED_BOX
-#define NH_WIDE_PACKED_BOX 1
+#define NH_WIDE_PACKED_BOX 0
 #endif
 
 // Traversal stack of one lane, (ref, entry distance) pairs: the top K entries live in LDS
