@@ -448,7 +448,7 @@ def main():
             "config": {"workload": f"{r['desc']}, {spp} spp, path_mis", "config": args.config,
                        "width": W, "height": H, "spp": spp, "rounds_per_step": R,
                        "mode": args.mode, "traversal": args.traversal,
-                       "pools": args.pools or int(os.environ.get("NH_POOLS", "0")) or "library default (4)",
+                       "pools": args.pools or int(os.environ.get("NH_POOLS", "0")) or "library default (2)",
                        "parallelism": (f"{par} + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce"
                                        if world > 1 else "single GPU"),
                        "bvh_build_s": round(r["bvh_s"], 3), "upload_s": round(r["upload_s"], 3)},

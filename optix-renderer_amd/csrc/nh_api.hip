@@ -33,10 +33,11 @@ using nhd::DShape;
 // ---- wavefront pipeline state (used by nh_render, see the pipeline section below) ----
 constexpr int kRing = 4;   // bounce-count copies in flight per pool
 // path pools in flight: while one drains its last bounces (long specular chains are a latency chain of
-// hundreds of bounces) the next ones fill the GPU; NH_POOLS=1..kPools overrides the default
+// hundreds of bounces) the next ones fill the GPU; NH_POOLS=1..kPools overrides the default (2 measured
+// best: C4 2134-2147 Msamples/s vs 1913-1938 at 3 pools and 2078-2092 at 4; C2 / bumpy-1M unchanged)
 constexpr int kPools = 4;
 #ifndef NH_DEFAULT_POOLS
-#define NH_DEFAULT_POOLS 4
+#define NH_DEFAULT_POOLS 2
 #endif
 constexpr int kMaxStack = 128;  // deepest per-lane LDS stack of the binary-tree kernels (DEPTH template)
 
