@@ -124,6 +124,14 @@ def pmc_traffic(workload_key):
     return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_traffic.json[{workload_key}]: {rec.get('source', '')}"
 
 
+def pmc_record(workload_key):
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(path)).get(workload_key) or {}
+    except (OSError, ValueError):
+        return {}
+
+
 def stage_work(calib):
     """Traversal work per stage from the calibration launch's in-kernel counters: the tail kernel
     counts into its own slots, so extend / shadow are those kernels' own visits."""
@@ -217,7 +225,21 @@ def roofline(args, calib, st, W, H, R):
             "lds_scene": lds, "queries_per_sample": round(calib["ray_queries"] / paths, 3),
             "splat_ms_per_launch": round(st["kernel_ms_splat"] / max(st["launches_splat"], 1), 4),
             "stages": report}
+    rec = pmc_record(key) if single else {}
+    if rec.get("valu_issue_frac") is not None and rec.get("kernel", "").split("<")[0] in kernel:
+        # what bounds the kernel, from the same committed PMC passes: VALU issue slots used (one wave64
+        # VALU instruction per CU per cycle) and the share of wave-cycles spent waiting
+        roof["limiter"] = {"valu_issue_frac": rec["valu_issue_frac"], "wait_frac": rec.get("wait_frac"),
+                           "valu_insts_per_launch": rec.get("valu_insts_per_launch"),
+                           "note": ("VALU-issue bound (the LDS-resident traversal and shading arithmetic), not HBM: "
+                                    "its HBM bytes are the path state only" if rec["valu_issue_frac"] > 0.6 else
+                                    "latency bound (waves waiting on dependent loads)"),
+                           "source": traffic_source_of(key)}
     return roof
+
+
+def traffic_source_of(key):
+    return f"profiles/pmc_traffic.json[{key}]"
 
 
 def traversal_record(roof):

@@ -16,7 +16,8 @@ root, key, pat = sys.argv[1:4]
 vals = defaultdict(list)
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if pat in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
+        if pat in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU",
+                                                             "GRBM_GUI_ACTIVE", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"]) * 2 * 1024
 write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"]) * 1024
@@ -25,5 +26,14 @@ data = json.load(open(out)) if os.path.exists(out) else {}
 data[key] = {"kernel": pat, "hbm_bytes_per_launch": int(fetch + write), "read_bytes_per_launch": int(fetch),
              "write_bytes_per_launch": int(write), "dispatches": len(vals["FETCH_SIZE"]),
              "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {os.path.basename(root)}"}
+avg = lambda k: sum(vals[k]) / len(vals[k]) if vals[k] else None  # noqa: E731
+if avg("SQ_INSTS_VALU") and avg("GRBM_GUI_ACTIVE"):
+    # VALU issue: one wave64 VALU instruction per cycle per CU (4 SIMDs x 1 per 4 cycles, MI355X_MICROARCH.md
+    # issue-cost table); GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles
+    cycles = avg("GRBM_GUI_ACTIVE") / 8
+    data[key]["valu_insts_per_launch"] = int(avg("SQ_INSTS_VALU"))
+    data[key]["valu_issue_frac"] = round(avg("SQ_INSTS_VALU") / (cycles * 256), 3)
+if avg("SQ_WAIT_ANY") and avg("SQ_WAVE_CYCLES"):
+    data[key]["wait_frac"] = round(avg("SQ_WAIT_ANY") / avg("SQ_WAVE_CYCLES"), 3)
 json.dump(data, open(out, "w"), indent=1, sort_keys=True)
 print(key, data[key])
