@@ -117,11 +117,8 @@ struct P3 {
 NHD P3 psub(P3 a, P3 b) { return P3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 NHD P3 pcross(P3 a, P3 b) { return P3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 NHD f2 pdot(P3 a, P3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
-NHD void tri_test_pair(float4 a0, float4 b0, float4 c0, float4 a1, float4 b1, float4 c1, F3 o, F3 d, float mint,
-                       f2 &t, f2 &u, f2 &v, bool &ok0, bool &ok1) {
-    const P3 p0{f2{a0.x, a1.x}, f2{a0.y, a1.y}, f2{a0.z, a1.z}};
-    const P3 p1{f2{b0.x, b1.x}, f2{b0.y, b1.y}, f2{b0.z, b1.z}};
-    const P3 p2{f2{c0.x, c1.x}, f2{c0.y, c1.y}, f2{c0.z, c1.z}};
+NHD void tri_test_pair_p(const P3 &p0, const P3 &p1, const P3 &p2, F3 o, F3 d, float mint, f2 &t, f2 &u, f2 &v,
+                         bool &ok0, bool &ok1) {
     const P3 po{f2{o.x, o.x}, f2{o.y, o.y}, f2{o.z, o.z}}, pd{f2{d.x, d.x}, f2{d.y, d.y}, f2{d.z, d.z}};
     const P3 e1 = psub(p1, p0), e2 = psub(p2, p0);
     const P3 pvec = pcross(pd, e2);
@@ -137,6 +134,13 @@ NHD void tri_test_pair(float4 a0, float4 b0, float4 c0, float4 a1, float4 b1, fl
           (t.x >= mint);
     ok1 = !(det.y > -1e-8f && det.y < 1e-8f) & !(u.y < 0.0f || u.y > 1.0f) & !(v.y < 0.0f || uv.y > 1.0f) &
           (t.y >= mint);
+}
+NHD void tri_test_pair(float4 a0, float4 b0, float4 c0, float4 a1, float4 b1, float4 c1, F3 o, F3 d, float mint,
+                       f2 &t, f2 &u, f2 &v, bool &ok0, bool &ok1) {
+    const P3 p0{f2{a0.x, a1.x}, f2{a0.y, a1.y}, f2{a0.z, a1.z}};
+    const P3 p1{f2{b0.x, b1.x}, f2{b0.y, b1.y}, f2{b0.z, b1.z}};
+    const P3 p2{f2{c0.x, c1.x}, f2{c0.y, c1.y}, f2{c0.z, c1.z}};
+    tri_test_pair_p(p0, p1, p2, o, d, mint, t, u, v, ok0, ok1);
 }
 
 // tri_test without early exits: the same predicates on the same values (so the same answer, NaNs
@@ -211,7 +215,13 @@ struct Traversal {
     const int2 *leaves;
     const float4 *prims;
     const float4 *wnodes;  // 4-wide collapse of the same tree (kWideF4 float4 per node), see Tracer4
+    // LDS-staged scenes (wf_bounce): records k and k+1 interleaved component by component, kPairF4 float4
+    // per k, so a primitive pair loads straight into packed-FP32 register pairs (leaf_test<.., PAIRS>)
+    const float4 *ppairs;
 };
+// pair k: (a.x a.x') (a.y a.y') | (a.z a.z') (a.w a.w') | (b.x b.x') (b.y b.y') | (b.z b.z') (c.x c.x') |
+//         (c.y c.y') (c.z c.z') | (c.w c.w') (0 0)      -- unprimed record k, primed record k+1
+constexpr int kPairF4 = 6;
 
 // primitive record type / leaf-end bits (word 2 .w of the record), and the BSDF type of the owning
 // shape in bits 2-3 (the material key of the sorted shade queues)
@@ -220,10 +230,48 @@ NHD bool prim_is_tri(float4 c) { return (__float_as_int(c.w) & kPrimSphere) == 0
 NHD int prim_material(float4 c) { return (__float_as_int(c.w) >> kPrimMatShift) & 3; }
 
 // Test the primitives of one leaf. Returns true when an any-hit query is answered.
-template <bool ANY, bool STATS>
+template <bool ANY, bool STATS, bool PAIRS = false>
 NHD bool leaf_test(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float &maxt, Hit &best, bool &found,
                    TravStats &st) {
     const int2 lf = tv.leaves[leaf];
+    if constexpr (PAIRS) {  // interleaved pair records: no AoS -> pair shuffles
+        for (int k = lf.x, e = lf.x + lf.y; k < e; k += 2) {
+            const float4 *pp = tv.ppairs + (size_t)kPairF4 * k;
+            const float4 q0 = pp[0], q1 = pp[1], q2 = pp[2], q3 = pp[3], q4 = pp[4], q5 = pp[5];
+            const P3 p0{f2{q0.x, q0.y}, f2{q0.z, q0.w}, f2{q1.x, q1.y}};
+            const P3 p1{f2{q2.x, q2.y}, f2{q2.z, q2.w}, f2{q3.x, q3.y}};
+            const P3 p2{f2{q3.z, q3.w}, f2{q4.x, q4.y}, f2{q4.z, q4.w}};
+            f2 pt, pu, pv;
+            bool ok0, ok1;
+            tri_test_pair_p(p0, p1, p2, o, d, mint, pt, pu, pv, ok0, ok1);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (j == 1 && k + 1 >= e) break;
+                if (STATS) st.prims++;
+                float t = j ? pt.y : pt.x, u = j ? pu.y : pu.x, v = j ? pv.y : pv.x;
+                const float cw = j ? q5.y : q5.x;
+                bool hit;
+                if ((__float_as_int(cw) & kPrimSphere) == 0) {
+                    hit = (j ? ok1 : ok0) && t <= maxt;
+                } else {
+                    u = v = 0.f;
+                    const float4 a = j ? make_float4(q0.y, q0.w, q1.y, q1.w) : make_float4(q0.x, q0.z, q1.x, q1.z);
+                    hit = sphere_test(a, o, d, mint, maxt, t);
+                }
+                if (!hit) continue;
+                if (ANY) return true;
+                if (t < maxt || k + j > best.k) {
+                    found = true;
+                    maxt = t;
+                    best.t = t;
+                    best.u = u;
+                    best.v = v;
+                    best.k = k + j;
+                }
+            }
+        }
+        return false;
+    }
     // primitives in pairs: both triangle tests in packed FP32 (tri_test_pair), then accepted in
     // order -- a hit of the first shrinks maxt before the second is bounded by it
     for (int k = lf.x, e = lf.x + lf.y; k < e; k += 2) {
@@ -272,7 +320,7 @@ NHD bool child_box_test(const float4 &n0, const float4 &n1, const float4 &n2, in
 // entries are `stride` words apart (lane-interleaved, bank-conflict free). An entry is
 // (parent inner node << 1) | side: the deferred child's box is tested again when it is
 // popped, with the maxt of that moment -- the reference's visit-time test verbatim.
-template <int DEPTH, bool ORDERED, bool ANY, bool STATS>
+template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool PAIRS = false>
 NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, float maxt, Hit &best, uint32_t *stk,
                int stride, TravStats &st) {
     // adaptive ray epsilon (bvh.cpp:407-410)
@@ -288,7 +336,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
                   mint, maxt, near_t))
         return false;
     if (S.root_kind == 2) {
-        bool any = leaf_test<ANY, STATS>(tv, 0, o, d, mint, maxt, best, found, st);
+        bool any = leaf_test<ANY, STATS, PAIRS>(tv, 0, o, d, mint, maxt, best, found, st);
         return ANY ? any : found;
     }
     int sp = 0;
@@ -318,7 +366,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
                 cur = next;
                 continue;
             }
-            if (leaf_test<ANY, STATS>(tv, ~next, o, d, mint, maxt, best, found, st)) return true;
+            if (leaf_test<ANY, STATS, PAIRS>(tv, ~next, o, d, mint, maxt, best, found, st)) return true;
             break;
         }
         // pop: re-test the deferred child against the current maxt
@@ -336,7 +384,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
                 cur = ref;
                 break;
             }
-            if (leaf_test<ANY, STATS>(tv, ~ref, o, d, mint, maxt, best, found, st)) return true;
+            if (leaf_test<ANY, STATS, PAIRS>(tv, ~ref, o, d, mint, maxt, best, found, st)) return true;
         }
         if (cur < 0) break;
     }

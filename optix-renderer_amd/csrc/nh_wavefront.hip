@@ -158,20 +158,48 @@ __device__ __forceinline__ void load_ray(const DScene &S, const WfLaunch &L, con
 }
 
 
+// float4 offset of the pair table in the dynamic LDS of a small scene (after nodes, primitives, leaves)
+__host__ __device__ __forceinline__ int small_pairs_offset_f4(const WfLaunch &L) {
+    return L.small_nodes + L.small_prims + (L.small_leaves + 1) / 2;
+}
+
 // Stage a small BVH (nodes, leaf table, primitives) into dynamic LDS and return a traversal view
 // of the copy. Instantiated only for SMALL kernels, so every traversal pointer derives from the
 // __shared__ array: the compiler emits ds_read, not flat loads. Called by the whole workgroup.
+// PAIRS: also the pair-interleaved copy of the primitive records (Traversal::ppairs, kPairF4 float4 per
+// record, after the leaf table; record n_prims = zeros).
+template <bool PAIRS = false>
 __device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, const WfLaunch &L, float4 *lds) {
     float4 *nodes = lds, *prims = lds + L.small_nodes;
     int2 *leaves = reinterpret_cast<int2 *>(prims + L.small_prims);
     for (int i = threadIdx.x; i < L.small_nodes; i += blockDim.x) nodes[i] = tv.nodes[i];
     for (int i = threadIdx.x; i < L.small_prims; i += blockDim.x) prims[i] = tv.prims[i];
     for (int i = threadIdx.x; i < L.small_leaves; i += blockDim.x) leaves[i] = tv.leaves[i];
-    __syncthreads();
     Traversal t;
     t.nodes = nodes;
     t.prims = prims;
     t.leaves = leaves;
+    t.ppairs = nullptr;
+    if constexpr (PAIRS) {
+        float4 *pairs = lds + small_pairs_offset_f4(L);
+        const int n = L.small_prims / 3;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = threadIdx.x; k < n; k += blockDim.x) {
+            const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
+            const bool nx = k + 1 < n;
+            const float4 a1 = nx ? tv.prims[3 * k + 3] : z, b1 = nx ? tv.prims[3 * k + 4] : z,
+                         c1 = nx ? tv.prims[3 * k + 5] : z;
+            float4 *q = pairs + (size_t)kPairF4 * k;
+            q[0] = make_float4(a.x, a1.x, a.y, a1.y);
+            q[1] = make_float4(a.z, a1.z, a.w, a1.w);
+            q[2] = make_float4(b.x, b1.x, b.y, b1.y);
+            q[3] = make_float4(b.z, b1.z, c.x, c1.x);
+            q[4] = make_float4(c.y, c1.y, c.z, c1.z);
+            q[5] = make_float4(c.w, c1.w, 0.f, 0.f);
+        }
+        t.ppairs = pairs;
+    }
+    __syncthreads();
     return t;
 }
 
@@ -662,7 +690,7 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce(const DScene *
     const int base = blockIdx.x * 256;
     if (base >= qv.n) return;  // whole workgroup
     if (threadIdx.x < kMatClasses) s_n[threadIdx.x] = 0u;  // visible after the staging barrier
-    const Traversal tv = stage_small_scene(tv_g, L, lds_scene);
+    const Traversal tv = stage_small_scene<true>(tv_g, L, lds_scene);
     // gridDim.x is a multiple of kQueueShards: shard s receives the chunks c = s (mod 8), at most
     // seg_cap entries (as wf_shade)
     const int shard = blockIdx.x & (kQueueShards - 1);
@@ -684,7 +712,7 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce(const DScene *
             Hit h;
             const bool live = rd.w >= ro.w;
             q_e += live ? 1 : 0;
-            const bool found = live && trace<16, ORDERED, false, STATS>(tv, S, xyz(ro), xyz(rd), ro.w, rd.w, h,
+            const bool found = live && trace<16, ORDERED, false, STATS, true>(tv, S, xyz(ro), xyz(rd), ro.w, rd.w, h,
                                                                         my_stk, 256, st_e);
             hv = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
         } else {
@@ -697,7 +725,7 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce(const DScene *
             if (nee) {  // the light sample's any-hit query (wf_shadow), its outcome applied as shade_path would
                 Hit hs;
                 ++q_s;
-                if (!trace<16, ORDERED, true, STATS>(tv, S, xyz(so), xyz(sd), so.w, sd.w, hs, my_stk, 256, st_s)) {
+                if (!trace<16, ORDERED, true, STATS, true>(tv, S, xyz(so), xyz(sd), so.w, sd.w, hs, my_stk, 256, st_s)) {
                     o.li.x = o.li.x + o.pe.x;
                     o.li.y = o.li.y + o.pe.y;
                     o.li.z = o.li.z + o.pe.z;
@@ -712,7 +740,14 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce(const DScene *
             Hit h;  // the next ray's closest hit (wf_extend)
             const bool live = o.rd.w >= o.ro.w;
             q_e += live ? 1 : 0;
-            const bool found = live && trace<16, ORDERED, false, STATS>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h,
+#ifdef NH_EXPERIMENT_TRACE_TWICE  // cost attribution only: the closest-hit query runs twice (same answer)
+            {
+                Hit h2;
+                if (live && trace<16, ORDERED, false, STATS, true>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h2, my_stk, 256, st_e))
+                    o.rng ^= (uint64_t)(h2.k == -7);
+            }
+#endif
+            const bool found = live && trace<16, ORDERED, false, STATS, true>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h,
                                                                         my_stk, 256, st_e);
             hit_out = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
             if (found) cls = prim_material(tv.prims[3 * h.k + 2]);
@@ -899,7 +934,7 @@ void launch_wf_bounce(const DScene *S, const Traversal &tv, const WfLaunch &L, b
                       int bound, hipStream_t st) {
     int blocks = std::max(1, (bound + 255) / 256);
     blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
-    const size_t lds = 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves;
+    const size_t lds = 16 * ((size_t)small_pairs_offset_f4(L) + (size_t)kPairF4 * (L.small_prims / 3));
 #define NH_FB(O, T, SO) hipLaunchKernelGGL((wf_bounce<O, T, SO>), dim3(blocks), dim3(256), lds, st, S, tv, L)
     if (ordered) {
         if (stats) { if (sort) NH_FB(true, true, true); else NH_FB(true, true, false); }
