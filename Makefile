@@ -32,7 +32,7 @@ HOSTLIB  := $(LIBDIR)/libnori_host.so
 ORACLE   := oracle/_build/libnori_oracle.so
 CLI      := $(LIBDIR)/nori_hip
 
-RCPCHECK := tools/bin/rcp_exhaustive tools/bin/div_check
+RCPCHECK := tools/bin/rcp_exhaustive
 
 MANUAL   := tests/c/bin/manual_scene
 
@@ -46,7 +46,7 @@ $(MANUAL): tests/c/manual_scene.c $(LIB) $(ORACLE) include/nori_hip.h oracle/nor
 	    -lm -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../../../oracle/_build'
 
 # exhaustive check of the fast reciprocal the traversal kernels use (run by the GPU tests)
-tools/bin/%: tools/%.hip $(HIP_DEPS)
+$(RCPCHECK): tools/rcp_exhaustive.hip $(HIP_DEPS)
 	@mkdir -p tools/bin
 	$(HIPCC) $(HIP_FLAGS) -o $@ $<
 

@@ -62,35 +62,6 @@ NHD float f_log(float x) { return (float)log((double)x); }
 NHD float f_acos(float x) { return (float)acos((double)x); }
 NHD float f_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
 NHD float f_sqrt(float x) { return __builtin_sqrtf(x); }  // correctly rounded (HIP default)
-
-// Correctly rounded 1/x in 3 instructions: the hardware estimate (within 1 ulp) and one FMA Newton step.
-// Equal to `1.0f / x` for every |x| in [2^-125, 2^126) -- all 2^32 inputs checked on gfx950
-// (tools/rcp_exhaustive.hip, run by test_fast_reciprocal_exhaustive); callers keep `1.0f / x` outside.
-NHD float rcp_rn(float x) {
-    const float r = __builtin_amdgcn_rcpf(x);
-    const float e = __builtin_fmaf(-x, r, 1.0f);
-    return __builtin_fmaf(e, r, r);
-}
-// Correctly rounded a / b from r = rcp_rn(b): q = a*r is within 1 ulp of a/b, the FMA residual a - b*q is
-// exact, and one correction q + (a - b*q)*r rounds to a/b (Markstein's theorem, no over/underflow on the
-// way); a zero a keeps a*r, whose sign is a/b's. Valid for |a| in {0} u [2^-40, 2^40] and |b| in
-// [2^-40, 2^40] (fdiv_ok: the residual then stays far from underflow). Checked against the division on
-// 2^31 (a, b) pairs covering every significand of b, random a, exact zeros and both signs
-// (tools/div_check.hip, run by test_fast_division).
-NHD bool fdiv_ok(float a, float b) {
-    const float fa = fabsf(a), fb = fabsf(b);
-    return fa <= 0x1p40f && (fa >= 0x1p-40f || fa == 0.f) && fb >= 0x1p-40f && fb <= 0x1p40f;
-}
-NHD float fdiv_r(float a, float b, float r) {
-    const float q = a * r;
-    const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
-    return a == 0.f ? q : q1;
-}
-// a / b, correctly rounded (the fast path when fdiv_ok, else the division)
-NHD float fdiv(float a, float b) {
-    if (__builtin_expect(fdiv_ok(a, b), 1)) return fdiv_r(a, b, rcp_rn(b));
-    return a / b;
-}
 NHD float e_min(float a, float b) { return (b < a) ? b : a; }  // std::min
 NHD float e_max(float a, float b) { return (a < b) ? b : a; }  // std::max
 
@@ -103,18 +74,15 @@ NHD F3 sub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
 NHD F3 neg(F3 a) { return f3(-a.x, -a.y, -a.z); }
 NHD F3 scl(float s, F3 a) { return f3(s * a.x, s * a.y, s * a.z); }
 NHD F3 mulc(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, a.z * b.z); }
-NHD F3 divs(F3 a, float s) {  // a / s per component, correctly rounded (one reciprocal for the three)
-    if (__builtin_expect(fdiv_ok(a.x, s) && fdiv_ok(a.y, s) && fdiv_ok(a.z, s), 1)) {
-        const float r = rcp_rn(s);
-        return f3(fdiv_r(a.x, s, r), fdiv_r(a.y, s, r), fdiv_r(a.z, s, r));
-    }
-    return f3(a.x / s, a.y / s, a.z / s);
-}
+NHD F3 divs(F3 a, float s) { return f3(a.x / s, a.y / s, a.z / s); }
 NHD float dot(F3 a, F3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
 NHD F3 cross(F3 a, F3 b) { return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
 NHD F3 normalized(F3 a) {
     float n = dot(a, a);
-    if (n > 0.0f) return divs(a, f_sqrt(n));
+    if (n > 0.0f) {
+        float s = f_sqrt(n);
+        return f3(a.x / s, a.y / s, a.z / s);
+    }
     return a;
 }
 NHD float max_coeff(F3 c) { return e_max(c.x, e_max(c.y, c.z)); }
@@ -222,10 +190,10 @@ NHD Frame frame_from_n(F3 a) {
     f.n = a;
     F3 c;
     if (fabsf(a.x) > fabsf(a.y)) {
-        float inv_len = fdiv(1.0f, f_sqrt(a.x * a.x + a.z * a.z));
+        float inv_len = 1.0f / f_sqrt(a.x * a.x + a.z * a.z);
         c = f3(a.z * inv_len, 0.0f, -a.x * inv_len);
     } else {
-        float inv_len = fdiv(1.0f, f_sqrt(a.y * a.y + a.z * a.z));
+        float inv_len = 1.0f / f_sqrt(a.y * a.y + a.z * a.z);
         c = f3(0.0f, a.z * inv_len, -a.y * inv_len);
     }
     f.t = c;
@@ -243,12 +211,12 @@ NHD float fresnel(float cos_i, float ext_ior, float int_ior) {
         float tmp = eta_i; eta_i = eta_t; eta_t = tmp;
         cos_i = -cos_i;
     }
-    float eta = fdiv(eta_i, eta_t), sin_t2 = eta * eta * (1 - cos_i * cos_i);
+    float eta = eta_i / eta_t, sin_t2 = eta * eta * (1 - cos_i * cos_i);
     if (sin_t2 > 1.0f) return 1.0f;
     float cos_t = f_sqrt(1.0f - sin_t2);
-    float rs = fdiv(eta_i * cos_i - eta_t * cos_t, eta_i * cos_i + eta_t * cos_t);
-    float rp = fdiv(eta_t * cos_i - eta_i * cos_t, eta_t * cos_i + eta_i * cos_t);
-    return fdiv(rs * rs + rp * rp, 2.0f);
+    float rs = (eta_i * cos_i - eta_t * cos_t) / (eta_i * cos_i + eta_t * cos_t);
+    float rp = (eta_t * cos_i - eta_i * cos_t) / (eta_t * cos_i + eta_i * cos_t);
+    return (rs * rs + rp * rp) / 2.0f;
 }
 
 // ---- warps (warp.cpp) -------------------------------------------------------------
@@ -265,7 +233,7 @@ NHD F3 beckmann(float sx, float sy, float alpha) {  // warp.cpp:131-150
     if (isinf(ls)) ls = 0;
     float tan2 = -alpha * alpha * ls;
     float phi = sy * 2.f * kPi;
-    float ct = fdiv(1.f, f_sqrt(1 + tan2));
+    float ct = 1.f / f_sqrt(1 + tan2);
     float st = f_sqrt(1.f - ct * ct);
     float sphi, cphi;
     f_sincos(phi, sphi, cphi);
@@ -289,20 +257,20 @@ NHD F3 uniform_sphere(float sx, float sy) {  // warp.cpp:74-82
 NHD float tan_theta(F3 v) {
     float temp = 1 - v.z * v.z;
     if (temp <= 0.0f) return 0.0f;
-    return fdiv(f_sqrt(temp), v.z);
+    return f_sqrt(temp) / v.z;
 }
 NHD float beckmann_d(const DBsdf &b, F3 m) {  // microfacet.cpp:60-66
-    float temp = fdiv(tan_theta(m), b.alpha), ct = m.z, ct2 = ct * ct;
-    return fdiv(f_exp(-temp * temp), kPi * b.alpha * b.alpha * ct2 * ct2);
+    float temp = tan_theta(m) / b.alpha, ct = m.z, ct2 = ct * ct;
+    return f_exp(-temp * temp) / (kPi * b.alpha * b.alpha * ct2 * ct2);
 }
 NHD float smith_g1(const DBsdf &b, F3 v, F3 m) {  // microfacet.cpp:69-89
     float tt = tan_theta(v);
     if (tt == 0.0f) return 1.0f;
     if (dot(m, v) * v.z <= 0) return 0.0f;
-    float a = fdiv(1.0f, b.alpha * tt);
+    float a = 1.0f / (b.alpha * tt);
     if (a >= 1.6f) return 1.0f;
     float a2 = a * a;
-    return fdiv(3.535f * a + 2.181f * a2, 1.0f + 2.276f * a + 2.577f * a2);
+    return (3.535f * a + 2.181f * a2) / (1.0f + 2.276f * a + 2.577f * a2);
 }
 NHD F3 bsdf_eval(const DBsdf &b, F3 wi, F3 wo, int measure) {
     if (b.type == BSDF_DIFFUSE) {  // diffuse.cpp:94-103
@@ -315,7 +283,7 @@ NHD F3 bsdf_eval(const DBsdf &b, F3 wi, F3 wo, int measure) {
         float den = b.ks * beckmann_d(b, wh) * fresnel(dot(wh, wi), b.ext_ior, b.int_ior) * smith_g1(b, wi, wh) *
                     smith_g1(b, wo, wh);
         float num = 4.f * wi.z * wo.z;
-        float spec = fdiv(den, num);
+        float spec = den / num;
         return f3(b.kr * kInvPi + spec, b.kg * kInvPi + spec, b.kb * kInvPi + spec);
     }
     return f3(0, 0, 0);
@@ -328,7 +296,7 @@ NHD float bsdf_pdf(const DBsdf &b, F3 wi, F3 wo, int measure) {
     if (b.type == BSDF_MICROFACET) {  // microfacet.cpp:108-119
         if (wo.z <= 0) return 0.f;
         F3 wh = normalized(add(wo, wi));
-        float p1 = fdiv(b.ks * beckmann_d(b, wh) * wh.z, 4.f * dot(wo, wh));
+        float p1 = b.ks * beckmann_d(b, wh) * wh.z / (4.f * dot(wo, wh));
         float p2 = (1.f - b.ks) * wo.z * kInvPi;
         return p1 + p2;
     }
@@ -360,9 +328,9 @@ NHD F3 bsdf_sample(const DBsdf &b, F3 wi, float sx, float sy, F3 &wo, int &measu
             float eta;
             if (wi.z < 0.f) {
                 nrm = neg(nrm);
-                eta = fdiv(b.int_ior, b.ext_ior);
+                eta = b.int_ior / b.ext_ior;
             } else {
-                eta = fdiv(b.ext_ior, b.int_ior);
+                eta = b.ext_ior / b.int_ior;
             }
             float dn = dot(wi, nrm);
             F3 wt1 = scl(-eta, sub(wi, scl(dn, nrm)));
@@ -370,25 +338,24 @@ NHD F3 bsdf_sample(const DBsdf &b, F3 wi, float sx, float sy, F3 &wo, int &measu
             double root = sqrt(1.0 - (double)(eta * eta) * (1.0 - p2));
             F3 wt2 = scl((float)(-root), nrm);
             wo = add(wt1, wt2);
-            float w = fdiv(fdiv(1.f, eta), eta);
+            float w = 1.f / eta / eta;
             return f3(w, w, w);
         }
         case BSDF_MICROFACET: {  // microfacet.cpp:122-148
             if (wi.z < 0) return f3(0, 0, 0);
             float s1 = sy;
             if (s1 < b.ks) {
-                s1 = fdiv(s1, b.ks);
+                s1 /= b.ks;
                 F3 wh = beckmann(sx, s1, b.alpha);
                 wo = sub(scl(2.f, scl(dot(wi, wh), wh)), wi);
             } else {
-                s1 = fdiv(s1 - b.ks, 1.f - b.ks);
+                s1 = (s1 - b.ks) / (1.f - b.ks);
                 wo = cosine_hemisphere(sx, s1);
             }
             if (wo.z <= 0.f) return f3(0, 0, 0);
             F3 e = bsdf_eval(b, wi, wo, M_UNKNOWN);
             float p = bsdf_pdf(b, wi, wo, M_UNKNOWN);
-            const F3 ep = divs(e, p);
-            return f3(ep.x * wo.z, ep.y * wo.z, ep.z * wo.z);
+            return f3(e.x / p * wo.z, e.y / p * wo.z, e.z / p * wo.z);
         }
     }
     return f3(0, 0, 0);

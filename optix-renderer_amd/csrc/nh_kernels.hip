@@ -82,7 +82,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
             li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
                         ems_col.z * cs * f.z * n_lights);
             pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
-            pdfems = fdiv(emitter_pdf(S, em, its.p, es.p, es.n, es.wi), n_lights);
+            pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
         }
         // BSDF sampling (path_mis.cpp:109-113)
         const float bx = rng.next1d(), by = rng.next1d();
@@ -111,7 +111,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
                 pdfems_mats = 0.f;
             }
         }
-        if ((pdfems_mats + pdfems) > kEps) w_ems = fdiv(pdfems, pdfems_mats + pdfems);
+        if ((pdfems_mats + pdfems) > kEps) w_ems = pdfems / (pdfems_mats + pdfems);
 
         // probe ray == next bounce (path_mis.cpp:115-146); a zero direction misses every
         // primitive (det == 0 / NaN roots), so its traversal is skipped
@@ -129,8 +129,8 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
                 hit_info(S, tv, h, no, nd, its_s);
                 const DEmitter em2 = S.emitters[hem];
                 const F3 wim = normalized(sub(its_s.p, no));
-                const float pdfmat_ems = fdiv(emitter_pdf(S, em2, no, its_s.p, its_s.sh.n, wim), n_lights);
-                if ((pdfmat + pdfmat_ems) > kEps) w_mats = fdiv(pdfmat, pdfmat + pdfmat_ems);
+                const float pdfmat_ems = emitter_pdf(S, em2, no, its_s.p, its_s.sh.n, wim) / n_lights;
+                if ((pdfmat + pdfmat_ems) > kEps) w_mats = pdfmat / (pdfmat + pdfmat_ems);
             }
         }
         if (measure == M_DISCRETE) {
@@ -341,7 +341,7 @@ __device__ F3 li_direct_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o
             const F3 we = to_local(its.sh, es.wi);
             const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
             const float cs = we.z;
-            const float pdf_ems = fdiv(emitter_pdf(S, em, its.p, es.p, es.n, es.wi), n_lights);
+            const float pdf_ems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
             const float pdf_mat = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
             result_ems = f3(li.x * cs * f.x * n_lights, li.y * cs * f.y * n_lights, li.z * cs * f.z * n_lights);
             if (pdf_ems + pdf_mat > kEps) w_ems = pdf_ems / (pdf_ems + pdf_mat);

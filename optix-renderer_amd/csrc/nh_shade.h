@@ -126,13 +126,13 @@ __device__ __forceinline__ float emitter_pdf(const DScene &S, const DEmitter &e,
     float prob = sh.type == SHAPE_MESH
                      ? sh.pdf_norm
                      : (float)((double)(1.f / sh.radius) * (double)(1.f / sh.radius) * (double)(0.25f / kPi));
-    return fdiv(prob * dot(sub(p, ref), sub(p, ref)), fabsf(dot(n, neg(wi))));
+    return prob * dot(sub(p, ref), sub(p, ref)) / fabsf(dot(n, neg(wi)));
 }
 __device__ __forceinline__ F3 emitter_eval(const DEmitter &e, F3 ref, F3 n, F3 wi) {
     if (e.type == EMITTER_POINT) {
         F3 dd = sub(ref, f3(e.px, e.py, e.pz));
         float q = dot(dd, dd);
-        return divs(f3(e.lr, e.lg, e.lb), q);
+        return f3(e.lr / q, e.lg / q, e.lb / q);
     }
     if (dot(n, neg(wi)) < 0.f) return f3(0, 0, 0);
     return f3(e.lr, e.lg, e.lb);
@@ -162,7 +162,7 @@ __device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e,
         const float pdf = env_pdf(S, es.wi);
         if (pdf < kEps) return f3(0, 0, 0);
         const F3 ev = env_eval(S, es.wi);
-        return divs(ev, pdf);
+        return f3(ev.x / pdf, ev.y / pdf, ev.z / pdf);
     }
     if (e.type == EMITTER_POINT) {
         F3 pos = f3(e.px, e.py, e.pz);
@@ -181,7 +181,7 @@ __device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e,
     if (sh.type == SHAPE_MESH) {  // Mesh::sampleSurface (mesh.cpp:50-71)
         const float *cdf = S.area_cdf + sh.pdf_off;
         int idt = dpdf_sample(cdf, sh.n_faces, sx);
-        sx = fdiv(sx - cdf[idt], cdf[idt + 1] - cdf[idt]);
+        sx = (sx - cdf[idt]) / (cdf[idt + 1] - cdf[idt]);
         float su1 = f_sqrt(sx);  // squareToUniformTriangle (warp.cpp:162-166)
         float bu = 1.f - su1, bv = sy * su1, bw = 1.f - bu - bv;
         const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + idt);
@@ -208,7 +208,7 @@ __device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e,
     float probs = emitter_pdf(S, e, ref, p, n, es.wi);
     if (fabsf(probs) < kEps) return f3(0, 0, 0);
     F3 ev = emitter_eval(e, ref, n, es.wi);
-    return divs(ev, probs);
+    return f3(ev.x / probs, ev.y / probs, ev.z / probs);
 }
 
 // PerspectiveCamera::sampleRay without depth of field (perspective.cpp:97-141)
@@ -224,7 +224,7 @@ __device__ __forceinline__ void camera_ray(const DScene &S, float px, float py, 
         acc = acc + S.s2c[4 * i + 3] * 1.0f;
         r[i] = acc;
     }
-    F3 dl = normalized(divs(f3(r[0], r[1], r[2]), r[3]));
+    F3 dl = normalized(f3(r[0] / r[3], r[1] / r[3], r[2] / r[3]));
     float ow[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -234,11 +234,11 @@ __device__ __forceinline__ void camera_ray(const DScene &S, float px, float py, 
         acc = acc + S.c2w[4 * i + 3] * 1.0f;
         ow[i] = acc;
     }
-    o = divs(f3(ow[0], ow[1], ow[2]), ow[3]);
+    o = f3(ow[0] / ow[3], ow[1] / ow[3], ow[2] / ow[3]);
     const float *w = S.c2w;
     d = f3(w[0] * dl.x + (w[1] * dl.y + w[2] * dl.z), w[4] * dl.x + (w[5] * dl.y + w[6] * dl.z),
            w[8] * dl.x + (w[9] * dl.y + w[10] * dl.z));
-    const float inv_z = fdiv(1.0f, dl.z);
+    const float inv_z = 1.0f / dl.z;
     mint = S.near_clip * inv_z;
     maxt = S.far_clip * inv_z;
 }

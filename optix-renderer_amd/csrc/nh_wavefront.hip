@@ -517,8 +517,8 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
                 if (hem >= 0) {
                     const float pdfmat = ro.w;
                     const F3 wim = normalized(sub(its.p, org));
-                    const float pdfmat_ems = fdiv(emitter_pdf(S, S.emitters[hem], org, its.p, its.sh.n, wim), n_lights);
-                    if ((pdfmat + pdfmat_ems) > kEps) w_mats = fdiv(pdfmat, pdfmat + pdfmat_ems);
+                    const float pdfmat_ems = emitter_pdf(S, S.emitters[hem], org, its.p, its.sh.n, wim) / n_lights;
+                    if ((pdfmat + pdfmat_ems) > kEps) w_mats = pdfmat / (pdfmat + pdfmat_ems);
                 }
             }
             if (flags & F_DISCRETE) w_mats = 1.f;  // :136-140
@@ -556,7 +556,7 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
                     li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
                                 ems_col.z * cs * f.z * n_lights);
                     pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
-                    pdfems = fdiv(emitter_pdf(S, em, its.p, es.p, es.n, es.wi), n_lights);
+                    pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
                     so = make_float4(es.so.x, es.so.y, es.so.z, es.smint);
                     sd = make_float4(es.sd.x, es.sd.y, es.sd.z, es.smaxt);
                 }
@@ -571,7 +571,7 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
                 // it either way (:136-140)
                 const bool discrete = measure == M_DISCRETE;
                 float w_occ = w_ems, w_un = w_ems;
-                if (nee && (pdfems_mats + pdfems) > kEps) w_un = fdiv(pdfems, pdfems_mats + pdfems);
+                if (nee && (pdfems_mats + pdfems) > kEps) w_un = pdfems / (pdfems_mats + pdfems);
                 if (discrete) w_occ = w_un = 0.f;
                 int fl = (discrete ? F_DISCRETE : 0) | (is_zero(bsdf_col) ? F_ZERO_COL : 0);
                 if (nee && discrete) {

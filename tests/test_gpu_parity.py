@@ -466,15 +466,3 @@ def test_manual_scene_description_through_cabi(gpu):
     print(r.stdout.strip(), r.stderr.strip())
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bit-identical 1" in r.stdout
-
-
-def test_fast_division(gpu):
-    """nhd::fdiv (rcp_rn + one FMA correction, the shading code's a / b) equals the correctly rounded
-    division on 2^31 pairs covering every significand of b with random a, zeros, +-1 quotients and range
-    limits, and falls back to the division outside its range (tools/div_check.hip, built by `make`)."""
-    import subprocess
-    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "bin", "div_check")
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
-    print(r.stdout.strip())
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert " mismatches 0 " in r.stdout
