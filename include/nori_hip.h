@@ -23,6 +23,10 @@
  *                         and the OptiX subframe launch (include/nori/optix/OptixState.cpp:485-510)
  *   nh_get_framebuffer    ImageBlock master (src/utils/block.cpp:38-134); toBitmap is nh_framebuffer_to_rgb
  *   nh_reduce_framebuffers  (new) RCCL sum of per-GPU RGBW framebuffers over xGMI
+ *   nh_denoise            Denoiser::denoise on the master ImageBlock after the render loop
+ *                         (src/utils/render.cpp:368-369): SimpleDenoiser (src/denoiser/simple.cpp:29-76,
+ *                         computeVarianceFromImage src/utils/common.cpp:339-398); the GPU counterpart of
+ *                         OptixState::denoise (include/nori/optix/OptixState.denoiser.cpp:123-150)
  *
  * Conventions (mirroring the reference's threading contract):
  *   - input pointers are host-owned and only read during the call;
@@ -130,6 +134,18 @@ typedef struct nh_envmap {
     float normalization;          /* DiscretePDF::getNormalization() */
 } nh_envmap;
 
+/* <denoiser> of the scene (Scene::m_denoiser, src/utils/scene.cpp:242-245): SimpleDenoiser's parameters after
+ * its constructor's clamps (src/denoiser/simple.cpp:15-24): sigma_d = clamp(sigma_d [0], Epsilon, 10),
+ * sigma_vr = clamp(sigma_vr [0.6], Epsilon, 10), range = clamp(range [1], 0, 50), amount = clamp(amount [1], 1, 10) */
+enum { NH_DENOISER_NONE = 0, NH_DENOISER_SIMPLE = 1 };
+typedef struct nh_denoiser {
+    int32_t type;            /* NH_DENOISER_* */
+    float sigma_d;           /* spatial Gaussian sigma (pixels) */
+    float sigma_vr;          /* range sigma of the variance-scaled L1 colour distance */
+    int32_t range;           /* window half-size: (2 range + 1)^2 pixels */
+    int32_t amount;          /* passes */
+} nh_denoiser;
+
 typedef struct nh_scene_desc {
     nh_camera camera;
     nh_filter filter;
@@ -154,6 +170,7 @@ typedef struct nh_scene_desc {
     uint32_t n_area_cdf;
     const float *area_cdf;        /* concatenated per-mesh area CDFs */
     nh_envmap env;                /* valid when envmap >= 0 */
+    nh_denoiser denoiser;         /* type NH_DENOISER_NONE when the scene has none */
 } nh_scene_desc;
 
 /* ---- BVH in the reference's own layout (include/nori/bvh.h:127-165) ---- */
@@ -252,6 +269,9 @@ typedef struct nh_render_stats {
     /* RCCL communicator cliques created by nh_reduce_framebuffers with this context as root (a clique
        is reused while the same contexts reduce again) */
     uint64_t comm_inits;
+    /* nh_denoise / nh_denoise_image: summed device time and kernel launches */
+    double kernel_ms_denoise;
+    uint64_t launches_denoise;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;
@@ -308,6 +328,16 @@ int nh_reset_stats(nh_ctx *ctx);
    a one-rank reduce). The communicator clique is created on the first call for a set of contexts and
    reused by later calls with the same contexts in the same order; it is destroyed with the contexts. */
 int nh_reduce_framebuffers(nh_ctx **ctxs, int32_t n, int32_t root);
+/* SimpleDenoiser::denoise (src/denoiser/simple.cpp:29-76) in place on the context's master ImageBlock (its
+   interior W x H pixels; the border is left as is), after completing every submitted render. The pixels are
+   updated in the row-major order of the reference's loops -- a pixel reads the already denoised values of
+   the pixels before it and the previous pass's values of the others -- which is what the reference computes
+   with one TBB thread (with more, its rows race). params->type must be NH_DENOISER_SIMPLE, the other fields
+   within the constructor's clamps. Finite framebuffer values are assumed (ImageBlock::put drops the others). */
+int nh_denoise(nh_ctx *ctx, const nh_denoiser *params);
+/* the same on a caller's host ImageBlock: (width + 2 border) x (height + 2 border) x 4 floats, in place */
+int nh_denoise_image(nh_ctx *ctx, float *rgbw, int32_t width, int32_t height, int32_t border,
+                     const nh_denoiser *params);
 const char *nh_last_error(const nh_ctx *ctx);
 
 #ifdef __cplusplus

@@ -1370,6 +1370,124 @@ int nh_reset_stats(nh_ctx *c) {
     return NH_OK;
 }
 
+// SimpleDenoiser on a device ImageBlock (nh_denoise.hip): `amount` passes, each the raw variance + its
+// max / min, then the banded wavefront schedule of the in-place row-major sweep. Scratch is per call.
+static int run_denoise(nh_ctx *c, float *fb, int W, int H, int bs, const nh_denoiser *p) {
+    if (!p || p->type != NH_DENOISER_SIMPLE) return fail(c, "denoise: type must be NH_DENOISER_SIMPLE"), NH_ERR_INVALID;
+    // SimpleDenoiser's constructor clamps (simple.cpp:15-24): anything outside is not a reference configuration
+    if (!(p->sigma_d >= 1e-4f && p->sigma_d <= 10.f) || !(p->sigma_vr >= 1e-4f && p->sigma_vr <= 10.f) ||
+        p->range < 0 || p->range > 50 || p->amount < 1 || p->amount > 10)
+        return fail(c, "denoise: parameters outside SimpleDenoiser's clamps"), NH_ERR_INVALID;
+    if (W <= 0 || H <= 0 || bs < 0) return fail(c, "denoise: empty image"), NH_ERR_INVALID;
+    const int r = p->range, cols = W + 2 * bs;
+    // g_sigma (simple.cpp:136-139) depends only on the squared pixel distance: the reference's float expf per
+    // distance, tabulated
+    std::vector<float> g((size_t)2 * r * r + 1);
+    for (size_t d = 0; d < g.size(); ++d) g[d] = std::exp((float)-(int)d / 2.f / p->sigma_d / p->sigma_d);
+    std::vector<void *> tmp;
+    struct Free {
+        std::vector<void *> &v;
+        ~Free() { free_all(v); }
+    } guard{tmp};
+    float4 *B = nullptr;
+    float *var = nullptr, *dg = nullptr;
+    unsigned *minmax = nullptr;
+    HIP_TRY(c, hipMalloc(&B, (size_t)W * H * sizeof(float4)));
+    tmp.push_back(B);
+    HIP_TRY(c, hipMalloc(&var, (size_t)W * H * sizeof(float)));
+    tmp.push_back(var);
+    HIP_TRY(c, hipMalloc(&dg, g.size() * sizeof(float)));
+    tmp.push_back(dg);
+    HIP_TRY(c, hipMalloc(&minmax, 2 * sizeof(unsigned)));
+    tmp.push_back(minmax);
+    HIP_TRY(c, hipMemcpyAsync(dg, g.data(), g.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    float4 *F = reinterpret_cast<float4 *>(fb) + (size_t)bs * cols + bs;
+    // schedule: bands of BH rows start (r+1) BH wavefront steps apart; a launch runs `chunk` steps of each
+    // band in flight; band w's chunk k runs in launch w lag + k, lag = ceil((skew - 1) / chunk) + 1, so the
+    // band above has finished every step this chunk reads before the launch starts
+    const int BH = nh::denoise_band_rows();
+    const int n_bands = (H + BH - 1) / BH, skew = BH * (r + 1);
+    const int chunk = std::max(1, skew / 4);
+    const int lag = (skew - 1 + chunk - 1) / chunk + 1;
+    const int k_max = ((r + 1) * (BH - 1) + W + chunk - 1) / chunk;
+    const int n_launch = (n_bands - 1) * lag + k_max;
+    hipEvent_t e0, e1;
+    HIP_TRY(c, hipEventCreate(&e0));
+    HIP_TRY(c, hipEventCreate(&e1));
+    HIP_TRY(c, hipEventRecord(e0, c->stream));
+    uint64_t launches = 0;
+    for (int pass = 0; pass < p->amount; ++pass) {
+        DenoiseLaunch P{};
+        const bool even = (pass & 1) == 0;
+        P.src = even ? F : B;
+        P.src_stride = even ? cols : W;
+        P.dst = even ? B : F;
+        P.dst_stride = even ? W : cols;
+        P.width = W;
+        P.height = H;
+        P.range = r;
+        P.sigma_vr = p->sigma_vr;
+        P.g = dg;
+        P.var = var;
+        P.minmax = minmax;
+        P.lag = lag;
+        P.chunk = chunk;
+        HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(minmax), 0, 1, c->stream));
+        HIP_TRY(c, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(minmax + 1), 0x7f800000, 1, c->stream));
+        nh::launch_denoise_variance(P, c->stream);
+        launches += 1;
+        for (int L = 0; L < n_launch; ++L) {
+            const int w_lo = std::max(0, (L - k_max + 1 + lag - 1) / lag), w_hi = std::min(n_bands - 1, L / lag);
+            if (w_hi < w_lo) continue;
+            P.band_first = w_lo;
+            nh::launch_denoise_band(P, L, w_hi - w_lo + 1, c->stream);
+            ++launches;
+        }
+    }
+    if (p->amount & 1) {  // the last pass wrote the scratch image
+        nh::launch_denoise_copy(B, W, F, cols, W, H, c->stream);
+        ++launches;
+    }
+    HIP_TRY(c, hipEventRecord(e1, c->stream));
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    c->stats.kernel_ms_denoise += ms;
+    c->stats.launches_denoise += launches;
+    return NH_OK;
+}
+
+int nh_denoise(nh_ctx *c, const nh_denoiser *params) {
+    if (!c || !params) return NH_ERR_INVALID;
+    if (!c->has_scene) return fail(c, "no scene"), NH_ERR_STATE;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc = pipeline_drain(c)) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return run_denoise(c, c->fb, c->width, c->height, c->border, params);
+}
+
+int nh_denoise_image(nh_ctx *c, float *rgbw, int32_t width, int32_t height, int32_t border,
+                     const nh_denoiser *params) {
+    if (!c || !rgbw || !params || width <= 0 || height <= 0 || border < 0) return NH_ERR_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (int rc = pipeline_drain(c)) return rc;
+    const size_t n = 4 * (size_t)(width + 2 * border) * (size_t)(height + 2 * border);
+    float *d = nullptr;
+    HIP_TRY(c, hipMalloc(&d, n * sizeof(float)));
+    std::vector<void *> own{d};
+    struct Free {
+        std::vector<void *> &v;
+        ~Free() { free_all(v); }
+    } guard{own};
+    HIP_TRY(c, hipMemcpyAsync(d, rgbw, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if (int rc = run_denoise(c, d, width, height, border, params)) return rc;
+    HIP_TRY(c, hipMemcpy(rgbw, d, n * sizeof(float), hipMemcpyDeviceToHost));
+    return NH_OK;
+}
+
 int nh_reduce_framebuffers(nh_ctx **ctxs, int32_t n, int32_t root) {
     if (!ctxs || n <= 0 || root < 0 || root >= n) return NH_ERR_INVALID;
     for (int i = 0; i < n; ++i)

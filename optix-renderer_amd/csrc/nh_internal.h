@@ -40,6 +40,22 @@ struct SplatLaunch {
     float4 *staging;
 };
 
+// SimpleDenoiser pass (nh_denoise.hip): interior pixel (i, j) of an image at ptr[i * stride + j]
+struct DenoiseLaunch {
+    const float4 *src;      // the image at the start of the pass
+    int src_stride;
+    float4 *dst;            // the denoised image (pixels before p in row-major order already final)
+    int dst_stride;
+    int width, height, range;
+    float sigma_vr;
+    const float *g;         // g_sigma by squared pixel distance, 2 range^2 + 1 entries (host expf)
+    float *var;             // raw variance per pixel (width * height)
+    unsigned *minmax;       // [0] max, [1] min of var (float bits)
+    int band_first;         // band of workgroup 0 of this launch
+    int lag;                // launches between a band's chunk k and the next band's chunk k
+    int chunk;              // wavefront steps per band per launch
+};
+
 // In-kernel work counters (collect_stats): kStatShards copies of [0-3] queries, nodes, boxes, prims,
 // [4] invalid samples, [8-11] the any-hit share, [16-19] / [20-23] the closest / any-hit work of
 // the tail kernel, one copy per XCD (workgroup b adds to copy b % 8) so the per-wave atomics of
@@ -59,6 +75,11 @@ void launch_path(const nhd::DScene *S, const nhd::Traversal &tv, const PathLaunc
                  int depth, hipStream_t st);
 void launch_splat(const SplatLaunch &P, hipStream_t st);
 void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st);
+void launch_denoise_variance(const DenoiseLaunch &P, hipStream_t st);
+int denoise_band_rows();
+void launch_denoise_band(const DenoiseLaunch &P, int L, int n_bands, hipStream_t st);
+void launch_denoise_copy(const float4 *src, int src_stride, float4 *dst, int dst_stride, int width, int height,
+                         hipStream_t st);
 }  // namespace nh
 
 // Queue appends go to one counter per XCD (blocks are dealt round-robin over the 8 XCDs), so no

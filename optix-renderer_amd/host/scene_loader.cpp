@@ -279,6 +279,7 @@ struct SceneData {
     std::vector<float> area_cdf;
     nh_envmap env{};
     std::vector<float> env_rgba, env_cdf;
+    nh_denoiser denoiser{};  // type NH_DENOISER_NONE unless the scene has a <denoiser>
     // camera parameters kept for re-projection on resize
     float fov = 30.f, near_clip = 1e-4f, far_clip = 1e4f, focal = 10.f, fstop = 0.f, lens = 0.f;
     M4 to_world = M4::identity();
@@ -939,8 +940,20 @@ void build_scene(const Obj &scene, const std::string &base_dir, SceneData &sd) {
                 throw SceneError("emitter \"" + ch.type + "\" is not supported yet");
             }
             sd.emitters.push_back(em);
-        } else if (ch.tag == "denoiser" || ch.tag == "renderer") {
-            // GUI/OptiX-only objects: no effect on the path_mis hot path
+        } else if (ch.tag == "denoiser") {
+            // Scene::addChild (scene.cpp:242-245) + SimpleDenoiser's constructor clamps (simple.cpp:15-24)
+            if (sd.denoiser.type != NH_DENOISER_NONE) throw SceneError("There can only be one denoiser per scene!");
+            if (ch.type != "simple") throw SceneError("denoiser \"" + ch.type + "\" is not supported");
+            const float eps = 1e-4f;
+            auto clampf = [](float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); };
+            auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+            sd.denoiser.type = NH_DENOISER_SIMPLE;
+            sd.denoiser.sigma_d = clampf(ch.props.get_float("sigma_d", 0.f), eps, 10.f);
+            sd.denoiser.sigma_vr = clampf(ch.props.get_float("sigma_vr", 0.6f), eps, 10.f);
+            sd.denoiser.range = clampi(ch.props.get_int("range", 1), 0, 50);
+            sd.denoiser.amount = clampi(ch.props.get_int("amount", 1), 1, 10);
+        } else if (ch.tag == "renderer") {
+            // OptixRenderer settings object (OptixRenderer.h:17-36): no effect on the path_mis hot path
         } else if (ch.tag == "medium") {
             if (ch.type != "vacuum") throw SceneError("participating media are out of scope for path_mis");
         } else {
@@ -1012,6 +1025,7 @@ void fill_desc(const SceneData &sd, nh_scene_desc *d) {
     d->emitters = sd.emitters.data();
     d->emitter_cdf = sd.emitter_cdf.data();
     d->envmap = sd.envmap;
+    d->denoiser = sd.denoiser;
     d->n_vertices = (uint32_t)(sd.V.size() / 3);
     d->V = sd.V.data();
     d->N = sd.N.data();

@@ -33,6 +33,7 @@ INTEGRATOR_PATH_MIS, INTEGRATOR_PATH_MATS, INTEGRATOR_DIRECT_EMS, INTEGRATOR_DIR
 INTEGRATOR_DIRECT = 5  # the point-light `direct` integrator of scenes/pa1 (direct.cpp)
 MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1
 TRAVERSAL_REFERENCE, TRAVERSAL_ORDERED, TRAVERSAL_WIDE = 0, 1, 2
+DENOISER_NONE, DENOISER_SIMPLE = 0, 1
 
 _f = C.c_float
 _i32 = C.c_int32
@@ -74,13 +75,34 @@ class nh_envmap(C.Structure):
                 ("cdf", _fp), ("normalization", _f)]
 
 
+class nh_denoiser(C.Structure):
+    _fields_ = [("type", _i32), ("sigma_d", _f), ("sigma_vr", _f), ("range", _i32), ("amount", _i32)]
+
+
+def simple_denoiser(sigma_d: float = 0.0, sigma_vr: float = 0.6, range: int = 1, amount: int = 1) -> nh_denoiser:
+    """SimpleDenoiser's parameters with its constructor's defaults and clamps (src/denoiser/simple.cpp:15-24,
+    Nori's clamp and Epsilon = 1e-4f)."""
+    eps = np.float32(1e-4)
+
+    def clampf(v, lo, hi):
+        v = np.float32(v)
+        return float(lo if v < lo else (hi if v > hi else v))
+    d = nh_denoiser()
+    d.type = DENOISER_SIMPLE
+    d.sigma_d = clampf(sigma_d, eps, np.float32(10))
+    d.sigma_vr = clampf(sigma_vr, eps, np.float32(10))
+    d.range = int(min(max(range, 0), 50))
+    d.amount = int(min(max(amount, 1), 10))
+    return d
+
+
 class nh_scene_desc(C.Structure):
     _fields_ = [("camera", nh_camera), ("filter", nh_filter), ("integrator", _i32), ("sample_count", _i32),
                 ("n_shapes", _u32), ("shapes", C.POINTER(nh_shape)), ("n_bsdfs", _u32),
                 ("bsdfs", C.POINTER(nh_bsdf)), ("n_emitters", _u32), ("emitters", C.POINTER(nh_emitter)),
                 ("emitter_cdf", _fp), ("envmap", _i32), ("n_vertices", _u32), ("V", _fp), ("N", _fp),
                 ("UV", _fp), ("T", _fp), ("BT", _fp), ("n_faces", _u32), ("F", _u32p), ("n_area_cdf", _u32),
-                ("area_cdf", _fp), ("env", nh_envmap)]
+                ("area_cdf", _fp), ("env", nh_envmap), ("denoiser", nh_denoiser)]
 
 
 class nh_bvh_node(C.Structure):
@@ -122,7 +144,8 @@ class nh_render_stats(C.Structure):
                 ("node_bytes", C.c_uint64)] + [
         (n, C.c_uint64) for n in ("tail_queries", "tail_nodes_visited", "tail_boxes_tested", "tail_prims_tested",
                                   "tail_shadow_queries", "tail_shadow_nodes_visited", "tail_shadow_boxes_tested",
-                                  "tail_shadow_prims_tested", "lds_scene", "fused_bounce", "comm_inits")]
+                                  "tail_shadow_prims_tested", "lds_scene", "fused_bounce", "comm_inits")] + [
+        ("kernel_ms_denoise", C.c_double), ("launches_denoise", C.c_uint64)]
 
 
 def _sig(name, res, *args):
@@ -164,6 +187,8 @@ _sig("nh_framebuffer_device_ptr", _i32, _vp, C.POINTER(_vp), C.POINTER(C.c_size_
 _sig("nh_get_stats", _i32, _vp, C.POINTER(nh_render_stats))
 _sig("nh_reset_stats", _i32, _vp)
 _sig("nh_reduce_framebuffers", _i32, C.POINTER(_vp), _i32, _i32)
+_sig("nh_denoise", _i32, _vp, C.POINTER(nh_denoiser))
+_sig("nh_denoise_image", _i32, _vp, _fp, _i32, _i32, _i32, C.POINTER(nh_denoiser))
 _sig("nh_last_error", C.c_char_p, _vp)
 
 lib = _lib
@@ -344,6 +369,20 @@ class Context:
 
     def reset_stats(self):
         self._check(_lib.nh_reset_stats(self._h), "reset_stats")
+
+    def denoise(self, params: nh_denoiser = None):
+        """Denoiser::denoise on the master ImageBlock (src/utils/render.cpp:368-369): the scene's
+        <denoiser> unless params are given."""
+        if params is None:
+            params = self.scene.desc.denoiser
+        self._check(_lib.nh_denoise(self._h, C.byref(params)), "denoise")
+
+    def denoise_image(self, rgbw: np.ndarray, border: int, params: nh_denoiser) -> np.ndarray:
+        """SimpleDenoiser on a host (H+2b, W+2b, 4) float32 ImageBlock; returns the denoised copy."""
+        out = np.array(rgbw, dtype=np.float32, order="C", copy=True)
+        h, w = out.shape[0] - 2 * border, out.shape[1] - 2 * border
+        self._check(_lib.nh_denoise_image(self._h, _fptr(out), w, h, border, C.byref(params)), "denoise_image")
+        return out
 
     def trace(self, o: np.ndarray, d: np.ndarray, mint: np.ndarray, maxt: np.ndarray, any_hit=False,
               traversal: int = TRAVERSAL_REFERENCE) -> dict:

@@ -34,9 +34,10 @@ def materialize(out_dir: str) -> str:
 
 
 def cbox_xml(out_dir: str, variant: str = "c1", width: int | None = None, height: int | None = None,
-             spp: int | None = None, extra_shapes: str = "", drop_spheres: bool = False) -> str:
+             spp: int | None = None, extra_shapes: str = "", drop_spheres: bool = False, denoiser: str = "") -> str:
     """Cornell box scene file. variant: c1/c4 = reference (mirror + dielectric spheres),
-    c2 = both spheres diffuse (albedo of the walls), as SURVEY.md 8(d) defines."""
+    c2 = both spheres diffuse (albedo of the walls), as SURVEY.md 8(d) defines. denoiser: a
+    <denoiser> element to add (scenes/project/denoiser/denoiser-test.xml:28-32 form)."""
     materialize(out_dir)
     src = os.path.join(out_dir, "scenes/pa4/cbox/cbox_path_mis.xml")
     text = open(src).read()
@@ -48,13 +49,15 @@ def cbox_xml(out_dir: str, variant: str = "c1", width: int | None = None, height
         text = re.sub(r'<shape type="sphere">.*?</shape>', "", text, flags=re.S)
     if extra_shapes:
         text = text.replace("</scene>", extra_shapes + "\n</scene>")
+    if denoiser:
+        text = text.replace("</scene>", denoiser + "\n</scene>")
     if width:
         text = text.replace('<integer name="width" value="800"/>', f'<integer name="width" value="{width}"/>')
     if height:
         text = text.replace('<integer name="height" value="600"/>', f'<integer name="height" value="{height}"/>')
     if spp:
         text = text.replace('<integer name="sampleCount" value="512"/>', f'<integer name="sampleCount" value="{spp}"/>')
-    key = repr((width, height, spp, extra_shapes, drop_spheres)).encode()
+    key = repr((width, height, spp, extra_shapes, drop_spheres, denoiser)).encode()
     name = f"cbox_{variant}_{hashlib.sha1(key).hexdigest()[:10]}.xml"
     dst = os.path.join(out_dir, "scenes/pa4/cbox", name)
     with open(dst, "w") as f:

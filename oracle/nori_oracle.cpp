@@ -1354,6 +1354,99 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
 
 void no_scene_free(no_scene *s) { delete s; }
 
+// Eigen's Vector4f::lpNorm<1>() = cwiseAbs().sum(): one SSE packet reduced as (x0 + x2) + (x1 + x3)
+// (pinned against ext/eigen by oracle/eigen_probe.cpp)
+static float l1_norm4(float x0, float x1, float x2, float x3) {
+    return (std::fabs(x0) + std::fabs(x2)) + (std::fabs(x1) + std::fabs(x3));
+}
+
+// ---------------------------------------------------------------------------------------------------
+// SimpleDenoiser (src/denoiser/simple.cpp) on an ImageBlock of (W + 2b) x (H + 2b) RGBW pixels, serial:
+// the reference's loops run with one TBB thread (with several, its in-place rows race).
+// ---------------------------------------------------------------------------------------------------
+namespace {
+constexpr float kNoriEpsilon = 1e-4f;
+
+// Color4f::divideByFilterWeight().getLuminance() (color.h:113-118, common.cpp:265-268)
+float block_luminance(const float *px) {
+    float r = 0.f, g = 0.f, b = 0.f;
+    if (std::fabs(px[3]) > kNoriEpsilon) { r = px[0] / px[3]; g = px[1] / px[3]; b = px[2] / px[3]; }
+    return r * 0.212671f + g * 0.715160f + b * 0.072169f;
+}
+
+// computeVarianceFromImage (src/utils/common.cpp:339-398): 3x3 luminance variance, then normalised to
+// [1, 1.254] (or all zero). std::pow(float, 2) is the double-precision pow of C++11's promotion rules, so
+// each term and the running sum are evaluated in double and stored back to float.
+std::vector<float> denoise_variance(const float *blk, int W, int H, int bs) {
+    const int cols = W + 2 * bs;
+    auto at = [&](int i, int j) { return blk + 4 * ((size_t)(i + bs) * cols + (j + bs)); };
+    std::vector<float> var((size_t)W * H, 0.f);
+    for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j) {
+            float mean = 0.f, sum = 0.f;
+            for (int k = 0; k < 3; ++k)
+                for (int l = 0; l < 3; ++l) {
+                    const int i_ = i - 1 + k, j_ = j - 1 + l;
+                    if (i_ < 0 || i_ > H - 1 || j_ < 0 || j_ > W - 1) continue;
+                    mean += std::fabs(block_luminance(at(i_, j_)));
+                    sum += 1.f;
+                }
+            mean /= sum;
+            float col = 0.f;
+            for (int k = 0; k < 3; ++k)
+                for (int l = 0; l < 3; ++l) {
+                    const int i_ = i - 1 + k, j_ = j - 1 + l;
+                    if (i_ < 0 || i_ > H - 1 || j_ < 0 || j_ > W - 1) continue;
+                    const double d = (double)(std::fabs(block_luminance(at(i_, j_))) - mean);
+                    col = (float)((double)col + (double)(1.f / sum) * (d * d));
+                }
+            var[(size_t)i * W + j] = col;
+        }
+    float mx = var[0], mn = var[0];
+    for (float v : var) { mx = std::max(mx, v); mn = std::min(mn, v); }
+    if (mx - mn < kNoriEpsilon) {
+        std::fill(var.begin(), var.end(), 0.f);
+    } else {
+        for (float &v : var) v = 1.f + (v - mn) / (mx - mn) * 0.254f;
+    }
+    return var;
+}
+}  // namespace
+
+int no_denoise_simple(float *rgbw, int32_t width, int32_t height, int32_t border, const nh_denoiser *p) {
+    if (!rgbw || !p || width <= 0 || height <= 0 || border < 0 || p->type != NH_DENOISER_SIMPLE) return NH_ERR_INVALID;
+    const int W = width, H = height, bs = border, cols = W + 2 * bs, r = p->range;
+    const float sigma_d = p->sigma_d, sigma_vr = p->sigma_vr;
+    auto at = [&](int i, int j) { return rgbw + 4 * ((size_t)(i + bs) * cols + (j + bs)); };
+    for (int pass = 0; pass < p->amount; ++pass) {
+        const std::vector<float> var = denoise_variance(rgbw, W, H, bs);
+        for (int i = 0; i < H; ++i)
+            for (int j = 0; j < W; ++j) {
+                float sum_weights = 0.f, result[4] = {0.f, 0.f, 0.f, 0.f};
+                const int i_s = std::clamp(i - r, 0, H), i_e = std::clamp(i + r + 1, 0, H);
+                const int j_s = std::clamp(j - r, 0, W), j_e = std::clamp(j + r + 1, 0, W);
+                const float vp = var[(size_t)i * W + j];
+                for (int i_ = i_s; i_ < i_e; ++i_)
+                    for (int j_ = j_s; j_ < j_e; ++j_) {
+                        // g_sigma (simple.cpp:136-139): float expf of -(squaredNorm) / 2 / sigma_d / sigma_d
+                        const int dsq = (i - i_) * (i - i_) + (j - j_) * (j - j_);
+                        const float g = std::exp((float)-dsq / 2.f / sigma_d / sigma_d);
+                        // f_prime (:140-149): p's current value (not yet overwritten) against q's current one
+                        const float *ip = at(i, j), *iq = at(i_, j_);
+                        const float l1 = l1_norm4(ip[0] - iq[0], ip[1] - iq[1], ip[2] - iq[2], ip[3] - iq[3]);
+                        const float x = (l1 * vp) / sigma_vr;
+                        const float f = (float)std::exp(-0.5f * ((double)x * (double)x));
+                        const float w = g * f;
+                        for (int k = 0; k < 4; ++k) result[k] += iq[k] * w;
+                        sum_weights += w;
+                    }
+                float *op = at(i, j);
+                for (int k = 0; k < 4; ++k) op[k] = result[k] / sum_weights;
+            }
+    }
+    return NH_OK;
+}
+
 // The oracle's restated Eigen arithmetic on the probe's cases (oracle/eigen_probe.cpp layout): the same
 // helpers the path uses (dot, normalized, max_coeff, sqnorm, norm, cross, cwise chains; camera_ray's
 // 3x3 direction product and 4x4 point product)
@@ -1362,7 +1455,7 @@ int no_eigen_ops(int32_t n, const float *in, float *out) {
         const float *p = in + 36 * (size_t)i;
         const V3 a = mk(p[0], p[1], p[2]), b = mk(p[3], p[4], p[5]), c = mk(p[6], p[7], p[8]);
         const float s = p[9], *m3 = p + 10, *m4 = p + 20;
-        float *o = out + 24 * (size_t)i;
+        float *o = out + 28 * (size_t)i;
         o[0] = dot(a, b);
         const V3 an = normalized(a);
         o[1] = an.x; o[2] = an.y; o[3] = an.z;
@@ -1385,6 +1478,8 @@ int no_eigen_ops(int32_t n, const float *in, float *out) {
         const V3 x = cross(a, b);
         o[20] = x.x; o[21] = x.y; o[22] = x.z;
         o[23] = norm(a - b);
+        o[24] = l1_norm4(a.x - b.x, a.y - b.y, a.z - b.z, c.x - s);
+        o[25] = a.x / s; o[26] = a.y / s; o[27] = a.z / s;
     }
     return NH_OK;
 }

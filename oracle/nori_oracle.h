@@ -39,9 +39,13 @@ int no_bvh_info(const no_scene *s, uint32_t *n_nodes, uint32_t *n_indices);
 int no_env_cdf(const no_scene *s, const float **cdf, uint32_t *n, float *normalization);
 int no_bvh_export(const no_scene *s, nh_bvh_node *nodes, uint32_t *indices);
 
-/* the oracle's restated Eigen arithmetic on n cases of 36 floats (oracle/eigen_probe.cpp layout) -> 24 floats
+/* the oracle's restated Eigen arithmetic on n cases of 36 floats (oracle/eigen_probe.cpp layout) -> 28 floats
    each, for the bit-for-bit comparison with the reference's Eigen */
 int no_eigen_ops(int32_t n, const float *in, float *out);
+
+/* SimpleDenoiser::denoise (src/denoiser/simple.cpp:29-76) in place on an (W+2b)(H+2b)x4 RGBW ImageBlock,
+   serial row-major order (the reference with one thread) */
+int no_denoise_simple(float *rgbw, int32_t width, int32_t height, int32_t border, const nh_denoiser *p);
 
 /* BVH::rayIntersect over a ray batch (closest or any hit) */
 int no_trace_rays(const no_scene *s, const nh_ray_soa *rays, int32_t n, int32_t any_hit, nh_hit_soa *out);

@@ -51,6 +51,7 @@ _sig("no_bsdf_sample", _i32, C.POINTER(nh.nh_bsdf), _fp, _fp, _fp, _fp, _fp, C.P
 _sig("no_bsdf_pdf", C.c_float, C.POINTER(nh.nh_bsdf), _fp, _fp)
 _sig("no_bsdf_pdf_batch", _i32, C.POINTER(nh.nh_bsdf), _fp, _i32, _fp, _fp)
 _sig("no_eigen_ops", _i32, _i32, _fp, _fp)
+_sig("no_denoise_simple", _i32, _fp, _i32, _i32, _i32, C.POINTER(nh.nh_denoiser))
 _sig("no_chi2_histogram", _i32, C.POINTER(nh.nh_bsdf), _fp, _u64p, _u64p, _i32, _i32, _i32, C.POINTER(C.c_double))
 
 
@@ -189,9 +190,19 @@ def chi2_histogram(bsdf, wi, rng: Pcg32, n, res_theta, res_phi):
     return obs
 
 
+def denoise_simple(rgbw, border: int, params) -> np.ndarray:
+    """SimpleDenoiser (src/denoiser/simple.cpp:29-76), serial row-major order, on a copy of a
+    (H+2b, W+2b, 4) float32 ImageBlock. params: nori_hip.nh_denoiser."""
+    out = np.array(rgbw, dtype=np.float32, order="C", copy=True)
+    h, w = out.shape[0] - 2 * border, out.shape[1] - 2 * border
+    if _lib.no_denoise_simple(out.ctypes.data_as(_fp), w, h, border, C.byref(params)) != 0:
+        raise RuntimeError("no_denoise_simple: invalid arguments")
+    return out
+
+
 def eigen_ops(cases):
-    """The oracle's restated Eigen arithmetic (no_eigen_ops) on (n, 36) float32 cases -> (n, 24)."""
+    """The oracle's restated Eigen arithmetic (no_eigen_ops) on (n, 36) float32 cases -> (n, 28)."""
     cases = np.ascontiguousarray(cases, np.float32)
-    out = np.zeros((len(cases), 24), np.float32)
+    out = np.zeros((len(cases), 28), np.float32)
     _lib.no_eigen_ops(len(cases), cases.ctypes.data_as(_fp), out.ctypes.data_as(_fp))
     return out

@@ -200,7 +200,8 @@ def test_microfacet_chi2(scene_dir):
 
 def test_oracle_arithmetic_matches_reference_eigen(tmp_path):
     """The oracle's restated Eigen arithmetic (dot = x0*y0 + (x1*y1 + x2*y2), normalized, maxCoeff,
-    squaredNorm/norm, cross, 3x3 and 4x4 matrix-vector products, Color3f cwise chains) is bit-identical
+    squaredNorm/norm, cross, 3x3 and 4x4 matrix-vector products, Color3f cwise chains, the denoiser's
+    Vector4f lpNorm<1> = (|x0|+|x2|) + (|x1|+|x3|) and Color3f / w) is bit-identical
     to the reference's own vendored Eigen 3.3.8 (ext/eigen, compiled unmodified into
     oracle/_ref/eigen_probe by oracle/build_ref.sh) on random inputs, including wide exponent ranges,
     signed zeros and denormals. Only where the reference checkout is present (this container)."""
@@ -220,10 +221,11 @@ def test_oracle_arithmetic_matches_reference_eigen(tmp_path):
     inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
     cases.tofile(inp)
     subprocess.run([exe, str(inp), str(out)], check=True, timeout=120)
-    ref = np.fromfile(out, np.float32).reshape(n, 24)
+    ref = np.fromfile(out, np.float32).reshape(n, 28)
     mine = no.eigen_ops(cases)
     names = ["dot"] + ["normalized"] * 3 + ["maxCoeff"] + ["mat3*v"] * 3 + ["mat4*v"] * 4 + ["squaredNorm", "norm"] + \
-            ["(a*s)*b"] * 3 + ["a*b*c"] * 3 + ["cross"] * 3 + ["(a-b).norm"]
+            ["(a*s)*b"] * 3 + ["a*b*c"] * 3 + ["cross"] * 3 + ["(a-b).norm"] + \
+            ["Vector4f.lpNorm<1>"] + ["Color3f/w"] * 3
     for j, name in enumerate(names):
         r, m = ref[:, j].view(np.uint32), mine[:, j].view(np.uint32)
         nan_both = np.isnan(ref[:, j]) & np.isnan(mine[:, j])
