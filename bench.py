@@ -28,6 +28,9 @@ The JSON line also carries:
                 ~1M-triangle scene (perf-1M), timed in the same run
   cpu_baseline  the CPU oracle (oracle/, a restatement of the reference's path_mis) timed on
                 this host's cores on a bounded sample of the same workload (rank 0, N=1 only)
+  denoise       (N=1) Denoiser::denoise on the rendered master block (render.cpp:368-369): the GPU
+                SimpleDenoiser with scenes/project/denoiser/denoiser-test.xml's parameters, HIP-event time,
+                beside the serial CPU oracle on a crop of the same image
 """
 import argparse
 import json
@@ -64,6 +67,7 @@ def parse():
     p.add_argument("--mode", default="wavefront", choices=["megakernel", "wavefront"])
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-denoise", action="store_true", help="skip the denoise record")
     p.add_argument("--no-calibrate", action="store_true")
     p.add_argument("--pools", type=int, default=0,
                    help="wavefront path pools in flight (0: the library default; >1: a chunk's last bounces overlap "
@@ -393,6 +397,37 @@ def max_over_ranks(elapsed, dist, args, local):
     return float(t.item())
 
 
+def denoise_record(nh, ctx, scene, no_cpu):
+    """SimpleDenoiser (simple.cpp) on the rendered framebuffer, in place, with denoiser-test.xml's parameters
+    (sigma_d 6, sigma_vr 1.5, range 7): GPU time from HIP events; the serial CPU oracle on a 128x128 crop."""
+    p = nh.simple_denoiser(6.0, 1.5, 7, 1)
+    W, H, b = scene.width, scene.height, scene.border
+    crop = None
+    if not no_cpu:
+        fb = ctx.framebuffer()
+        crop = np.ascontiguousarray(fb[:128 + 2 * b, :128 + 2 * b])
+    ctx.reset_stats()
+    t0 = time.perf_counter()
+    ctx.denoise(p)
+    wall = time.perf_counter() - t0
+    st = ctx.stats()
+    ms = st["kernel_ms_denoise"]
+    out = {"denoiser": "simple (src/denoiser/simple.cpp), sigma_d 6, sigma_vr 1.5, range 7, 1 pass",
+           "image": f"{W}x{H}", "ms": round(ms, 3), "wall_ms": round(wall * 1e3, 3), "launches": st["launches_denoise"],
+           "mpixels_s": round(W * H / ms / 1e3, 3),
+           "order": "the reference's in-place row-major sweep (serial loop order), bit-identical to the oracle"}
+    if crop is not None:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import nori_oracle as no
+        t0 = time.perf_counter()
+        no.denoise_simple(crop, b, p)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"mpixels_s": round(128 * 128 / dt / 1e6, 4), "cores": 1, "kind": "port",
+                               "sample": f"128x128 crop of the same framebuffer ({dt:.2f} s), oracle "
+                                         "no_denoise_simple, one thread (the reference's loop order)"}
+    return out
+
+
 def traversal_1m(nh, args, local):
     """perf-1M: the north star's traversal roofline target is set on the BVH-traversal
     kernel of the ~1M-triangle scene at 1 GPU; measured here in the same run (a short bench of it)."""
@@ -445,6 +480,9 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(r["scene"], args.cpu_seconds, args.seed)
+        dn = None
+        if world == 1 and not args.no_denoise:
+            dn = denoise_record(nh, r["ctx"], r["scene"], args.no_cpu)
         t1m = None
         if world == 1 and args.traversal_1m_steps > 0 and args.config != "bumpy1m":
             r["ctx"].close()
@@ -478,6 +516,7 @@ def main():
             "traversal": traversal_record(roof) if roof else None,
             "traversal_1m": t1m,
             "cpu_baseline": cpu,
+            "denoise": dn,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -1411,6 +1411,11 @@ static int run_denoise(nh_ctx *c, float *fb, int W, int H, int bs, const nh_deno
     const int lag = (skew - 1 + chunk - 1) / chunk + 1;
     const int k_max = ((r + 1) * (BH - 1) + W + chunk - 1) / chunk;
     const int n_launch = (n_bands - 1) * lag + k_max;
+    // LDS tile of a chunk's window (input + denoised pixels): rows BH + 2r, columns chunk + (r+1)(BH-1) + 2r
+    const size_t tile_rows = (size_t)std::min(H, BH + 2 * r);
+    const size_t tile_cols = (size_t)std::min(W, chunk + (r + 1) * (BH - 1) + 2 * r);
+    size_t tile_bytes = 2 * tile_rows * tile_cols * sizeof(float4);
+    if (tile_bytes > 64 * 1024 || chunk > nh::denoise_max_chunk() || std::getenv("NH_DENOISE_NO_TILE")) tile_bytes = 0;
     hipEvent_t e0, e1;
     HIP_TRY(c, hipEventCreate(&e0));
     HIP_TRY(c, hipEventCreate(&e1));
@@ -1440,7 +1445,7 @@ static int run_denoise(nh_ctx *c, float *fb, int W, int H, int bs, const nh_deno
             const int w_lo = std::max(0, (L - k_max + 1 + lag - 1) / lag), w_hi = std::min(n_bands - 1, L / lag);
             if (w_hi < w_lo) continue;
             P.band_first = w_lo;
-            nh::launch_denoise_band(P, L, w_hi - w_lo + 1, c->stream);
+            nh::launch_denoise_band(P, L, w_hi - w_lo + 1, tile_bytes, c->stream);
             ++launches;
         }
     }

@@ -25,6 +25,7 @@ constexpr int kBandRows = 4;                 // rows per band (pixels per step p
 constexpr int kTermChunk = 256;              // window terms per LDS pass (range 7: 225 terms)
 constexpr int kLanesPerPixel = 5;            // R, G, B, W sums and the weight sum
 constexpr int kSumLanes = kBandRows * kLanesPerPixel;
+constexpr int kMaxChunk = 16;                // steps per launch the tiled kernel precomputes (range <= 15)
 static_assert(kSumLanes <= 64, "the sequential sums run in wave 0");
 
 // Color4f::divideByFilterWeight().getLuminance() (include/nori/color.h:113-118, common.cpp:265-268)
@@ -89,43 +90,65 @@ struct DnPixel {
 
 // One launch: `chunk` steps of every band in flight (see the schedule above). Band w runs its k-th chunk,
 // k = L - w * lag, covering global steps [row0 (r+1) + k chunk, ... + chunk) (row0 (r+1): the band's first).
+// TILE: the chunk's whole window -- input pixels and the denoised ones written by earlier launches -- is
+// copied to LDS once (dynamic shared memory, DenoiseLaunch::tile_* bounds) and the steps run from LDS; the
+// pixels this launch denoises go to the LDS copy as well as to dst. Without TILE every term reads HBM/L2.
+template <bool TILE>
 __global__ __launch_bounds__(kDnThreads) void dn_band_kernel(DenoiseLaunch P, int L) {
+    extern __shared__ float4 s_tile[];                   // TILE: src window, then dst window
     __shared__ float s_val[kSumLanes][kTermChunk + 1];  // +1: the summing lanes read distinct banks
-    __shared__ DnPixel s_px[kBandRows];
+    __shared__ DnPixel s_px[kMaxChunk][kBandRows];      // per step of the chunk, per band row
     const int w = P.band_first + blockIdx.x;
     const int k = L - w * P.lag;
     const int row0 = w * kBandRows, rows = min(kBandRows, P.height - row0);
     const int span = (P.range + 1) * (rows - 1) + P.width;  // steps with work in this band
     if (k < 0 || rows <= 0 || k * P.chunk >= span) return;
-    const int r = P.range;
+    const int r = P.range, lane = threadIdx.x;
+    const int s0 = row0 * (r + 1) + k * P.chunk;  // global wavefront step of the chunk's first step
+    const int nst = TILE ? P.chunk : 1;           // steps whose pixel setup is precomputed at once
+    // window of the chunk: rows [ti0, ti1], columns [tj0, tj1] (clamped to the image)
+    const int ti0 = max(row0 - r, 0), ti1 = min(row0 + rows - 1 + r, P.height - 1);
+    const int tj0 = max(s0 - (r + 1) * (row0 + rows - 1) - r, 0), tj1 = min(s0 + P.chunk - 1 - (r + 1) * row0 + r, P.width - 1);
+    const int tw = tj1 - tj0 + 1, tn = tw > 0 ? (ti1 - ti0 + 1) * tw : 0;
+    float4 *t_src = s_tile, *t_dst = s_tile + (TILE ? tn : 0);
+    if constexpr (TILE) {
+        for (int e = lane; e < tn; e += kDnThreads) {
+            const int di = e / tw, i_ = ti0 + di, j_ = tj0 + (e - di * tw);
+            t_src[e] = P.src[(size_t)i_ * P.src_stride + j_];
+            t_dst[e] = P.dst[(size_t)i_ * P.dst_stride + j_];
+        }
+    }
     const float mx = __uint_as_float(P.minmax[0]), mn = __uint_as_float(P.minmax[1]);
     const bool flat = mx - mn < kNoriEps;
-    const int lane = threadIdx.x;
     float acc = 0.f;  // wave 0, lane < kSumLanes: running sum of (pixel lane / 5, channel lane % 5)
     for (int st = 0; st < P.chunk; ++st) {
-        const int s = row0 * (r + 1) + k * P.chunk + st;  // global wavefront step
-        if (lane < kBandRows) {
-            DnPixel px{};
-            const int i = row0 + lane, j = s - (r + 1) * i;
-            if (lane < rows && j >= 0 && j < P.width) {
-                px.i = i;
-                px.j = j;
-                px.is = max(i - r, 0);
-                px.js = max(j - r, 0);
-                px.nj = min(j + r + 1, P.width) - px.js;
-                px.n = (min(i + r + 1, P.height) - px.is) * px.nj;
-                px.ip = P.src[(size_t)i * P.src_stride + j];
-                const float v = P.var[(size_t)i * P.width + j];
-                px.vn = flat ? 0.f : 1.f + (v - mn) / (mx - mn) * 0.254f;
+        const int s = s0 + st;  // global wavefront step
+        const int slot = TILE ? st : 0;
+        if (!TILE || st == 0) {  // pixel setup: every step of the chunk at once (TILE) or this step
+            for (int e = lane; e < nst * kBandRows; e += kDnThreads) {
+                const int q = e / kBandRows, a = e - q * kBandRows;
+                DnPixel px{};
+                const int i = row0 + a, j = s + q - (r + 1) * i;
+                if (a < rows && j >= 0 && j < P.width) {
+                    px.i = i;
+                    px.j = j;
+                    px.is = max(i - r, 0);
+                    px.js = max(j - r, 0);
+                    px.nj = min(j + r + 1, P.width) - px.js;
+                    px.n = (min(i + r + 1, P.height) - px.is) * px.nj;
+                    px.ip = P.src[(size_t)i * P.src_stride + j];
+                    const float v = P.var[(size_t)i * P.width + j];
+                    px.vn = flat ? 0.f : 1.f + (v - mn) / (mx - mn) * 0.254f;
+                }
+                s_px[q][a] = px;
             }
-            s_px[lane] = px;
+            __syncthreads();
         }
-        __syncthreads();
         int n_max = 0;
 #pragma unroll
-        for (int a = 0; a < kBandRows; ++a) n_max = max(n_max, s_px[a].n);
+        for (int a = 0; a < kBandRows; ++a) n_max = max(n_max, s_px[slot][a].n);
         if (n_max == 0) {
-            __syncthreads();
+            if (!TILE) __syncthreads();
             continue;
         }
         if (lane < kSumLanes) acc = 0.f;
@@ -133,7 +156,7 @@ __global__ __launch_bounds__(kDnThreads) void dn_band_kernel(DenoiseLaunch P, in
             // window terms: weight g * f and the four weighted channels (simple.cpp:56-66, f_prime :140-149)
             for (int task = lane; task < kBandRows * kTermChunk; task += kDnThreads) {
                 const int a = task / kTermChunk, t = t0 + (task - a * kTermChunk);
-                const DnPixel &px = s_px[a];
+                const DnPixel &px = s_px[slot][a];
                 if (t >= px.n) continue;
                 const int di = t / px.nj;
                 const int i_ = px.is + di, j_ = px.js + (t - di * px.nj);
@@ -141,8 +164,14 @@ __global__ __launch_bounds__(kDnThreads) void dn_band_kernel(DenoiseLaunch P, in
                 // comparison and a select of the row address: the short-circuit form (i_ < i || (i_ == i &&
                 // j_ < j)) with the buffer chosen inside the branches was miscompiled (dst base with src stride)
                 const bool before = i_ * P.width + j_ < px.i * P.width + px.j;
-                const float4 *row = before ? P.dst + (size_t)i_ * P.dst_stride : P.src + (size_t)i_ * P.src_stride;
-                const float4 iq = row[j_];
+                float4 iq;
+                if constexpr (TILE) {
+                    const float4 *tb = before ? t_dst : t_src;
+                    iq = tb[(i_ - ti0) * tw + (j_ - tj0)];
+                } else {
+                    const float4 *row = before ? P.dst + (size_t)i_ * P.dst_stride : P.src + (size_t)i_ * P.src_stride;
+                    iq = row[j_];
+                }
                 const int dsq = (px.i - i_) * (px.i - i_) + (px.j - j_) * (px.j - j_);
                 const float g = P.g[dsq];
                 // Eigen Vector4f::lpNorm<1>: (|x0| + |x2|) + (|x1| + |x3|)
@@ -162,29 +191,42 @@ __global__ __launch_bounds__(kDnThreads) void dn_band_kernel(DenoiseLaunch P, in
             // the reference's running sums, term by term in window order
             if (lane < kSumLanes) {
                 const int a = lane / kLanesPerPixel;
-                const int m = min(s_px[a].n - t0, kTermChunk);
+                const int m = min(s_px[slot][a].n - t0, kTermChunk);
                 const float *v = s_val[lane];
                 float x = acc;
+                // 16-term batches, the next batch's LDS reads issued before this batch's dependent adds
+                constexpr int kB = 16;
+                float cur[kB], nxt[kB];
                 int t = 0;
-                for (; t + 4 <= m; t += 4) {
-                    const float v0 = v[t], v1 = v[t + 1], v2 = v[t + 2], v3 = v[t + 3];
-                    x += v0;
-                    x += v1;
-                    x += v2;
-                    x += v3;
+                if (m >= kB) {
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) cur[u] = v[u];
+                    for (; t + 2 * kB <= m; t += kB) {
+#pragma unroll
+                        for (int u = 0; u < kB; ++u) nxt[u] = v[t + kB + u];
+#pragma unroll
+                        for (int u = 0; u < kB; ++u) x += cur[u];
+#pragma unroll
+                        for (int u = 0; u < kB; ++u) cur[u] = nxt[u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) x += cur[u];
+                    t += kB;
                 }
                 for (; t < m; ++t) x += v[t];
                 acc = x;
             }
-            __syncthreads();
+            if (t0 + kTermChunk < n_max) __syncthreads();  // s_val is refilled by the next term chunk
         }
         // result[k] / sum_weights (simple.cpp:71-72)
         if (threadIdx.x < 64) {
             const int a = lane / kLanesPerPixel, ch = lane - a * kLanesPerPixel;
             const float wsum = __shfl(acc, a * kLanesPerPixel + 4, 64);
-            if (lane < kSumLanes && ch < 4 && s_px[a].n > 0) {
-                float *o = reinterpret_cast<float *>(&P.dst[(size_t)s_px[a].i * P.dst_stride + s_px[a].j]);
-                o[ch] = acc / wsum;
+            if (lane < kSumLanes && ch < 4 && s_px[slot][a].n > 0) {
+                const DnPixel &px = s_px[slot][a];
+                const float o = acc / wsum;
+                reinterpret_cast<float *>(&P.dst[(size_t)px.i * P.dst_stride + px.j])[ch] = o;
+                if constexpr (TILE) reinterpret_cast<float *>(&t_dst[(px.i - ti0) * tw + (px.j - tj0)])[ch] = o;
             }
         }
         __syncthreads();
@@ -208,8 +250,11 @@ void launch_denoise_variance(const DenoiseLaunch &P, hipStream_t st) {
 
 int denoise_band_rows() { return kBandRows; }
 
-void launch_denoise_band(const DenoiseLaunch &P, int L, int n_bands, hipStream_t st) {
-    hipLaunchKernelGGL(dn_band_kernel, dim3(n_bands), dim3(kDnThreads), 0, st, P, L);
+int denoise_max_chunk() { return kMaxChunk; }
+
+void launch_denoise_band(const DenoiseLaunch &P, int L, int n_bands, size_t tile_bytes, hipStream_t st) {
+    if (tile_bytes) hipLaunchKernelGGL(dn_band_kernel<true>, dim3(n_bands), dim3(kDnThreads), tile_bytes, st, P, L);
+    else hipLaunchKernelGGL(dn_band_kernel<false>, dim3(n_bands), dim3(kDnThreads), 0, st, P, L);
 }
 
 void launch_denoise_copy(const float4 *src, int src_stride, float4 *dst, int dst_stride, int width, int height,

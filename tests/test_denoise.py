@@ -137,8 +137,14 @@ def rel_l2(a, b):
     (64, 48, 1, 3, 3, 2.0, 0.3),      # three passes (the result ends in the framebuffer)
     (20, 23, 0, 12, 1, 4.0, 1.0),     # 625-term windows: several LDS chunks per pixel
     (16, 16, 2, 0, 1, 1.0, 0.6),      # range 0: identity
+    (40, 5, 2, 9, 1, 3.0, 0.6),       # narrower than the window
+    (50, 3, 0, 15, 2, 5.0, 0.9),      # range 15: the largest chunk the tiled kernel precomputes
+    (24, 30, 2, 20, 1, 6.0, 1.5),     # range 20: window tile beyond 64 KB -> the untiled kernel
 ])
-def test_denoise_image_matches_oracle(gpu, h, w, bs, r, amount, sigma_d, sigma_vr):
+@pytest.mark.parametrize("tile", [True, False], ids=["tile", "global"])
+def test_denoise_image_matches_oracle(gpu, monkeypatch, tile, h, w, bs, r, amount, sigma_d, sigma_vr):
+    if not tile:
+        monkeypatch.setenv("NH_DENOISE_NO_TILE", "1")
     blk = random_block(h, w, bs, 7 * h + w)
     p = nh.simple_denoiser(sigma_d, sigma_vr, r, amount)
     ctx = nh.Context(0)
