@@ -1,7 +1,8 @@
 // nori_hip: headless equivalent of the reference's `nori <scene.xml>` entry
 // (src/utils/main.cpp:32-114 + RenderThread::renderThreadMain, render.cpp:232-419),
 // rendering the scene's path_mis / path_mats integrator on one MI355X through the
-// C-ABI and writing <scene>.exr next to the input (Bitmap::save, bitmap.cpp:82-110).
+// C-ABI, applying the scene's <denoiser> (render.cpp:368-369), and writing <scene>.exr next to the input
+// (Bitmap::save, bitmap.cpp:82-110).
 //
 //   nori_hip scene.xml [--spp N] [--width W --height H] [--device D] [--ordered] [--pfm out.pfm] [--png]
 // --png also writes <scene>.png as Bitmap::saveToLDR (bitmap.cpp:122-140; the reference's hdrToLdr).
@@ -65,6 +66,9 @@ int main(int argc, char **argv) {
     if (nh_render(ctx, &req)) return die("render", nh_last_error(ctx));
     nh_synchronize(ctx);
     auto t3 = std::chrono::steady_clock::now();
+    // Denoiser::denoise on the master block after the render loop (render.cpp:368-369)
+    if (desc.denoiser.type != NH_DENOISER_NONE && nh_denoise(ctx, &desc.denoiser))
+        return die("denoise", nh_last_error(ctx));
     const int W = desc.camera.width, H = desc.camera.height, B = desc.filter.border;
     std::vector<float> rgbw(4 * (size_t)(W + 2 * B) * (H + 2 * B)), rgb(3 * (size_t)W * H);
     nh_get_framebuffer(ctx, rgbw.data(), rgbw.size());
