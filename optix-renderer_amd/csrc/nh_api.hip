@@ -1205,8 +1205,12 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     const size_t per_round = (size_t)c->n_list;
     const size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px(c) * 16 +
                                    (wavefront ? per_round * kWfBytesPerPath : 0);
-    // device memory per chunk: sample records + block ImageBlocks (+ path state, per pool)
-    size_t budget = wavefront ? (size_t)8 << 30 : (size_t)1 << 30;
+    // device memory per chunk: sample records + block ImageBlocks (+ path state, per pool). Every
+    // wavefront chunk ends in a tail whose length is set by its longest path (C4: ~5-7 ms of
+    // dielectric / mirror chains, whatever the chunk's size), so chunks are as large as the 26-bit
+    // path ids allow: one chunk per C4 step (67M paths, ~18 GB per pool) instead of 7 + 7 + 2 rounds
+    // under an 8 GiB budget (C4 2590 -> 3140 Msamples/s); 288 GB of HBM holds two such pools.
+    size_t budget = wavefront ? (size_t)24 << 30 : (size_t)1 << 30;
     if (const char *e = std::getenv(wavefront ? "NH_WF_BUDGET_MB" : "NH_RECORD_BUDGET_MB"))
         budget = (size_t)std::max(1L, std::atol(e)) << 20;
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / per_round_bytes));
