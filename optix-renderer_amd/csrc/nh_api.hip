@@ -846,7 +846,11 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     // measured on 16.7M-path chunks: C2 3025 / 3030 / 2692 Msamples/s at 64k / 262k / 1M,
     // bumpy-1M 708 / 744 / 739 / 603 at 64k / 262k / 1M / 3M; 67M-path C4 chunks 2102 / 2206 / 2226 / 2209
     // at 1M / 262k / 131k / 64k
-    p.tail_at = std::min<int64_t>(std::max<int64_t>(n_paths / 64, 8192), 262144);
+    // at 67M / 16.7M paths with the fused bounce (round 2): C4 3134 / 3229 / 3254 Msamples/s at
+    // 262k / 64k / 32k, C2 3680 / 3717 at 262k / 64k, bumpy-1M (persistent traversal) 1404 / 1378 at
+    // 262k / 64k -- an LDS-staged bounce stays efficient down to fewer paths than a deep-tree one
+    p.tail_at = p.fused ? std::min<int64_t>(std::max<int64_t>(n_paths / 256, 8192), 65536)
+                        : std::min<int64_t>(std::max<int64_t>(n_paths / 64, 8192), 262144);
     if (const char *e = std::getenv("NH_TAIL")) p.tail_at = std::atoll(e);
     // below this many live paths the pool counts as draining: the next chunk may start beside it
     p.drain_at = std::max<int64_t>(n_paths / 8, p.tail_at);
