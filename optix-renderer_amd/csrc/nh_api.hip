@@ -785,11 +785,24 @@ static SplatLaunch make_splat(const nh_ctx *c, const float4 *rec, const float *r
 
 static size_t block_px(const nh_ctx *c) { return (size_t)(32 + 2 * c->border) * (32 + 2 * c->border); }
 
+// path pools driven by pipeline_run (NH_POOLS: 1 = no overlap, for A/B and tests)
+static int active_pools() {
+    const char *np = std::getenv("NH_POOLS");
+    return std::max(1, std::min(kPools, np ? std::atoi(np) : NH_DEFAULT_POOLS));
+}
+
 // start job j on idle pool p: buffers, traversal choice, initial queue (all n_paths camera paths)
 static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     const int n_paths = j.rounds * c->n_list;
     int rc = pool_alloc(c, p, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c));
     if (rc) return rc;
+    // the other pools in use get the same capacity now (idle ones only: nothing of theirs is in
+    // flight), so the first render call, not a later one, pays for their allocation
+    for (int i = 0; i < active_pools(); ++i) {
+        WfPool &o = c->pools[i];
+        if (&o == &p || o.state != WfPool::IDLE) continue;
+        if ((rc = pool_alloc(c, o, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c)))) return rc;
+    }
     p.job = j;
     WfLaunch &L = p.L;
     L = WfLaunch{};
@@ -1073,8 +1086,7 @@ static void pipeline_reset(nh_ctx *c) {
 // Drive the pools. all = run until every chunk has finished; otherwise return once every
 // submitted chunk has started and every busy pool is draining.
 static int pipeline_run(nh_ctx *c, bool all) {
-    const char *np = std::getenv("NH_POOLS");  // 1 = no overlap (A/B and tests)
-    const int n_pools = std::max(1, std::min(kPools, np ? std::atoi(np) : NH_DEFAULT_POOLS));
+    const int n_pools = active_pools();
     for (;;) {
         bool progress = false;
         for (WfPool &p : c->pools) {
