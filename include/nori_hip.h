@@ -290,6 +290,12 @@ int nh_scene_set_bsdf(nh_scene *scene, uint32_t shape, const nh_bsdf *bsdf);
 int nh_scene_set_integrator(nh_scene *scene, int32_t integrator);
 void nh_scene_free(nh_scene *scene);
 const char *nh_host_last_error(void);
+/* Parity hook for the loader's transform arithmetic (the Eigen operations of parser.cpp:308-360,
+ * transform.h:73-86, transform.cpp:9-10 and perspective.cpp:68-95 as the product restates them). One
+ * request line in the protocol of oracle/eigen_xform_probe.cpp (floats as 8-hex-digit bit patterns:
+ * "inv", "xf", "cam", "pt", "vec", "nrm"); writes the reply floats to out and returns their count, or
+ * -1 (nh_host_last_error) for a malformed request or too small a cap. */
+int nh_debug_transform(const char *request, float *out, int32_t cap);
 
 int nh_bvh_build(const nh_scene_desc *scene, int32_t n_threads, nh_bvh **out);
 int nh_bvh_get_desc(const nh_bvh *bvh, nh_bvh_desc *out);

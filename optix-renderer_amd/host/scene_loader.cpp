@@ -16,8 +16,9 @@
 // Floating-point conventions: per-element arithmetic is fp32 with no contraction;
 // 3-element dot products / squared norms are evaluated x0*y0 + (x1*y1 + x2*y2),
 // which is what the reference's vendored Eigen 3.3.8 emits for Vector3f (measured,
-// DESIGN.md). Matrix inverses are computed in fp64 and rounded (the reference uses
-// Eigen's SSE 4x4 inverse; host-side setup only, identical for GPU and oracle).
+// DESIGN.md). Transform composition, Matrix4f::inverse (Eigen's SSE path) and the camera matrices
+// are restated bit for bit in nori_transform.h (pinned against the reference's Eigen by
+// tests/test_transforms.py).
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -34,6 +35,7 @@
 
 #include "nori_hip.h"
 #include "nh_host.h"
+#include "nori_transform.h"
 #include "xml_lite.h"
 
 namespace nh {
@@ -69,80 +71,15 @@ inline V3 normalized(V3 a) {
     return a;
 }
 
-struct M4 {
-    float m[4][4];
-    static M4 identity() {
-        M4 r;
-        for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) r.m[i][j] = (i == j) ? 1.0f : 0.0f;
-        return r;
-    }
-};
+using M4 = xf::Mat4;
 
-// 4x4 product, left-to-right accumulation (Eigen's lazy 4x4 product on SSE).
-M4 mul(const M4 &a, const M4 &b) {
-    M4 r;
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) {
-            float s = a.m[i][0] * b.m[0][j];
-            s = s + a.m[i][1] * b.m[1][j];
-            s = s + a.m[i][2] * b.m[2][j];
-            s = s + a.m[i][3] * b.m[3][j];
-            r.m[i][j] = s;
-        }
-    return r;
-}
+inline xf::Vec3 to_xf(V3 a) { return {a.x, a.y, a.z}; }
+inline V3 from_xf(xf::Vec3 a) { return v3(a.x, a.y, a.z); }
 
-M4 inverse(const M4 &a) {
-    double m[4][8];
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 8; ++j) m[i][j] = (j < 4) ? (double)a.m[i][j] : (j - 4 == i ? 1.0 : 0.0);
-    for (int c = 0; c < 4; ++c) {
-        int p = c;
-        for (int r = c + 1; r < 4; ++r)
-            if (std::fabs(m[r][c]) > std::fabs(m[p][c])) p = r;
-        if (m[p][c] == 0.0) throw SceneError("singular transform matrix");
-        if (p != c)
-            for (int j = 0; j < 8; ++j) std::swap(m[p][j], m[c][j]);
-        double inv = 1.0 / m[c][c];
-        for (int j = 0; j < 8; ++j) m[c][j] *= inv;
-        for (int r = 0; r < 4; ++r) {
-            if (r == c) continue;
-            double f = m[r][c];
-            if (f == 0.0) continue;
-            for (int j = 0; j < 8; ++j) m[r][j] -= f * m[c][j];
-        }
-    }
-    M4 r;
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) r.m[i][j] = (float)m[i][j + 4];
-    return r;
-}
-
-// Transform::operator*(Point3f): homogeneous, left-to-right 4x4 product, divide by w.
-V3 xform_point(const M4 &t, V3 p) {
-    float r[4];
-    for (int i = 0; i < 4; ++i) {
-        float s = t.m[i][0] * p.x;
-        s = s + t.m[i][1] * p.y;
-        s = s + t.m[i][2] * p.z;
-        s = s + t.m[i][3] * 1.0f;
-        r[i] = s;
-    }
-    return v3(r[0] / r[3], r[1] / r[3], r[2] / r[3]);
-}
-// Transform::operator*(Vector3f): top-left 3x3 product (Eigen redux order per row).
-V3 xform_vector(const M4 &t, V3 v) {
-    return v3(t.m[0][0] * v.x + (t.m[0][1] * v.y + t.m[0][2] * v.z),
-              t.m[1][0] * v.x + (t.m[1][1] * v.y + t.m[1][2] * v.z),
-              t.m[2][0] * v.x + (t.m[2][1] * v.y + t.m[2][2] * v.z));
-}
-// Transform::operator*(Normal3f): inverse-transpose 3x3.
-V3 xform_normal(const M4 &inv, V3 n) {
-    return v3(inv.m[0][0] * n.x + (inv.m[1][0] * n.y + inv.m[2][0] * n.z),
-              inv.m[0][1] * n.x + (inv.m[1][1] * n.y + inv.m[2][1] * n.z),
-              inv.m[0][2] * n.x + (inv.m[1][2] * n.y + inv.m[2][2] * n.z));
-}
+// nori::Transform applied to points / vectors / normals (include/nori/transform.h:73-86)
+V3 xform_point(const M4 &t, V3 p) { return from_xf(xf::apply_point(t, to_xf(p))); }
+V3 xform_vector(const M4 &t, V3 v) { return from_xf(xf::apply_vector(t, to_xf(v))); }
+V3 xform_normal(const M4 &inv, V3 n) { return from_xf(xf::apply_normal(inv, to_xf(n))); }
 
 float to_float(const std::string &str) {
     const char *c = str.c_str();
@@ -315,51 +252,33 @@ void check_attrs(const XmlNode &n, std::initializer_list<const char *> allowed, 
     if (!need.empty()) throw SceneError("missing attribute \"" + need[0] + "\" in \"" + n.name + "\" at " + c.pos(n.offset));
 }
 
-M4 xform_op(const XmlNode &n, const ParseCtx &c) {
-    M4 r = M4::identity();
+// One transform operation pre-multiplied onto the Affine3f being composed (parser.cpp:308-360).
+void apply_xform_op(M4 &t, const XmlNode &n, const ParseCtx &c) {
     if (n.name == "translate") {
         check_attrs(n, {"value"}, c);
-        V3 v = to_v3(*n.attr("value"));
-        r.m[0][3] = v.x; r.m[1][3] = v.y; r.m[2][3] = v.z;
+        xf::pre_translate(t, to_xf(to_v3(*n.attr("value"))));
     } else if (n.name == "scale") {
         check_attrs(n, {"value"}, c);
-        V3 v = to_v3(*n.attr("value"));
-        r.m[0][0] = v.x; r.m[1][1] = v.y; r.m[2][2] = v.z;
+        xf::pre_scale(t, to_xf(to_v3(*n.attr("value"))));
     } else if (n.name == "matrix") {
         check_attrs(n, {"value"}, c);
-        auto t = tokenize(*n.attr("value"));
-        if (t.size() != 16) throw SceneError("expected 16 values");
+        auto tk = tokenize(*n.attr("value"));
+        if (tk.size() != 16) throw SceneError("expected 16 values");
+        M4 m;
         for (int i = 0; i < 4; ++i)
-            for (int j = 0; j < 4; ++j) r.m[i][j] = to_float(t[i * 4 + j]);
+            for (int j = 0; j < 4; ++j) m.m[i][j] = to_float(tk[i * 4 + j]);
+        xf::pre_affine(t, m);
     } else if (n.name == "rotate") {
         check_attrs(n, {"angle", "axis"}, c);
-        float angle = to_float(*n.attr("angle")) * (3.14159265358979323846f / 180.0f);
-        V3 a = to_v3(*n.attr("axis"));
-        // Eigen::AngleAxis::toRotationMatrix
-        float s = (float)std::sin((double)angle), co = (float)std::cos((double)angle);
-        V3 sa = v3(s * a.x, s * a.y, s * a.z);
-        V3 c1 = v3((1.0f - co) * a.x, (1.0f - co) * a.y, (1.0f - co) * a.z);
-        float tmp = c1.x * a.y;
-        r.m[0][1] = tmp - sa.z; r.m[1][0] = tmp + sa.z;
-        tmp = c1.x * a.z;
-        r.m[0][2] = tmp + sa.y; r.m[2][0] = tmp - sa.y;
-        tmp = c1.y * a.z;
-        r.m[1][2] = tmp - sa.x; r.m[2][1] = tmp + sa.x;
-        r.m[0][0] = c1.x * a.x + co; r.m[1][1] = c1.y * a.y + co; r.m[2][2] = c1.z * a.z + co;
+        const float angle = xf::deg_to_rad(to_float(*n.attr("angle")));
+        xf::pre_rotate(t, angle, to_xf(to_v3(*n.attr("axis"))));
     } else if (n.name == "lookat") {
         check_attrs(n, {"origin", "target", "up"}, c);
-        V3 origin = to_v3(*n.attr("origin")), target = to_v3(*n.attr("target")), up = to_v3(*n.attr("up"));
-        V3 dir = normalized(sub(target, origin));
-        V3 left = normalized(cross3(normalized(up), dir));
-        V3 new_up = normalized(cross3(dir, left));
-        r.m[0][0] = left.x; r.m[1][0] = left.y; r.m[2][0] = left.z;
-        r.m[0][1] = new_up.x; r.m[1][1] = new_up.y; r.m[2][1] = new_up.z;
-        r.m[0][2] = dir.x; r.m[1][2] = dir.y; r.m[2][2] = dir.z;
-        r.m[0][3] = origin.x; r.m[1][3] = origin.y; r.m[2][3] = origin.z;
+        xf::pre_affine(t, xf::lookat_matrix(to_xf(to_v3(*n.attr("origin"))), to_xf(to_v3(*n.attr("target"))),
+                                            to_xf(to_v3(*n.attr("up")))));
     } else {
         throw SceneError("unhandled transform element \"" + n.name + "\"");
     }
-    return r;
 }
 
 std::unique_ptr<Obj> parse_node(const XmlNode &n, PropList *parent_props, const std::string &parent_tag,
@@ -396,7 +315,7 @@ std::unique_ptr<Obj> parse_node(const XmlNode &n, PropList *parent_props, const 
         for (auto &ch : n.children) {
             if (!in_list(ch->name, kXformTags, sizeof(kXformTags) / sizeof(*kXformTags)))
                 throw SceneError("transform nodes can only contain transform operations (at " + c.pos(ch->offset) + ")");
-            acc = mul(xform_op(*ch, c), acc);  // pre-multiply: later operations apply last
+            apply_xform_op(acc, *ch, c);  // pre-multiply: later operations apply last
         }
         Prop p; p.kind = Prop::Transform; p.t = acc;
         parent_props->set(*n.attr("name"), p);
@@ -507,7 +426,7 @@ void load_obj(const std::string &path, const M4 &trafo, SceneData &sd, nh_shape 
     auto it_cache = sd.obj_cache.find(path);
     if (it_cache == sd.obj_cache.end()) it_cache = sd.obj_cache.emplace(path, std::make_shared<ObjText>(parse_obj(path))).first;
     const ObjText &obj = *it_cache->second;
-    const M4 inv = inverse(trafo);
+    const M4 inv = xf::inverse(trafo);  // nori::Transform(Matrix4f) keeps Matrix4f::inverse()
     std::vector<V3> positions(obj.positions.size()), normals(obj.normals.size());
     V3 bmin = v3(INFINITY, INFINITY, INFINITY), bmax = v3(-INFINITY, -INFINITY, -INFINITY);
     for (size_t i = 0; i < positions.size(); ++i) {
@@ -640,18 +559,8 @@ void camera_update(SceneData &sd) {
     nh_camera &c = sd.camera;
     c.inv_output_size[0] = 1.0f / (float)c.width;
     c.inv_output_size[1] = 1.0f / (float)c.height;
-    float aspect = (float)c.width / (float)c.height;
-    float recip = 1.0f / (sd.far_clip - sd.near_clip);
-    float cot = 1.0f / (float)std::tan((double)((sd.fov / 2.0f) * (3.14159265358979323846f / 180.0f)));
-    M4 persp = M4::identity();
-    persp.m[0][0] = cot; persp.m[1][1] = cot;
-    persp.m[2][2] = sd.far_clip * recip;
-    persp.m[2][3] = -sd.near_clip * sd.far_clip * recip;
-    persp.m[3][2] = 1.0f; persp.m[3][3] = 0.0f;
-    M4 st = M4::identity();  // DiagonalMatrix(0.5, -0.5*aspect, 1) * Translation(1, -1/aspect, 0)
-    st.m[0][0] = 0.5f; st.m[1][1] = -0.5f * aspect; st.m[2][2] = 1.0f;
-    st.m[0][3] = 0.5f * 1.0f; st.m[1][3] = (-0.5f * aspect) * (-1.0f / aspect); st.m[2][3] = 1.0f * 0.0f;
-    M4 s2c = inverse(mul(st, persp));
+    // sampleToCamera = Transform(D * T * P).inverse(): the inverse Eigen stored for D * T * P
+    const M4 s2c = xf::inverse(xf::camera_projection(c.width, c.height, sd.fov, sd.near_clip, sd.far_clip));
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) {
             c.sample_to_camera[i * 4 + j] = s2c.m[i][j];
@@ -1111,6 +1020,84 @@ void nh_scene_free(nh_scene *scene) {
     if (!scene) return;
     delete scene->data;
     delete scene;
+}
+
+// The loader's own transform functions (nori_transform.h) behind oracle/eigen_xform_probe.cpp's protocol.
+int nh_debug_transform(const char *request, float *out, int32_t cap) {
+    namespace xf = nh::xf;
+    if (!request || !out) { nh::set_host_error("null argument"); return -1; }
+    std::istringstream in(request);
+    auto next = [&in]() -> float {
+        std::string t;
+        if (!(in >> t)) throw std::runtime_error("truncated request");
+        uint32_t u = (uint32_t)std::stoul(t, nullptr, 16);
+        float f;
+        std::memcpy(&f, &u, 4);
+        return f;
+    };
+    auto m4 = [&next]() {
+        xf::Mat4 m;
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) m.m[i][j] = next();
+        return m;
+    };
+    auto v3 = [&next]() {
+        const float x = next(), y = next(), z = next();
+        return xf::Vec3{x, y, z};
+    };
+    std::vector<float> r;
+    auto put_m4 = [&r](const xf::Mat4 &m) {
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) r.push_back(m.m[i][j]);
+    };
+    try {
+        std::string cmd;
+        in >> cmd;
+        if (cmd == "inv") {
+            put_m4(xf::inverse(m4()));
+        } else if (cmd == "xf") {
+            int n = 0;
+            in >> n;
+            xf::Mat4 t = xf::Mat4::identity();
+            for (int k = 0; k < n; ++k) {
+                std::string op;
+                in >> op;
+                if (op == "t") xf::pre_translate(t, v3());
+                else if (op == "s") xf::pre_scale(t, v3());
+                else if (op == "r") {
+                    const float angle = xf::deg_to_rad(next());
+                    xf::pre_rotate(t, angle, v3());
+                } else if (op == "m") xf::pre_affine(t, m4());
+                else if (op == "l") {
+                    const xf::Vec3 o = v3(), tg = v3(), up = v3();
+                    xf::pre_affine(t, xf::lookat_matrix(o, tg, up));
+                } else throw std::runtime_error("unknown transform op " + op);
+            }
+            put_m4(t);
+            put_m4(xf::inverse(t));
+        } else if (cmd == "cam") {
+            const float w = next(), h = next(), fov = next(), n = next(), f = next();
+            const xf::Mat4 p = xf::camera_projection((int)w, (int)h, fov, n, f);
+            put_m4(xf::inverse(p));
+            put_m4(p);
+        } else if (cmd == "pt" || cmd == "vec" || cmd == "nrm") {
+            const xf::Mat4 m = m4();
+            const xf::Vec3 v = v3();
+            xf::Vec3 o;
+            if (cmd == "pt") o = xf::apply_point(m, v);
+            else if (cmd == "vec") o = xf::apply_vector(m, v);
+            else o = xf::normalized(xf::apply_normal(xf::inverse(m), v));
+            r.insert(r.end(), {o.x, o.y, o.z});
+        } else {
+            throw std::runtime_error("unknown request " + cmd);
+        }
+    } catch (const std::exception &e) {
+        nh::set_host_error(e.what());
+        return -1;
+    }
+    if ((int32_t)r.size() > cap) { nh::set_host_error("output capacity too small"); return -1; }
+    std::memcpy(out, r.data(), r.size() * sizeof(float));
+    return (int32_t)r.size();
 }
 
 }  // extern "C"

@@ -165,6 +165,7 @@ _sig("nh_scene_set_bsdf", _i32, _vp, _u32, C.POINTER(nh_bsdf))
 _sig("nh_scene_set_integrator", _i32, _vp, _i32)
 _sig("nh_scene_free", None, _vp)
 _sig("nh_host_last_error", C.c_char_p)
+_sig("nh_debug_transform", _i32, C.c_char_p, _fp, _i32)
 _sig("nh_bvh_build", _i32, C.POINTER(nh_scene_desc), _i32, C.POINTER(_vp))
 _sig("nh_bvh_get_desc", _i32, _vp, C.POINTER(nh_bvh_desc))
 _sig("nh_bvh_free", None, _vp)
@@ -298,6 +299,16 @@ class Bvh:
     def indices(self) -> np.ndarray:
         d = self.desc
         return np.ctypeslib.as_array(d.indices, shape=(d.n_indices,)).copy()
+
+
+def debug_transform(request: str) -> np.ndarray:
+    """The loader's transform arithmetic on one request of oracle/eigen_xform_probe.cpp's protocol
+    (parity hook, include/nori_hip.h nh_debug_transform): float32 results."""
+    out = np.zeros(64, np.float32)
+    n = _lib.nh_debug_transform(request.encode(), _fptr(out), out.size)
+    if n < 0:
+        raise NoriError(f"debug_transform: {_lib.nh_host_last_error().decode()}")
+    return out[:n].copy()
 
 
 def device_count() -> int:

@@ -22,3 +22,9 @@ if [ -d "$REF/ext/eigen/Eigen" ]; then
   g++ -O2 -std=c++17 -ffp-contract=off -I"$REF/ext/eigen" "$(dirname "$0")/eigen_probe.cpp" -o "$OUT/eigen_probe"
   echo "built $OUT/eigen_probe"
 fi
+# Transform probe (oracle/eigen_xform_probe.cpp, test infrastructure): the parser's transform composition,
+# Matrix4f::inverse (SSE path) and the camera's sampleToCamera, evaluated by the reference's own Eigen
+if [ -d "$REF/ext/eigen/Eigen" ]; then
+  g++ -O2 -std=c++17 -ffp-contract=off -I"$REF/ext/eigen" "$(dirname "$0")/eigen_xform_probe.cpp" -o "$OUT/eigen_xform_probe"
+  echo "built $OUT/eigen_xform_probe"
+fi

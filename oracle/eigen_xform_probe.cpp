@@ -1,0 +1,158 @@
+// TEST INFRASTRUCTURE ONLY. Transform probe: compiled by oracle/build_ref.sh against the reference's
+// own vendored Eigen 3.3.8 (/root/reference/ext/eigen, unmodified) with the reference's floating-point
+// setup (x86-64 SSE2 vectorisation, no FMA contraction). It evaluates, with Eigen's own types, the
+// host-side transform arithmetic of the reference's scene setup, so tests/test_transforms.py can check
+// the product loader (optix-renderer_amd/host/scene_loader.cpp) bit for bit:
+//   - the parser's transform composition (src/utils/parser.cpp:308-360: Translation / Affine3f(matrix) /
+//     DiagonalMatrix / AngleAxis / lookat pre-multiplied onto an Affine3f), stored as a nori Transform
+//     (include/nori/transform.h:43, src/utils/transform.cpp:9-10: m_inverse = Matrix4f::inverse(), the
+//     SSE path ext/eigen/Eigen/src/LU/arch/Inverse_SSE.h:35-163);
+//   - PerspectiveCamera::update's sampleToCamera (src/cameras/perspective.cpp:68-95);
+//   - Transform * Point3f / Vector3f / Normal3f (include/nori/transform.h:73-86) and the OBJ loader's
+//     (trafo * n).normalized() (src/shapes/obj.cpp:107,121).
+// The Eigen expressions below are those the reference writes; nothing else of the reference is used.
+//
+// Protocol: one request per stdin line, one reply line per request on stdout. Every float is given
+// and returned as the 8-hex-digit bit pattern of an IEEE single.
+//   inv  m[16]                          -> Matrix4f(m).inverse()                           (16)
+//   xf   n op...                        -> Transform(composed.matrix()): matrix, inverse   (32)
+//        op: t x y z | s x y z | r angle_deg ax ay az | m m[16] | l ox oy oz tx ty tz ux uy uz
+//   cam  w h fov near far               -> sampleToCamera matrix, and the matrix it inverts (32)
+//   pt   m[16] x y z                    -> Transform(m) * Point3f                           (3)
+//   vec  m[16] x y z                    -> Transform(m) * Vector3f                          (3)
+//   nrm  m[16] x y z                    -> (Transform(m) * Normal3f).normalized()           (3)
+// Matrices are row-major in the protocol.
+#include <Eigen/Core>
+#include <Eigen/Geometry>
+#include <Eigen/LU>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+#include <sstream>
+#include <string>
+
+namespace {
+
+float fb(const std::string &hex) {
+    uint32_t u = (uint32_t)std::stoul(hex, nullptr, 16);
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+void put(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    std::printf(" %08x", u);
+}
+float next(std::istringstream &in) {
+    std::string t;
+    in >> t;
+    return fb(t);
+}
+Eigen::Matrix4f read_m4(std::istringstream &in) {
+    Eigen::Matrix4f m;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) m(i, j) = next(in);
+    return m;
+}
+void put_m4(const Eigen::Matrix4f &m) {
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) put(m(i, j));
+}
+Eigen::Vector3f read_v3(std::istringstream &in) {
+    float x = next(in), y = next(in), z = next(in);
+    return Eigen::Vector3f(x, y, z);
+}
+// include/nori/common.h:218
+inline float degToRad(float value) { return value * (M_PI / 180.0f); }
+
+}  // namespace
+
+int main() {
+    std::string line;
+    while (std::getline(std::cin, line)) {
+        std::istringstream in(line);
+        std::string cmd;
+        in >> cmd;
+        if (cmd == "inv") {
+            const Eigen::Matrix4f m = read_m4(in);
+            const Eigen::Matrix4f r = m.inverse();
+            put_m4(r);
+        } else if (cmd == "xf") {
+            int n = 0;
+            in >> n;
+            Eigen::Affine3f transform;
+            transform.setIdentity();
+            for (int k = 0; k < n; ++k) {
+                std::string op;
+                in >> op;
+                if (op == "t") {
+                    const Eigen::Vector3f v = read_v3(in);
+                    transform = Eigen::Translation<float, 3>(v.x(), v.y(), v.z()) * transform;
+                } else if (op == "s") {
+                    const Eigen::Vector3f v = read_v3(in);
+                    transform = Eigen::DiagonalMatrix<float, 3>(v) * transform;
+                } else if (op == "r") {
+                    const float angle = degToRad(next(in));
+                    const Eigen::Vector3f axis = read_v3(in);
+                    transform = Eigen::AngleAxis<float>(angle, axis) * transform;
+                } else if (op == "m") {
+                    const Eigen::Matrix4f matrix = read_m4(in);
+                    transform = Eigen::Affine3f(matrix) * transform;
+                } else if (op == "l") {
+                    const Eigen::Vector3f origin = read_v3(in), target = read_v3(in), up = read_v3(in);
+                    const Eigen::Vector3f dir = (target - origin).normalized();
+                    const Eigen::Vector3f left = up.normalized().cross(dir).normalized();
+                    const Eigen::Vector3f newUp = dir.cross(left).normalized();
+                    Eigen::Matrix4f trafo;
+                    trafo << left, newUp, dir, origin, 0, 0, 0, 1;
+                    transform = Eigen::Affine3f(trafo) * transform;
+                } else {
+                    std::fprintf(stderr, "bad op %s\n", op.c_str());
+                    return 2;
+                }
+            }
+            // PropertyList::setTransform(name, transform.matrix()) -> Transform(Matrix4f)
+            const Eigen::Matrix4f m = transform.matrix();
+            const Eigen::Matrix4f inv = m.inverse();
+            put_m4(m);
+            put_m4(inv);
+        } else if (cmd == "cam") {
+            const float w = next(in), h = next(in), fov = next(in), nearClip = next(in), farClip = next(in);
+            const Eigen::Vector2i outputSize((int)w, (int)h);
+            const float aspect = outputSize.x() / (float)outputSize.y();
+            const float recip = 1.0f / (farClip - nearClip), cot = 1.0f / std::tan(degToRad(fov / 2.0f));
+            Eigen::Matrix4f perspective;
+            perspective << cot, 0, 0, 0, 0, cot, 0, 0, 0, 0, farClip * recip, -nearClip * farClip * recip, 0, 0, 1, 0;
+            const Eigen::Matrix4f prod = Eigen::DiagonalMatrix<float, 3>(Eigen::Vector3f(0.5f, -0.5f * aspect, 1.0f)) *
+                                         Eigen::Translation<float, 3>(1.0f, -1.0f / aspect, 0.0f) * perspective;
+            // Transform(prod).inverse() = Transform(prod.inverse(), prod): sampleToCamera's matrix
+            put_m4(prod.inverse());
+            put_m4(prod);
+        } else if (cmd == "pt" || cmd == "vec" || cmd == "nrm") {
+            const Eigen::Matrix4f m = read_m4(in);
+            const Eigen::Matrix4f inv = m.inverse();
+            const Eigen::Vector3f v = read_v3(in);
+            Eigen::Vector3f r;
+            if (cmd == "pt") {
+                const Eigen::Vector4f res = m * Eigen::Vector4f(v[0], v[1], v[2], 1.0f);
+                r = res.head<3>() / res.w();
+            } else if (cmd == "vec") {
+                r = m.topLeftCorner<3, 3>() * v;
+            } else {
+                r = (inv.topLeftCorner<3, 3>().transpose() * v).normalized();
+            }
+            put(r.x()); put(r.y()); put(r.z());
+        } else if (cmd.empty()) {
+            continue;
+        } else {
+            std::fprintf(stderr, "bad command %s\n", cmd.c_str());
+            return 2;
+        }
+        std::printf("\n");
+    }
+    return 0;
+}
