@@ -9,7 +9,8 @@ diffuse), 1024x1024, 256 spp, path_mis, per-path pcg32 seeding. One step = `--ro
 paths) or, with --mode megakernel, one path-kernel launch; then the ImageBlock splat. The
 default K=16 steps render the full 256 spp.
 
-Multi-GPU: one process per GPU (torchrun), 32x32 image blocks dealt round-robin to ranks (tile
+Multi-GPU: one process per GPU (torchrun; `python bench.py --gpus N` without a launcher starts the N ranks
+itself as a child torch.distributed.run), 32x32 image blocks dealt round-robin to ranks (tile
 shard), one RCCL reduce (sum) of the RGBW framebuffer to rank 0 inside the timed region, max
 time over ranks. --scaling weak (default): a step is N x --rounds sample rounds over each rank's
 1/N of the blocks, so every GPU traces the same 16.7M samples per step at any N. --scaling
@@ -78,6 +79,11 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (production); gloo = host-side reduce, for rehearsing the "
                         "multi-process flow with several ranks on one GPU")
+    p.add_argument("--dump-framebuffer", default=None,
+                   help="rank 0 saves the reduced RGBW framebuffer of the timed steps (.npy) before the roofline pass")
+    p.add_argument("--launcher-selftest", action="store_true",
+                   help="only rendezvous: every rank all-reduces its rank over gloo and rank 0 prints the world size "
+                        "(tests the --gpus N launcher without a GPU)")
     a = p.parse_args()
     a.config_given = a.config is not None
     a.config = a.config or "c2"
@@ -343,12 +349,15 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
     t_start = time.perf_counter()
     for s in range(steps):
         ctx.render(s * R, (s + 1) * R, seed=a.seed, blocks=blocks, traversal=trav, clear=False, mode=mode)
+    reduced = None
     if dist is not None:
-        reduce_framebuffer(ctx, dist, args, local)
+        reduced = reduce_framebuffer(ctx, dist, args, local, rank)
     ctx.synchronize()
     elapsed = time.perf_counter() - t_start
     if dist is not None:
         elapsed = max_over_ranks(elapsed, dist, args, local)
+    if args.dump_framebuffer and rank == 0:
+        np.save(args.dump_framebuffer, reduced if reduced is not None else ctx.framebuffer())
     st = ctx.stats()
     roof_pass = None
     if a.mode == "wavefront" and a.pools != 1 and calib is not None and a.roofline_steps > 0:
@@ -377,16 +386,20 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
             "roof": roof, "bvh_s": bvh_s, "upload_s": upload_s, "ctx": ctx}
 
 
-def reduce_framebuffer(ctx, dist, args, local):
+def reduce_framebuffer(ctx, dist, args, local, rank):
+    """One sum-reduce of the RGBW framebuffer to rank 0. Returns rank 0's reduced framebuffer for a host-side
+    (gloo) reduce, None otherwise (RCCL reduces in place into rank 0's device framebuffer)."""
     import torch
     ptr, n = ctx.framebuffer_device_ptr()  # completes every submitted chunk first
     if args.dist_backend == "nccl":
         fb = _wrap_device(ptr, n, local)
         dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
         torch.cuda.synchronize()
-    else:
-        fb = torch.from_numpy(ctx.framebuffer().reshape(-1))
-        dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+        return None
+    host = ctx.framebuffer()
+    fb = torch.from_numpy(host.reshape(-1))
+    dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+    return host if rank == 0 else None
 
 
 def max_over_ranks(elapsed, dist, args, local):
@@ -431,7 +444,9 @@ def denoise_record(nh, ctx, scene, no_cpu):
 def traversal_1m(nh, args, local):
     """perf-1M: the north star's traversal roofline target is set on the BVH-traversal
     kernel of the ~1M-triangle scene at 1 GPU; measured here in the same run (a short bench of it)."""
-    r = run_workload(nh, args, "bumpy1m", args.traversal_1m_steps, 1, local)
+    a = argparse.Namespace(**vars(args))
+    a.dump_framebuffer = None
+    r = run_workload(nh, a, "bumpy1m", args.traversal_1m_steps, 1, local)
     roof = r["roof"]
     e = roof["stages"]["extend"]
     traffic, source = pmc_traffic(f"bumpy1m_{r['W']}x{r['H']}_r{r['R']}_{args.traversal}_{args.mode}")
@@ -450,9 +465,47 @@ def traversal_1m(nh, args, local):
     return out
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher around it: start N ranks (one process per GPU) as a
+    child torch.distributed.run and exit with its status. Runs before anything touches torch.cuda or the HIP
+    library, and starts a child rather than exec'ing."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL between the rank processes
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launcher_selftest(args):
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(dist.get_rank())])
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"n_gpus": dist.get_world_size(), "rank_sum": float(t.item()),
+                          "gpus_arg": args.gpus}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: using the launcher's world size", file=sys.stderr)
+    if args.launcher_selftest:
+        return launcher_selftest(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

@@ -85,10 +85,23 @@ struct CommSet {
     std::vector<int> devices;
     std::vector<ncclComm_t> comms;
     ~CommSet() {
+        int cur = 0;
+        const bool have = hipGetDevice(&cur) == hipSuccess;
         for (size_t i = 0; i < comms.size(); ++i) {
             (void)hipSetDevice(devices[i]);
             (void)ncclCommDestroy(comms[i]);
         }
+        if (have) (void)hipSetDevice(cur);  // leave the caller's thread on its own device
+    }
+};
+
+// restores the calling thread's current device when an entry point that walks several devices returns
+struct DeviceGuard {
+    int dev = 0;
+    bool ok = false;
+    DeviceGuard() { ok = hipGetDevice(&dev) == hipSuccess; }
+    ~DeviceGuard() {
+        if (ok) (void)hipSetDevice(dev);
     }
 };
 
@@ -239,6 +252,7 @@ int nh_create(int device, nh_ctx **out) {
 
 void nh_destroy(nh_ctx *c) {
     if (!c) return;
+    DeviceGuard guard;
     (void)hipSetDevice(c->device);
     (void)pipeline_drain(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -1073,7 +1087,36 @@ static int pool_finish(nh_ctx *c, WfPool &p) {
     return NH_OK;
 }
 
-static bool event_done(hipEvent_t e) { return hipEventQuery(e) == hipSuccess; }
+// 1 = the event completed, 0 = pending; an error (a fault in the work before the event) goes to err
+static int event_done(hipEvent_t e, hipError_t &err) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return 1;
+    if (q != hipErrorNotReady) err = q;
+    return 0;
+}
+
+// Device errors of this context's work so far (HIP errors are sticky per thread): checked at the end of
+// nh_render / nh_synchronize, so a fault in a render's kernels is reported by the call that submitted or
+// completed them, not by the next unrelated call (a denoise, a framebuffer read).
+static int check_device(nh_ctx *c, const char *where) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) {
+        for (WfPool &p : c->pools) {
+            if (!p.stream) continue;
+            const hipError_t q = hipStreamQuery(p.stream);
+            if (q != hipSuccess && q != hipErrorNotReady) { e = q; break; }
+        }
+    }
+    if (e == hipSuccess && c->stream) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q != hipSuccess && q != hipErrorNotReady) e = q;
+    }
+    if (e != hipSuccess) {
+        c->err = std::string(where) + ": device error in the rendering kernels: " + hipGetErrorString(e);
+        return NH_ERR_DEVICE;
+    }
+    return NH_OK;
+}
 
 static void pipeline_reset(nh_ctx *c) {
     for (WfPool &p : c->pools)
@@ -1089,6 +1132,7 @@ static int pipeline_run(nh_ctx *c, bool all) {
     const int n_pools = active_pools();
     for (;;) {
         bool progress = false;
+        hipError_t ev_err = hipSuccess;
         for (WfPool &p : c->pools) {
             int rc = NH_OK;
             // a chunk starts on an idle pool once every running chunk is draining (staggered pools)
@@ -1103,7 +1147,7 @@ static int pipeline_run(nh_ctx *c, bool all) {
                 rc = pool_enqueue(c, p);
                 progress = true;
             }
-            if (!rc && p.state == WfPool::COUNTS && event_done(p.copy_ev[(p.it - 1) % kRing])) {
+            if (!rc && p.state == WfPool::COUNTS && event_done(p.copy_ev[(p.it - 1) % kRing], ev_err)) {
                 rc = pool_read(c, p);
                 progress = true;
             }
@@ -1111,9 +1155,13 @@ static int pipeline_run(nh_ctx *c, bool all) {
                 rc = pool_splat(c, p);
                 progress = true;
             }
-            if (!rc && p.state == WfPool::FINISH && event_done(p.ev_splat)) {
+            if (!rc && p.state == WfPool::FINISH && event_done(p.ev_splat, ev_err)) {
                 rc = pool_finish(c, p);
                 progress = true;
+            }
+            if (!rc && ev_err != hipSuccess) {
+                c->err = std::string("wavefront pipeline: ") + hipGetErrorString(ev_err);
+                rc = NH_ERR_DEVICE;
             }
             if (rc) {
                 pipeline_reset(c);
@@ -1229,6 +1277,18 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     size_t budget = wavefront ? (size_t)24 << 30 : (size_t)1 << 30;
     if (const char *e = std::getenv(wavefront ? "NH_WF_BUDGET_MB" : "NH_RECORD_BUDGET_MB"))
         budget = (size_t)std::max(1L, std::atol(e)) << 20;
+    if (wavefront) {
+        // every active pool is sized for the chunk: cap the budget at this device's free memory (plus what
+        // the pools already hold) shared by the pools, with headroom, so several contexts on one GPU get
+        // smaller chunks instead of a failed allocation
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            size_t held = 0;
+            for (const WfPool &p : c->pools) held += p.cap * (kWfBytesPerPath + 20) + p.staging_cap * sizeof(float4);
+            const size_t avail = (size_t)((double)(free_b + held) * 0.85) / (size_t)active_pools();
+            budget = std::min(budget, std::max(avail, per_round_bytes));
+        }
+    }
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)rounds, budget / per_round_bytes));
     while ((size_t)chunk * per_round > (size_t)0x7fffffff) chunk = std::max(1, chunk / 2);
     if (wavefront) {  // path ids of a chunk are packed into 26 bits of the path state (nh_wavefront.hip)
@@ -1244,6 +1304,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
                                     q->traversal != NH_TRAVERSAL_REFERENCE, q->collect_stats != 0});
         rc = q->collect_stats ? pipeline_drain(c) : pipeline_run(c, false);
         if (rc) return rc;
+        if (int e = check_device(c, "nh_render")) return e;
     } else {
         if (c->rec_cap < (size_t)chunk * per_round) {
             (void)hipFree(c->rec);
@@ -1342,7 +1403,7 @@ int nh_synchronize(nh_ctx *c) {
     int rc = pipeline_drain(c);
     if (rc) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return NH_OK;
+    return check_device(c, "nh_synchronize");
 }
 
 int nh_get_framebuffer(nh_ctx *c, float *rgbw, size_t n) {
@@ -1435,7 +1496,14 @@ static int run_denoise(nh_ctx *c, float *fb, int W, int H, int bs, const nh_deno
     const size_t tile_rows = (size_t)std::min(H, BH + 2 * r);
     const size_t tile_cols = (size_t)std::min(W, chunk + (r + 1) * (BH - 1) + 2 * r);
     size_t tile_bytes = 2 * tile_rows * tile_cols * sizeof(float4);
-    if (tile_bytes > 64 * 1024 || chunk > nh::denoise_max_chunk() || std::getenv("NH_DENOISE_NO_TILE")) tile_bytes = 0;
+    // the tile plus the kernel's static LDS must fit one workgroup's LDS (and the 64 KiB of dynamic LDS a
+    // launch may request without raising the function's attribute)
+    int lds_per_block = 0;
+    HIP_TRY(c, hipDeviceGetAttribute(&lds_per_block, hipDeviceAttributeMaxSharedMemoryPerBlock, c->device));
+    const size_t static_lds = nh::denoise_tile_static_lds();
+    if (tile_bytes > 64 * 1024 || tile_bytes + static_lds > (size_t)lds_per_block || chunk > nh::denoise_max_chunk() ||
+        std::getenv("NH_DENOISE_NO_TILE"))
+        tile_bytes = 0;
     hipEvent_t e0, e1;
     HIP_TRY(c, hipEventCreate(&e0));
     HIP_TRY(c, hipEventCreate(&e1));
@@ -1515,6 +1583,7 @@ int nh_denoise_image(nh_ctx *c, float *rgbw, int32_t width, int32_t height, int3
 
 int nh_reduce_framebuffers(nh_ctx **ctxs, int32_t n, int32_t root) {
     if (!ctxs || n <= 0 || root < 0 || root >= n) return NH_ERR_INVALID;
+    DeviceGuard guard;
     for (int i = 0; i < n; ++i)
         if (!ctxs[i] || !ctxs[i]->has_scene || ctxs[i]->fb_floats != ctxs[0]->fb_floats) return NH_ERR_INVALID;
     for (int i = 0; i < n; ++i) {

@@ -252,6 +252,13 @@ int denoise_band_rows() { return kBandRows; }
 
 int denoise_max_chunk() { return kMaxChunk; }
 
+// static LDS of the tiled band kernel (s_val + s_px), added to the dynamic tile when sizing a launch
+size_t denoise_tile_static_lds() {
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&dn_band_kernel<true>)) != hipSuccess) return 0;
+    return a.sharedSizeBytes;
+}
+
 void launch_denoise_band(const DenoiseLaunch &P, int L, int n_bands, size_t tile_bytes, hipStream_t st) {
     if (tile_bytes) hipLaunchKernelGGL(dn_band_kernel<true>, dim3(n_bands), dim3(kDnThreads), tile_bytes, st, P, L);
     else hipLaunchKernelGGL(dn_band_kernel<false>, dim3(n_bands), dim3(kDnThreads), 0, st, P, L);

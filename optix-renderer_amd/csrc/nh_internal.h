@@ -78,6 +78,7 @@ void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, 
 void launch_denoise_variance(const DenoiseLaunch &P, hipStream_t st);
 int denoise_band_rows();
 int denoise_max_chunk();
+size_t denoise_tile_static_lds();
 // tile_bytes > 0: the LDS-tiled kernel with that much dynamic shared memory (both windows of a chunk)
 void launch_denoise_band(const DenoiseLaunch &P, int L, int n_bands, size_t tile_bytes, hipStream_t st);
 void launch_denoise_copy(const float4 *src, int src_stride, float4 *dst, int dst_stride, int width, int height,

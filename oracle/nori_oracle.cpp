@@ -1663,8 +1663,9 @@ int no_ttest_bsdf(const nh_bsdf *b, float angle_deg, uint64_t *state, uint64_t *
     Pcg32 rng;
     rng.state = *state;
     rng.inc = *inc;
-    // sphericalDirection(degToRad(angle), 0) (common.cpp:270-281): sincosf
-    float theta = angle_deg * (kPi / 180.0f);
+    // sphericalDirection(degToRad(angle), 0) (common.cpp:270-281): sincosf; degToRad promotes to double
+    // (common.h:218: value * (M_PI / 180.0f))
+    float theta = (float)((double)angle_deg * (3.14159265358979323846 / (double)180.0f));
     float st = f_sin(theta), ct = f_cos(theta), sp = f_sin(0.f), cp = f_cos(0.f);
     V3 wi = mk(st * cp, st * sp, ct);
     double m = 0, var = 0;

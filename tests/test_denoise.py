@@ -139,7 +139,10 @@ def rel_l2(a, b):
     (16, 16, 2, 0, 1, 1.0, 0.6),      # range 0: identity
     (40, 5, 2, 9, 1, 3.0, 0.6),       # narrower than the window
     (50, 3, 0, 15, 2, 5.0, 0.9),      # range 15: the largest chunk the tiled kernel precomputes
-    (24, 30, 2, 20, 1, 6.0, 1.5),     # range 20: window tile beyond 64 KB -> the untiled kernel
+    (24, 30, 2, 20, 1, 6.0, 1.5),     # range 20: chunk 21 > 16 precomputed steps -> the untiled kernel
+    (70, 100, 2, 9, 1, 6.0, 1.5),     # range 9: full-size tile (45 KB) + the kernel's static LDS
+    (64, 96, 2, 10, 1, 6.0, 1.5),     # range 10: full-size tile 48 KB, with the static LDS 74 KB
+    (72, 112, 1, 11, 1, 6.0, 1.5),    # range 11: full-size tile 57 KB, with the static LDS 83 KB
 ])
 @pytest.mark.parametrize("tile", [True, False], ids=["tile", "global"])
 def test_denoise_image_matches_oracle(gpu, monkeypatch, tile, h, w, bs, r, amount, sigma_d, sigma_vr):

@@ -51,3 +51,49 @@ def test_tile_shard_reduce_world2(tmp_path):
     full = no.OracleScene(nh.Scene(xml)).render(0, 4, seed=21, threads=4)
     err = np.sqrt(((reduced.astype(np.float64) - full) ** 2).sum() / (full.astype(np.float64) ** 2).sum())
     assert err < 1e-6, err
+
+
+def _bench(args, timeout=600):
+    import json
+    import subprocess
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`python bench.py --gpus 2` with no launcher around it starts two ranks itself (a child
+    torch.distributed.run); here only their rendezvous runs (gloo, no GPU)."""
+    line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--launcher-selftest"], timeout=300)
+    assert line["n_gpus"] == 2 and line["rank_sum"] == 1.0
+
+
+@pytest.mark.gpu
+def test_bench_two_hip_ranks_reduce_to_one_rank_render(tmp_path, gpu):
+    """bench.py --gpus 2: both ranks render their tile shard with the HIP path (gloo reduce, both on GPU 0);
+    the reduced framebuffer equals one HIP render of the whole image over the same sample range
+    (src/utils/render.cpp:281-347 semantics: the samples of a block do not depend on who renders it), up to
+    fp32 summation order where block footprints overlap."""
+    sys.path.insert(0, os.path.join(REPO, "optix-renderer_amd"))
+    import nori_hip as nh
+    import scenegen
+    out = str(tmp_path / "reduced.npy")
+    line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--config", "c2", "--width", "160", "--height", "96",
+                   "--rounds", "2", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-denoise",
+                   "--traversal-1m-steps", "0", "--roofline-steps", "0", "--dump-framebuffer", out])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    reduced = np.load(out).astype(np.float64)
+    xml = scenegen.cbox_xml(str(tmp_path), "c2", width=160, height=96)
+    s = nh.Scene(xml)
+    ctx = nh.Context(0)
+    ctx.upload(s, nh.Bvh(s))
+    R = 2 * 2  # --rounds x world: each rank's weak-scaling step
+    ctx.render(0, 2 * R, seed=1234, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT)
+    full = ctx.framebuffer().astype(np.float64)
+    ctx.close()
+    err = np.sqrt(((reduced - full) ** 2).sum() / (full ** 2).sum())
+    assert err < 1e-6, err
