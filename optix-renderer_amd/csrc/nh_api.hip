@@ -73,6 +73,7 @@ struct WfPool {
     WfLaunch L{};
     bool persistent = false, wide = false, tail = false, draining = false;
     bool fused = false, sorted = false;  // one wf_bounce kernel per bounce (LDS-staged BVH); material-sorted queue
+    bool rr = false;                     // fused kernels with the next vertex's Russian roulette ahead (wf_bounce_rr)
     int64_t tail_at = 0, drain_at = 0;
     int it = 0;
     std::vector<uint64_t> in_e, in_s;  // live paths / shadow rays entering each bounce
@@ -488,6 +489,55 @@ static std::vector<float4> collapse_wide(const std::vector<float4> &nodes, const
     return wide;
 }
 
+// Number the K wide nodes most rays visit first, so the persistent traversal can keep them in LDS: the
+// connected top of the tree grown from the root by the largest child-box surface area (a ray's chance
+// of entering a box grows with its area). The other nodes keep their depth-first order. Renumbering
+// moves no box and changes no visit order: every answer is unchanged. Returns the top's size.
+static int number_top_first(std::vector<float4> &wide, const float root_min[3], const float root_max[3], int K) {
+    const int n = (int)(wide.size() / nhd::kWideF4);
+    if (n == 0 || K <= 0) return 0;
+    auto area = [](const float *mn, const float *mx) {
+        const float x = mx[0] - mn[0], y = mx[1] - mn[1], z = mx[2] - mn[2];
+        return x * y + y * z + z * x;
+    };
+    std::vector<int> order;  // new index -> old index, for the top
+    std::vector<char> in_top(n, 0);
+    std::vector<std::pair<float, int>> heap{{area(root_min, root_max), 0}};
+    while (!heap.empty() && (int)order.size() < K) {
+        std::pop_heap(heap.begin(), heap.end());
+        const int g = heap.back().second;
+        heap.pop_back();
+        order.push_back(g);
+        in_top[g] = 1;
+        const float *f = reinterpret_cast<const float *>(&wide[(size_t)g * nhd::kWideF4]);
+        int refs[4];
+        std::memcpy(refs, f + 24, 16);
+        for (int j = 0; j < 4; ++j) {
+            if (refs[j] < 0) continue;  // a leaf or an empty slot
+            const float mn[3] = {f[j], f[4 + j], f[8 + j]}, mx[3] = {f[12 + j], f[16 + j], f[20 + j]};
+            heap.push_back({area(mn, mx), refs[j]});
+            std::push_heap(heap.begin(), heap.end());
+        }
+    }
+    std::vector<int> perm(n);  // old -> new
+    for (int i = 0; i < (int)order.size(); ++i) perm[order[i]] = i;
+    int next = (int)order.size();
+    for (int g = 0; g < n; ++g)
+        if (!in_top[g]) perm[g] = next++;
+    std::vector<float4> out(wide.size());
+    for (int g = 0; g < n; ++g) {
+        float4 *dst = &out[(size_t)perm[g] * nhd::kWideF4];
+        std::memcpy(dst, &wide[(size_t)g * nhd::kWideF4], nhd::kWideF4 * sizeof(float4));
+        int refs[4];
+        std::memcpy(refs, &dst[6], 16);
+        for (int j = 0; j < 4; ++j)
+            if (refs[j] >= 0) refs[j] = perm[refs[j]];
+        std::memcpy(&dst[6], refs, 16);
+    }
+    wide.swap(out);
+    return (int)order.size();
+}
+
 int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     if (!c || !b) return NH_ERR_INVALID;
     if (!c->has_scene) return fail(c, "nh_upload_bvh: upload the scene first"), NH_ERR_STATE;
@@ -603,7 +653,11 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     if (tree_depth + 2 > (uint32_t)kMaxStack)
         return fail(c, "BVH deeper than " + std::to_string(kMaxStack - 2) + " levels is not supported"), NH_ERR_UNSUPPORTED;
     int depth4 = 0;
-    const std::vector<float4> wide = collapse_wide(nodes, leaves, depth4);
+    std::vector<float4> wide = collapse_wide(nodes, leaves, depth4);
+    // the top of the tree the persistent kernels stage in LDS (NH_TREE_TOP: its size, 0 = none)
+    int top_k = nh::tree_top_nodes();
+    if (const char *e = std::getenv("NH_TREE_TOP")) top_k = std::min(std::max(0, std::atoi(e)), top_k);
+    c->tv.n_top = S.root_kind == 1 ? number_top_first(wide, S.root_min, S.root_max, top_k) : 0;
     int rc;
     c->n_node_f4 = (int)nodes.size();
     c->n_leaves = (int)leaves.size();
@@ -864,6 +918,8 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     p.fused = small && !p.persistent && c->depth <= 16;
     if (const char *e = std::getenv("NH_FUSED")) p.fused = p.fused && e[0] != '0';
     p.sorted = p.fused && c->n_bsdf_types > 1;
+    p.rr = p.fused;
+    if (const char *e = std::getenv("NH_RR_AHEAD")) p.rr = p.fused && e[0] != '0';
     if (const char *e = std::getenv("NH_SORT")) p.sorted = p.fused && e[0] == '1';
     c->stats.fused_bounce = p.fused ? 1 : 0;
     c->stats.node_bytes = p.wide ? 16 * nhd::kWideF4 : 64;
@@ -921,7 +977,8 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
         HIP_TRY(c, hipEventRecord(ev[1], p.stream));
         HIP_TRY(c, hipEventRecord(ev[2], p.stream));
         if (it > 0 && (int64_t)bound <= p.tail_at) {
-            nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, false, bound, c->depth, p.stream);
+            if (p.rr) nh::launch_wf_tail_rr(c->d_scene, c->tv, L, ordered, stats, bound, p.stream);
+            else nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, false, bound, c->depth, p.stream);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev[3], p.stream));
             p.tail = true;
@@ -929,7 +986,8 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
             p.state = WfPool::SPLAT;
             return NH_OK;
         }
-        nh::launch_wf_bounce(c->d_scene, c->tv, L, ordered, stats, p.sorted, bound, p.stream);
+        if (p.rr) nh::launch_wf_bounce_rr(c->d_scene, c->tv, L, ordered, stats, p.sorted, bound, p.stream);
+        else nh::launch_wf_bounce(c->d_scene, c->tv, L, ordered, stats, p.sorted, bound, p.stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], p.stream));
         unsigned *h = p.h_counts + (size_t)(it % kRing) * 2 * kCountGroup;

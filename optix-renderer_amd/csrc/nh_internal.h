@@ -78,6 +78,7 @@ void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, 
 void launch_denoise_variance(const DenoiseLaunch &P, hipStream_t st);
 int denoise_band_rows();
 int denoise_max_chunk();
+int tree_top_nodes();  // wide nodes the persistent traversal stages in LDS (nh_wavefront.hip)
 size_t denoise_tile_static_lds();
 // tile_bytes > 0: the LDS-tiled kernel with that much dynamic shared memory (both windows of a chunk)
 void launch_denoise_band(const DenoiseLaunch &P, int L, int n_bands, size_t tile_bytes, hipStream_t st);
@@ -147,6 +148,12 @@ void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLau
 // fused shade + any-hit + closest-hit bounce for LDS-staged BVHs; sort = material-sorted output queue
 void launch_wf_bounce(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                       bool sort, int bound, hipStream_t st);
+// RR-ahead variants of the fused bounce / tail (nh_wavefront.hip): the stored state is a path after its
+// vertex's Russian roulette
+void launch_wf_bounce_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
+                         int bound, hipStream_t st);
+void launch_wf_tail_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
+                       hipStream_t st);
 void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                     bool wide, int bound, int depth, hipStream_t st);
 }  // namespace nh

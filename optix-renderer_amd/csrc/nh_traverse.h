@@ -218,6 +218,9 @@ struct Traversal {
     // LDS-staged scenes (wf_bounce): records k and k+1 interleaved component by component, kPairF4 float4
     // per k, so a primitive pair loads straight into packed-FP32 register pairs (leaf_test<.., PAIRS>)
     const float4 *ppairs;
+    // the first n_top wide nodes are the top of the tree (the nodes most rays visit, nh_api.hip numbers
+    // them first); the persistent traversal kernels read those from an LDS copy
+    int n_top;
 };
 // pair k: (a.x a.x') (a.y a.y') | (a.z a.z') (a.w a.w') | (b.x b.x') (b.y b.y') | (b.z b.z') (c.x c.x') |
 //         (c.y c.y') (c.z c.z') | (c.w c.w') (0 0)      -- unprimed record k, primed record k+1
@@ -675,7 +678,9 @@ struct Tracer4 {
     // each part only if the lane has that work. A wave executes every part some lane needs anyway,
     // so chaining them lets a lane do a pop, a node and a primitive for the cost of one divergent
     // iteration; the per-lane sequence of operations (and so every result and counter) is unchanged.
-    NHD void step(const Traversal &tv, Stack &stk, TravStats &st) {
+    NHD void step(const Traversal &tv, Stack &stk, TravStats &st) { step(tv, stk, st, nullptr, 0); }
+    // top / n_top: an LDS copy of the first n_top wide nodes (0: every node from tv.wnodes)
+    NHD void step(const Traversal &tv, Stack &stk, TravStats &st, const float4 *top, int n_top) {
         if (k < 0 && cur < 0) {  // deferred children: the visit-time test against the current maxt
             while (sp > 0) {
                 int ref;
@@ -695,9 +700,17 @@ struct Tracer4 {
         }
 #pragma unroll 1
         for (int it = 0; it < NH_NODES_PER_STEP && cur >= 0; ++it) {  // one wide node: test its child boxes
-            const float4 *n = tv.wnodes + (size_t)kWideF4 * cur;
-            const float4 mnx = n[0], mny = n[1], mnz = n[2], mxx = n[3], mxy = n[4], mxz = n[5];
-            const int4 ref = *reinterpret_cast<const int4 *>(&n[6]);
+            float4 mnx, mny, mnz, mxx, mxy, mxz;
+            int4 ref;
+            if (cur < n_top) {  // the top of the tree, from the workgroup's LDS copy
+                const float4 *n = top + kWideF4 * cur;
+                mnx = n[0]; mny = n[1]; mnz = n[2]; mxx = n[3]; mxy = n[4]; mxz = n[5];
+                ref = *reinterpret_cast<const int4 *>(&n[6]);
+            } else {
+                const float4 *n = tv.wnodes + (size_t)kWideF4 * cur;
+                mnx = n[0]; mny = n[1]; mnz = n[2]; mxx = n[3]; mxy = n[4]; mxz = n[5];
+                ref = *reinterpret_cast<const int4 *>(&n[6]);
+            }
             float n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f;
             bool v0, v1, v2, v3;
             if (finite_r) {

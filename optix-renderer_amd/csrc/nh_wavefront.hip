@@ -180,6 +180,8 @@ __device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, cons
     t.prims = prims;
     t.leaves = leaves;
     t.ppairs = nullptr;
+    t.wnodes = tv.wnodes;
+    t.n_top = 0;
     if constexpr (PAIRS) {
         float4 *pairs = lds + small_pairs_offset_f4(L);
         const int n = L.small_prims / 3;
@@ -271,6 +273,10 @@ constexpr int kTraceBlocksMax = 1 << 20;
 #define NH_RING_ENTRIES 16
 #endif
 constexpr int kRingEntries = NH_RING_ENTRIES;
+#ifndef NH_TOP_NODES
+#define NH_TOP_NODES 16
+#endif
+constexpr int kTopNodes = NH_TOP_NODES;  // wide nodes per LDS copy of the top of the tree (kTopNodes * 128 B)
 //
 // WIDE: the 4-wide collapse of the tree (Tracer4), LDS window of 8 (ref, distance) pairs per lane.
 template <bool WIDE>
@@ -329,7 +335,13 @@ __device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S,
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool WIDE>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES))) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[kRingEntries * 128];
+    __shared__ float4 s_top[WIDE ? kTopNodes * kWideF4 : 1];  // the top of the 4-wide tree (nodes 0 .. n_top-1)
     const DScene &S = *Sp;
+    const int n_top = WIDE ? min(tv.n_top, kTopNodes) : 0;
+    if constexpr (WIDE) {
+        for (int i = threadIdx.x; i < n_top * kWideF4; i += 128) s_top[i] = tv.wnodes[i];
+        __syncthreads();
+    }
     const QView qv = queue_view(L.cnt_in + (ANY ? kCountGroup : 0));
     const int n = qv.n;
     const int *pre = qv.pre;
@@ -383,7 +395,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
         }
         if (!__any(slot >= 0)) break;
         if (slot >= 0) {
-            if (!tr.done) tr.step(tv, my_stk, st);
+            if constexpr (WIDE) {
+                if (!tr.done) tr.step(tv, my_stk, st, s_top, n_top);
+            } else {
+                if (!tr.done) tr.step(tv, my_stk, st);
+            }
             if (tr.done) {
                 if (ANY) {
                     B.occl[L.st.sh_slot[slot]] = tr.found ? 1 : 0;
@@ -428,191 +444,235 @@ struct RegState {
     __device__ __forceinline__ float4 pending() const { return o.pe; }
 };
 
+// A path between two kernels or shade steps: its vertex's incoming ray (org, d), Li, throughput t, the MIS
+// weights, its random-number stream, flags and path id.
+struct PathV {
+    F3 org, d, li, t;
+    float w_mats, w_ems;
+    Rng rng;
+    int flags, pid;
+};
+
+// The head of a shade step (path_mis.cpp:26-71 / path_mats.cpp:22-56): with the hit of the path's ray,
+// finish the previous bounce's MIS probe weight (w_mats, :117-140), take the escaped ray's environment term
+// or the hit's emitter term, then Russian roulette. Returns whether the path survives; its = the hit's
+// Intersection. The previous bounce's pending light sample (F_NEE) must be resolved already.
+__device__ __forceinline__ bool shade_head(const DScene &S, const Traversal &tv, PathV &v, const Hit &h, bool found,
+                                           float pdfmat, Its &its) {
+    bool have_its = false;
+    if (S.integrator == 1) {  // ---------------- path_mats (path_mats.cpp:16-78)
+        if (!found) {  // path_mats.cpp:26-35
+            if (S.envmap >= 0) v.li = add(v.li, mulc(v.t, env_eval(S, v.d)));
+            return false;
+        }
+        hit_info(S, tv, h, v.org, v.d, its);
+        const DShape shape = S.shapes[its.shape];
+        if (shape.emitter >= 0) {
+            const F3 wi = normalized(sub(its.p, v.org));
+            v.li = add(v.li, mulc(v.t, emitter_eval(S.emitters[shape.emitter], v.org, its.sh.n, wi)));
+        }
+        int counter = (v.flags >> 4) & 3;
+        const float succ = e_min(max_coeff(v.t), 0.99f);
+        if (counter < 3) counter++;
+        else if (v.rng.next1d() > succ) return false;
+        else v.t = divs(v.t, succ);
+        v.flags = (v.flags & ~0x30) | (counter << 4);
+        return true;
+    }
+    // ---------------- path_mis
+    const float n_lights = (float)S.n_emitters;
+    if (!(v.flags & F_FIRST)) {  // finish the previous bounce (path_mis.cpp:115-140)
+        // the MIS probe hit an emitter (:117-133): w_mats from the pdfs of both strategies
+        if (!(v.flags & F_ZERO_COL) && found) {
+            hit_info(S, tv, h, v.org, v.d, its);
+            have_its = true;
+            const int hem = S.shapes[its.shape].emitter;
+            if (hem >= 0) {
+                const F3 wim = normalized(sub(its.p, v.org));
+                const float pdfmat_ems = emitter_pdf(S, S.emitters[hem], v.org, its.p, its.sh.n, wim) / n_lights;
+                if ((pdfmat + pdfmat_ems) > kEps) v.w_mats = pdfmat / (pdfmat + pdfmat_ems);
+            }
+        }
+        if (v.flags & F_DISCRETE) v.w_mats = 1.f;  // :136-140
+    }
+    if (!found) {  // path_mis.cpp:32-44: escaped rays see the environment map, no MIS weight
+        if (S.envmap >= 0) v.li = add(v.li, mulc(v.t, env_eval(S, v.d)));
+        return false;
+    }
+    if (!have_its) hit_info(S, tv, h, v.org, v.d, its);
+    const DShape shape = S.shapes[its.shape];
+    if (shape.emitter >= 0) {  // path_mis.cpp:51-56, ref = ray origin
+        const F3 wi = normalized(sub(its.p, v.org));
+        v.li = add(v.li, mulc(scl(v.w_mats, v.t), emitter_eval(S.emitters[shape.emitter], v.org, its.sh.n, wi)));
+    }
+    float succ = e_min(max_coeff(v.t), 0.99f);  // RR from depth 0 (path_mis.cpp:58-71)
+    succ = e_max(succ, kEps);
+    if (v.rng.next1d() > succ) return false;
+    v.t = divs(v.t, succ);
+    return true;
+}
+
+// The body of a shade step for a path that survived its head (path_mis.cpp:73-146 / path_mats.cpp:58-76):
+// NEE sample (path_mis), BSDF sample, this bounce's MIS-weighted light term and t *= bsdf weight. Writes the
+// path's next state to o; nee = a light sample whose shadow ray (so, sd) decides o.pe (F_NEE).
+__device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv, PathV &v, const Its &its, PState &o,
+                                           bool &nee, float4 &so, float4 &sd) {
+    const DShape shape = S.shapes[its.shape];
+    const DBsdf bsdf = S.bsdfs[shape.bsdf];
+    nee = false;
+    if (S.integrator == 1) {  // path_mats: BSDF sample only
+        const float bx = v.rng.next1d(), by = v.rng.next1d();
+        F3 wo;
+        int measure;
+        const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(v.d)), bx, by, wo, measure);
+        const F3 nd = to_world(its.sh, wo);
+        v.t = mulc(v.t, col);  // path_mats.cpp: the throughput update of this bounce
+        o.pdfmat = 0.f;
+        o.ro = make_float4(its.p.x, its.p.y, its.p.z, kEps);
+        o.rd = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
+        o.flags = v.flags & 0x30;
+    } else {
+        const float n_lights = (float)S.n_emitters;
+        const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, v.rng.next1d());
+        const DEmitter em = S.emitters[ei];
+        const float ex = v.rng.next1d(), ey = v.rng.next1d();
+        ESample es;
+        const F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
+        const F3 wi_l = to_local(its.sh, neg(v.d));
+        nee = !is_zero(ems_col);
+        F3 li_ems = f3(0, 0, 0);
+        float pdfems = 0.f, pdfems_mats = 0.f;
+        if (nee) {
+            const F3 we = to_local(its.sh, es.wi);
+            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
+            const float cs = we.z;
+            li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights, ems_col.z * cs * f.z * n_lights);
+            pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
+            pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
+            so = make_float4(es.so.x, es.so.y, es.so.z, es.smint);
+            sd = make_float4(es.sd.x, es.sd.y, es.sd.z, es.smaxt);
+        }
+        const float bx = v.rng.next1d(), by = v.rng.next1d();
+        F3 wo;
+        int measure;
+        const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
+        const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
+        const F3 nd = to_world(its.sh, wo);
+        // w_ems of this bounce (:103-106): the occluded shadow ray leaves both pdfs 0 (w_ems keeps its
+        // value), the unoccluded one sets it from them; a discrete sample zeroes it either way (:136-140)
+        const bool discrete = measure == M_DISCRETE;
+        float w_occ = v.w_ems, w_un = v.w_ems;
+        if (nee && (pdfems_mats + pdfems) > kEps) w_un = pdfems / (pdfems_mats + pdfems);
+        if (discrete) w_occ = w_un = 0.f;
+        int fl = (discrete ? F_DISCRETE : 0) | (is_zero(bsdf_col) ? F_ZERO_COL : 0);
+        if (nee && discrete) {
+            // the discrete sample zeroes both weights: a finite term (0 * t) * li_ems adds exactly zero
+            // occluded or not (Li never holds -0), so no shadow ray is queued (as the megakernel)
+            const F3 c = mulc(scl(w_un, v.t), li_ems), z = mulc(scl(w_occ, v.t), f3(0, 0, 0));
+            if (c.x == 0.f && c.y == 0.f && c.z == 0.f && z.x == 0.f && z.y == 0.f && z.z == 0.f) {
+                nee = false;
+                li_ems = f3(0, 0, 0);  // the unoccluded term is +-0: Li is unchanged either way
+            }
+        }
+        if (nee) {
+            // Li += w_ems * t * Li_ems (:142) once the shadow ray is known to be unoccluded
+            const F3 c = mulc(scl(w_un, v.t), li_ems);
+            o.pe = make_float4(c.x, c.y, c.z, w_un);
+            const F3 z = mulc(scl(w_occ, v.t), f3(0, 0, 0));
+            fl |= F_NEE | ((z.x != 0.f || z.y != 0.f || z.z != 0.f) ? F_ZNAN : 0);
+        } else {
+            v.li = add(v.li, mulc(scl(w_occ, v.t), li_ems));  // li_ems = 0: the same term, added now
+        }
+        v.w_ems = w_occ;
+        v.t = mulc(v.t, bsdf_col);  // :145
+        o.pdfmat = pdfmat;
+        o.ro = make_float4(its.p.x, its.p.y, its.p.z, kEps);
+        o.rd = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
+        o.flags = fl;
+    }
+    o.li = make_float4(v.li.x, v.li.y, v.li.z, v.w_mats);
+    o.thr = make_float4(v.t.x, v.t.y, v.t.z, v.w_ems);
+    o.rng = v.rng.state;
+    o.pid = v.pid;
+}
+
+// the path (state before its head) that a shade step's output o describes, its ray ending at the next hit
+__device__ __forceinline__ PathV path_of(const WfLaunch &L, const PState &o) {
+    PathV v;
+    v.org = xyz(o.ro);
+    v.d = xyz(o.rd);
+    v.li = xyz(o.li);
+    v.w_mats = o.li.w;
+    v.t = xyz(o.thr);
+    v.w_ems = o.thr.w;
+    v.rng.state = o.rng;
+    v.rng.inc = ((uint64_t)(L.s0 + o.pid / L.n_list) << 1u) | 1u;
+    v.flags = o.flags;
+    v.pid = o.pid;
+    return v;
+}
+
+__device__ __forceinline__ void write_radiance(const WfLaunch &L, const PathV &v) {
+    float4 *r = &L.rec_rgbx[v.pid];
+    r->x = v.li.x;
+    r->y = v.li.y;
+    r->z = v.li.z;
+}
+
 // One shade step of the path whose state src holds (slot s of the input queue), hv = the hit of its
-// ray. Returns whether the path continues (its next state in o); sets nee when it sampled a light
-// (shadow ray in so/sd). A terminated path writes its radiance to its sample record.
+// ray: head + body. Returns whether the path continues (its next state in o); sets nee when it sampled a
+// light (shadow ray in so/sd). A terminated path writes its radiance to its sample record.
 template <class Src>
 __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv, const WfLaunch &L, const Src &src,
                                            int s, const float4 hv, PState &o, bool &nee, float4 &so, float4 &sd) {
     float4 ro, rd, li4, th4;
-    int flags, pid;
-    Rng rng;
+    PathV v;
     if (L.first) {  // bounce 0: the state wf_generate used to write (dense queue: slot = path id)
         float jx, jy;
-        camera_sample(S, L, s, rng, ro, rd, jx, jy);
+        camera_sample(S, L, s, v.rng, ro, rd, jx, jy);
         li4 = make_float4(0.f, 0.f, 0.f, 1.f);   // Li, w_mats
         th4 = make_float4(1.f, 1.f, 1.f, 0.f);  // throughput, w_ems
-        flags = F_FIRST;
-        pid = s;
-        L.rec_rgbx[pid] = make_float4(0.f, 0.f, 0.f, jx);
-        L.rec_jy[pid] = jy;
+        v.flags = F_FIRST;
+        v.pid = s;
+        L.rec_rgbx[s] = make_float4(0.f, 0.f, 0.f, jx);
+        L.rec_jy[s] = jy;
     } else {
-        src.load(ro, rd, li4, th4, rng.state);
+        src.load(ro, rd, li4, th4, v.rng.state);
         const int bits = __float_as_int(rd.w);
-        flags = (int)((unsigned)bits >> kPidBits);
-        pid = bits & ((1 << kPidBits) - 1);
-        rng.inc = ((uint64_t)(L.s0 + pid / L.n_list) << 1u) | 1u;
+        v.flags = (int)((unsigned)bits >> kPidBits);
+        v.pid = bits & ((1 << kPidBits) - 1);
+        v.rng.inc = ((uint64_t)(L.s0 + v.pid / L.n_list) << 1u) | 1u;
     }
-    const F3 org = xyz(ro), d = xyz(rd);
-    F3 li = xyz(li4), t = xyz(th4);
-    float w_mats = li4.w, w_ems = th4.w;
+    v.org = xyz(ro);
+    v.d = xyz(rd);
+    v.li = xyz(li4);
+    v.t = xyz(th4);
+    v.w_mats = li4.w;
+    v.w_ems = th4.w;
     Hit h;
     h.t = hv.x;
     h.u = hv.y;
     h.v = hv.z;
     h.k = __float_as_int(hv.w);
     const bool found = h.k >= 0;
+    // the previous bounce's light sample counts unless occluded: its MIS-weighted term was computed by
+    // that bounce, Li += w_ems * t * Li_ems (:142), and w_ems is the unoccluded weight (:103-106)
+    if (S.integrator != 1 && !(v.flags & F_FIRST) && (v.flags & F_NEE)) {
+        if (!src.occluded()) {
+            const float4 pe = src.pending();
+            v.li = add(v.li, xyz(pe));
+            v.w_ems = pe.w;
+        } else if (v.flags & F_ZNAN) {
+            v.li = add(v.li, f3(NAN, NAN, NAN));  // (w_ems * t) * 0 with a non-finite product
+        }
+    }
     Its its;
-    bool have_its = false;
-    const float n_lights = (float)S.n_emitters;
-    bool alive = true;
-    if (S.integrator == 1) {  // ---------------- path_mats (path_mats.cpp:16-78)
-        if (!found) {  // path_mats.cpp:26-35
-            if (S.envmap >= 0) li = add(li, mulc(t, env_eval(S, d)));
-            alive = false;
-        } else {
-            hit_info(S, tv, h, org, d, its);
-            const DShape shape = S.shapes[its.shape];
-            const DBsdf bsdf = S.bsdfs[shape.bsdf];
-            if (shape.emitter >= 0) {
-                const F3 wi = normalized(sub(its.p, org));
-                li = add(li, mulc(t, emitter_eval(S.emitters[shape.emitter], org, its.sh.n, wi)));
-            }
-            int counter = (flags >> 4) & 3;
-            const float succ = e_min(max_coeff(t), 0.99f);
-            if (counter < 3) counter++;
-            else if (rng.next1d() > succ) alive = false;
-            else t = divs(t, succ);
-            if (alive) {
-                const float bx = rng.next1d(), by = rng.next1d();
-                F3 wo;
-                int measure;
-                const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure);
-                const F3 nd = to_world(its.sh, wo);
-                t = mulc(t, col);  // path_mats.cpp: the throughput update of this bounce
-                o.pdfmat = 0.f;
-                o.ro = make_float4(its.p.x, its.p.y, its.p.z, kEps);
-                o.rd = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
-                o.flags = counter << 4;
-            }
-        }
-    } else {  // ---------------- path_mis
-        if (!(flags & F_FIRST)) {  // finish the previous bounce (path_mis.cpp:103-146)
-            // the light sample counts unless occluded: its MIS-weighted term was computed by that
-            // bounce, Li += w_ems * t * Li_ems (:142), and w_ems is the unoccluded weight (:103-106)
-            if (flags & F_NEE) {
-                if (!src.occluded()) {
-                    const float4 pe = src.pending();
-                    li = add(li, xyz(pe));
-                    w_ems = pe.w;
-                } else if (flags & F_ZNAN) {
-                    li = add(li, f3(NAN, NAN, NAN));  // (w_ems * t) * 0 with a non-finite product
-                }
-            }
-            // the MIS probe hit an emitter (:117-133): w_mats from the pdfs of both strategies
-            if (!(flags & F_ZERO_COL) && found) {
-                hit_info(S, tv, h, org, d, its);
-                have_its = true;
-                const int hem = S.shapes[its.shape].emitter;
-                if (hem >= 0) {
-                    const float pdfmat = ro.w;
-                    const F3 wim = normalized(sub(its.p, org));
-                    const float pdfmat_ems = emitter_pdf(S, S.emitters[hem], org, its.p, its.sh.n, wim) / n_lights;
-                    if ((pdfmat + pdfmat_ems) > kEps) w_mats = pdfmat / (pdfmat + pdfmat_ems);
-                }
-            }
-            if (flags & F_DISCRETE) w_mats = 1.f;  // :136-140
-        }
-        if (!found) {  // path_mis.cpp:32-44: escaped rays see the environment map, no MIS weight
-            if (S.envmap >= 0) li = add(li, mulc(t, env_eval(S, d)));
-            alive = false;
-        } else {
-            if (!have_its) hit_info(S, tv, h, org, d, its);
-            const DShape shape = S.shapes[its.shape];
-            const DBsdf bsdf = S.bsdfs[shape.bsdf];
-            if (shape.emitter >= 0) {  // path_mis.cpp:51-56, ref = ray origin
-                const F3 wi = normalized(sub(its.p, org));
-                li = add(li, mulc(scl(w_mats, t), emitter_eval(S.emitters[shape.emitter], org, its.sh.n, wi)));
-            }
-            float succ = e_min(max_coeff(t), 0.99f);
-            succ = e_max(succ, kEps);
-            if (rng.next1d() > succ) {
-                alive = false;
-            } else {
-                t = divs(t, succ);
-                const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, rng.next1d());
-                const DEmitter em = S.emitters[ei];
-                const float ex = rng.next1d(), ey = rng.next1d();
-                ESample es;
-                const F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
-                const F3 wi_l = to_local(its.sh, neg(d));
-                nee = !is_zero(ems_col);
-                F3 li_ems = f3(0, 0, 0);
-                float pdfems = 0.f, pdfems_mats = 0.f;
-                if (nee) {
-                    const F3 we = to_local(its.sh, es.wi);
-                    const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
-                    const float cs = we.z;
-                    li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
-                                ems_col.z * cs * f.z * n_lights);
-                    pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
-                    pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
-                    so = make_float4(es.so.x, es.so.y, es.so.z, es.smint);
-                    sd = make_float4(es.sd.x, es.sd.y, es.sd.z, es.smaxt);
-                }
-                const float bx = rng.next1d(), by = rng.next1d();
-                F3 wo;
-                int measure;
-                const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
-                const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
-                const F3 nd = to_world(its.sh, wo);
-                // w_ems of this bounce (:103-106): the occluded shadow ray leaves both pdfs 0 (w_ems
-                // keeps its value), the unoccluded one sets it from them; a discrete sample zeroes
-                // it either way (:136-140)
-                const bool discrete = measure == M_DISCRETE;
-                float w_occ = w_ems, w_un = w_ems;
-                if (nee && (pdfems_mats + pdfems) > kEps) w_un = pdfems / (pdfems_mats + pdfems);
-                if (discrete) w_occ = w_un = 0.f;
-                int fl = (discrete ? F_DISCRETE : 0) | (is_zero(bsdf_col) ? F_ZERO_COL : 0);
-                if (nee && discrete) {
-                    // the discrete sample zeroes both weights: a finite term (0 * t) * li_ems adds exactly zero
-                    // occluded or not (Li never holds -0), so no shadow ray is queued (as the megakernel)
-                    const F3 c = mulc(scl(w_un, t), li_ems), z = mulc(scl(w_occ, t), f3(0, 0, 0));
-                    if (c.x == 0.f && c.y == 0.f && c.z == 0.f && z.x == 0.f && z.y == 0.f && z.z == 0.f) {
-                        nee = false;
-                        li_ems = f3(0, 0, 0);  // the unoccluded term is +-0: Li is unchanged either way
-                    }
-                }
-                if (nee) {
-                    // Li += w_ems * t * Li_ems (:142) once the shadow ray is known to be unoccluded
-                    const F3 c = mulc(scl(w_un, t), li_ems);
-                    o.pe = make_float4(c.x, c.y, c.z, w_un);
-                    const F3 z = mulc(scl(w_occ, t), f3(0, 0, 0));
-                    fl |= F_NEE | ((z.x != 0.f || z.y != 0.f || z.z != 0.f) ? F_ZNAN : 0);
-                } else {
-                    li = add(li, mulc(scl(w_occ, t), li_ems));  // li_ems = 0: the same term, added now
-                }
-                w_ems = w_occ;
-                t = mulc(t, bsdf_col);  // :145
-                o.pdfmat = pdfmat;
-                o.ro = make_float4(its.p.x, its.p.y, its.p.z, kEps);
-                o.rd = make_float4(nd.x, nd.y, nd.z, (nd.x == 0 && nd.y == 0 && nd.z == 0) ? -INFINITY : INFINITY);
-                o.flags = fl;
-            }
-        }
+    if (!shade_head(S, tv, v, h, found, ro.w, its)) {
+        write_radiance(L, v);
+        return false;
     }
-    if (alive) {
-        o.li = make_float4(li.x, li.y, li.z, w_mats);
-        o.thr = make_float4(t.x, t.y, t.z, w_ems);
-        o.rng = rng.state;
-        o.pid = pid;
-    } else {
-        float4 *r = &L.rec_rgbx[pid];
-        r->x = li.x;
-        r->y = li.y;
-        r->z = li.z;
-    }
-    return alive;
+    shade_body(S, tv, v, its, o, nee, so, sd);
+    return true;
 }
 
 // One queue entry per thread; survivors are ranked within the workgroup (wave ballots + LDS
@@ -676,6 +736,9 @@ __global__ __launch_bounds__(256, NH_SHADE_WAVES) void wf_shade(const DScene *__
 // runs of one material instead of interleaving the diffuse, mirror, dielectric and microfacet
 // code paths lane by lane (SURVEY.md north star: material-sorted shade queues).
 constexpr int kMatClasses = 5;  // 4 BSDF types + rays that leave the scene
+#ifndef NH_TAIL_WAVES
+#define NH_TAIL_WAVES 1
+#endif
 #ifndef NH_BOUNCE_WAVES
 #define NH_BOUNCE_WAVES 4
 #endif
@@ -787,14 +850,204 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce(const DScene *
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Russian roulette ahead (LDS-staged BVHs, default). A wf_bounce launch loses about a third of its lanes at the
+// roulette of path_mis.cpp:58-71 (C2: 29.4M -> 19.4M paths at the first bounce), and those lanes then idle
+// through the light sample's any-hit and the next closest-hit traversals, most of the launch's work
+// (measured: VALUUtilization 48 %, profiles/round3_c2_pmc_valu_summary.txt). Here a launch ends with the head
+// of the NEXT vertex instead -- its probe MIS weight, emitter term and roulette draw (shade_head: every
+// operand is known once the next ray's closest hit is) -- and stores only the paths that survive it, so the
+// next launch's lanes all carry live paths through body, shadow ray and traversal. The same float operations
+// and random draws in the same order per path; only where the kernel boundary falls moves.
+//
+// Stored state of a live path (WfBuf, as store_state): its vertex's incoming ray (org, d), Li / w_mats,
+// throughput / w_ems after the roulette division, the stream after the roulette draw, path_mats' counter,
+// and the ray's hit; the next launch recomputes the Intersection from the hit (hit_info is a pure function).
+__device__ __forceinline__ void store_post_head(const WfBuf &B, int s, const PathV &v, const Hit &h) {
+    B.ray_o[s] = make_float4(v.org.x, v.org.y, v.org.z, 0.f);
+    B.ray_d[s] = make_float4(v.d.x, v.d.y, v.d.z, __int_as_float((int)(((unsigned)(v.flags & 0x30) << kPidBits) | (unsigned)v.pid)));
+    B.li[s] = make_float4(v.li.x, v.li.y, v.li.z, v.w_mats);
+    B.thr[s] = make_float4(v.t.x, v.t.y, v.t.z, v.w_ems);
+    B.rng[s] = v.rng.state;
+    B.hit[s] = make_float4(h.t, h.u, h.v, __int_as_float(h.k));
+}
+
+__device__ __forceinline__ void load_post_head(const DScene &S, const Traversal &tv, const WfLaunch &L, const WfBuf &B,
+                                               int s, PathV &v, Hit &h, Its &its) {
+    const float4 ro = B.ray_o[s], rd = B.ray_d[s], li4 = B.li[s], th4 = B.thr[s], hv = B.hit[s];
+    v.rng.state = B.rng[s];
+    const int bits = __float_as_int(rd.w);
+    v.flags = (int)((unsigned)bits >> kPidBits);
+    v.pid = bits & ((1 << kPidBits) - 1);
+    v.rng.inc = ((uint64_t)(L.s0 + v.pid / L.n_list) << 1u) | 1u;
+    v.org = xyz(ro);
+    v.d = xyz(rd);
+    v.li = xyz(li4);
+    v.w_mats = li4.w;
+    v.t = xyz(th4);
+    v.w_ems = th4.w;
+    h.t = hv.x;
+    h.u = hv.y;
+    h.v = hv.z;
+    h.k = __float_as_int(hv.w);
+    hit_info(S, tv, h, v.org, v.d, its);
+}
+
+// the camera path of queue entry s at bounce 0, up to its first vertex's head
+template <bool ORDERED, bool STATS>
+__device__ __forceinline__ bool first_vertex(const DScene &S, const Traversal &tv, const WfLaunch &L, int s, PathV &v,
+                                             Hit &h, Its &its, uint32_t *stk, int stride, TravStats &st_e,
+                                             unsigned long long &q_e) {
+    float4 ro, rd;
+    float jx, jy;
+    camera_sample(S, L, s, v.rng, ro, rd, jx, jy);
+    L.rec_rgbx[s] = make_float4(0.f, 0.f, 0.f, jx);
+    L.rec_jy[s] = jy;
+    v.org = xyz(ro);
+    v.d = xyz(rd);
+    v.li = f3(0.f, 0.f, 0.f);
+    v.t = f3(1.f, 1.f, 1.f);
+    v.w_mats = 1.f;
+    v.w_ems = 0.f;
+    v.flags = F_FIRST;
+    v.pid = s;
+    const bool live = rd.w >= ro.w;
+    q_e += live ? 1 : 0;
+    const bool found = live && trace<16, ORDERED, false, STATS, true>(tv, S, v.org, v.d, ro.w, rd.w, h, stk, stride, st_e);
+    if (!shade_head(S, tv, v, h, found, 0.f, its)) {
+        write_radiance(L, v);
+        return false;
+    }
+    return true;
+}
+
+// body of the current vertex, its light sample's any-hit query, the next ray's closest hit, and the next
+// vertex's head; false once the path has ended (its radiance written)
+template <bool ORDERED, bool STATS>
+__device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, const WfLaunch &L, PathV &v, Its &its,
+                                        Hit &h, uint32_t *stk, int stride, TravStats &st_e, TravStats &st_s,
+                                        unsigned long long &q_e, unsigned long long &q_s) {
+    PState o;
+    bool nee = false;
+    float4 so, sd;
+    shade_body(S, tv, v, its, o, nee, so, sd);
+    if (nee) {  // the light sample's any-hit query, its outcome applied as the next shade_path would
+        Hit hs;
+        ++q_s;
+        if (!trace<16, ORDERED, true, STATS, true>(tv, S, xyz(so), xyz(sd), so.w, sd.w, hs, stk, stride, st_s)) {
+            o.li.x = o.li.x + o.pe.x;
+            o.li.y = o.li.y + o.pe.y;
+            o.li.z = o.li.z + o.pe.z;
+            o.thr.w = o.pe.w;
+        } else if (o.flags & F_ZNAN) {
+            o.li.x = o.li.x + NAN;
+            o.li.y = o.li.y + NAN;
+            o.li.z = o.li.z + NAN;
+        }
+        o.flags &= ~(F_NEE | F_ZNAN);
+    }
+    const bool live = o.rd.w >= o.ro.w;
+    q_e += live ? 1 : 0;
+    const bool found = live && trace<16, ORDERED, false, STATS, true>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h,
+                                                                    stk, stride, st_e);
+    v = path_of(L, o);
+    if (!shade_head(S, tv, v, h, found, o.pdfmat, its)) {
+        write_radiance(L, v);
+        return false;
+    }
+    return true;
+}
+
+template <bool ORDERED, bool STATS, bool SORT>
+__global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScene *__restrict__ Sp, Traversal tv_g,
+                                                                     WfLaunch L) {
+    __shared__ uint32_t stk[16 * 256];
+    __shared__ unsigned s_n[kMatClasses], s_off[kMatClasses], s_base;
+    extern __shared__ float4 lds_scene[];
+    const DScene &S = *Sp;
+    const QView qv = queue_view(L.cnt_in);
+    const int base = blockIdx.x * 256;
+    if (base >= qv.n) return;  // whole workgroup
+    if (threadIdx.x < kMatClasses) s_n[threadIdx.x] = 0u;  // visible after the staging barrier
+    const Traversal tv = stage_small_scene<true>(tv_g, L, lds_scene);
+    const int shard = blockIdx.x & (kQueueShards - 1);
+    const int q = base + (int)threadIdx.x;
+    uint32_t *my_stk = stk + threadIdx.x;
+    TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
+    unsigned long long q_e = 0, q_s = 0;
+    bool cont = false;
+    PathV v;
+    Hit h;
+    int cls = kMatClasses - 1;
+    if (q < qv.n) {
+        const int s = queue_slot(qv.pre, L.seg_cap, q);
+        Its its;
+        bool alive = true;
+        if (L.first) alive = first_vertex<ORDERED, STATS>(S, tv, L, s, v, h, its, my_stk, 256, st_e, q_e);
+        else load_post_head(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
+        if (alive) cont = rr_step<ORDERED, STATS>(S, tv, L, v, its, h, my_stk, 256, st_e, st_s, q_e, q_s);
+        if (cont) cls = prim_material(tv.prims[3 * h.k + 2]);  // a live path's ray has hit something
+    }
+    int rank = 0;  // survivors ranked by the material class of their hit (sorted queue) or in lane order
+    if (SORT) {
+#pragma unroll
+        for (int c = 0; c < kMatClasses; ++c) {
+            const int r = wave_append(&s_n[c], cont && cls == c);
+            if (cls == c) rank = r;
+        }
+    } else {
+        cls = 0;
+        rank = wave_append(&s_n[0], cont);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned tot = 0;
+        for (int c = 0; c < kMatClasses; ++c) {
+            s_off[c] = tot;
+            tot += s_n[c];
+        }
+        s_base = tot ? atomicAdd(&L.cnt_out[shard * kCountStride], tot) : 0u;
+    }
+    __syncthreads();
+    if (cont) store_post_head(L.st.buf[1 - L.in_q], shard * L.seg_cap + (int)(s_base + s_off[cls]) + rank, v, h);
+    if (STATS) {
+        flush_trav_stats(stat_shard(L.counters), q_e, st_e);
+        flush_trav_stats(stat_shard(L.counters) + kStatAny, q_s, st_s);
+    }
+}
+
+// the chunk's last paths (RR-ahead state) finished in place, one thread per path, as wf_tail
+template <bool ORDERED, bool STATS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAVES))) void wf_tail_rr(
+    const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
+    __shared__ uint32_t stk[16 * 256];
+    extern __shared__ float4 lds_scene[];
+    const DScene &S = *Sp;
+    const Traversal tv = stage_small_scene<true>(tv_g, L, lds_scene);
+    const QView qv = queue_view(L.cnt_in);
+    const WfBuf &B = L.st.buf[L.in_q];
+    TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
+    unsigned long long q_e = 0, q_s = 0;
+    for (int q = blockIdx.x * 256 + threadIdx.x; q < qv.n; q += gridDim.x * 256) {
+        const int s = queue_slot(qv.pre, L.seg_cap, q);
+        PathV v;
+        Hit h;
+        Its its;
+        load_post_head(S, tv, L, B, s, v, h, its);
+        while (rr_step<ORDERED, STATS>(S, tv, L, v, its, h, stk + threadIdx.x, 256, st_e, st_s, q_e, q_s)) {
+        }
+    }
+    if (STATS) {  // the tail's own counter slots (kStatTail*), so stage rates stay per kernel
+        flush_trav_stats(stat_shard(L.counters) + kStatTail, q_e, st_e);
+        flush_trav_stats(stat_shard(L.counters) + kStatTailAny, q_s, st_s);
+    }
+}
+
 // Tail of a chunk: once few paths are alive, per-bounce launches cost more than the work they
 // carry (three kernels + count traffic for a few thousand paths). wf_tail takes the live queue
 // of a bounce whose extend / any-hit traversals are done and finishes every path in place, one
 // thread per path: shade, then its next closest-hit and shadow traversals, until it terminates --
 // the same operations in the same order as further wavefront bounces.
-#ifndef NH_TAIL_WAVES
-#define NH_TAIL_WAVES 1
-#endif
 template <int DEPTH, bool ORDERED, bool STATS, bool SMALL, bool WIDE>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAVES))) void wf_tail(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
@@ -839,6 +1092,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAV
 
 namespace nh {
 
+int tree_top_nodes() { return kTopNodes; }
 
 // Persistent grids hold exactly the workgroups that are resident at once (occupancy of this
 // instantiation x CUs, at most kPersistentBlocks -- the spill area's size): a workgroup that
@@ -944,6 +1198,32 @@ void launch_wf_bounce(const DScene *S, const Traversal &tv, const WfLaunch &L, b
         else { if (sort) NH_FB(false, false, true); else NH_FB(false, false, false); }
     }
 #undef NH_FB
+}
+
+void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
+                         int bound, hipStream_t st) {
+    int blocks = std::max(1, (bound + 255) / 256);
+    blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
+    const size_t lds = 16 * ((size_t)small_pairs_offset_f4(L) + (size_t)kPairF4 * (L.small_prims / 3));
+#define NH_FB(O, T, SO) hipLaunchKernelGGL((wf_bounce_rr<O, T, SO>), dim3(blocks), dim3(256), lds, st, S, tv, L)
+    if (ordered) {
+        if (stats) { if (sort) NH_FB(true, true, true); else NH_FB(true, true, false); }
+        else { if (sort) NH_FB(true, false, true); else NH_FB(true, false, false); }
+    } else {
+        if (stats) { if (sort) NH_FB(false, true, true); else NH_FB(false, true, false); }
+        else { if (sort) NH_FB(false, false, true); else NH_FB(false, false, false); }
+    }
+#undef NH_FB
+}
+
+void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
+                       hipStream_t st) {
+    const dim3 grid(std::min(std::max(1, (bound + 255) / 256), kTraceBlocksMax));
+    const size_t lds = 16 * ((size_t)small_pairs_offset_f4(L) + (size_t)kPairF4 * (L.small_prims / 3));
+#define NH_TR(O, T) hipLaunchKernelGGL((wf_tail_rr<O, T>), grid, dim3(256), lds, st, S, tv, L)
+    if (ordered) { if (stats) NH_TR(true, true); else NH_TR(true, false); }
+    else { if (stats) NH_TR(false, true); else NH_TR(false, false); }
+#undef NH_TR
 }
 
 void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, int bound, hipStream_t st) {
