@@ -161,13 +161,15 @@ def roofline(args, calib, st, W, H, R):
     divided by the kernel's average launch duration (HIP events on the stream it runs on):
       wf_shade     path-state bytes loaded + stored (counted by construction from the queue counts)
       wf_extend /  BVH nodes x node bytes + primitive tests x 48 B (in-kernel counters) + queue bytes
-      wf_shadow    (ray in, hit / occlusion out). Node and primitive reads are HBM traffic only when the
-                   BVH is read from global memory; a BVH staged in LDS (the Cornell box, < 1 KB) makes
-                   them LDS reads, so `hbm_gbs` counts the queue bytes alone and `work_gbs` the
-                   algorithmic traversal rate (not an HBM figure)
+      wf_shadow    (ray in, hit / occlusion out). Node and primitive reads go to global memory only when
+                   the BVH is not staged in LDS; a BVH staged in LDS (the Cornell box, < 1 KB) makes them
+                   LDS reads, so `global_gbs` counts the queue bytes alone and `lds_work_gbs` the
+                   algorithmic traversal bytes read from LDS (never compared with the HBM peak)
       wf_tail      traversal + shade work of the last few paths, in place
       megakernel   nodes x 64 + prims x 48 + 20 B record per path
-    `peak` is the HBM roofline; only `hbm_gbs` figures are compared with it."""
+    These are algorithmic byte counts; the HBM bytes actually moved come from rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes (profiles/pmc_traffic.json) as `traffic` / `traffic_gbs`. `peak` is the
+    HBM roofline; `global_gbs` (algorithmic) and `traffic_gbs` (measured) are compared with it."""
     paths = calib["samples"]
     node_b = calib.get("node_bytes") or 64
     lds = bool(calib.get("lds_scene"))
@@ -205,47 +207,83 @@ def roofline(args, calib, st, W, H, R):
         if ms <= 0 or launches == 0:
             continue
         avg = ms / launches
+        # global_*: algorithmic bytes the kernel moves through global memory (path state / queues, and the
+        # BVH nodes and primitive records unless the BVH is staged in LDS), from counters and queue sizes --
+        # not a measurement of HBM traffic (that is roofline.traffic, from PMC counters)
         r = {"ms": round(ms, 3), "launches": launches, "avg_launch_ms": round(avg, 4),
-             "hbm_bytes_per_launch": int(per_launch(v["hbm_bytes"], launches)),
-             "hbm_gbs": round(per_launch(v["hbm_bytes"], launches) / (avg * 1e-3) / 1e9, 1)}
+             "global_bytes_per_launch": int(per_launch(v["hbm_bytes"], launches)),
+             "global_gbs": round(per_launch(v["hbm_bytes"], launches) / (avg * 1e-3) / 1e9, 1)}
         if v["work_bytes"] != v["hbm_bytes"]:
-            r["work_gbs"] = round(per_launch(v["work_bytes"], launches) / (avg * 1e-3) / 1e9, 1)
-            r["work_note"] = ("algorithmic node/primitive bytes read from the LDS copy of the BVH: not HBM traffic"
-                              if lds else "algorithmic bytes")
+            r["lds_work_gbs"] = round(per_launch(v["work_bytes"] - v["hbm_bytes"], launches) / (avg * 1e-3) / 1e9, 1)
+            r["lds_work_note"] = "algorithmic node/primitive bytes read from the LDS copy of the BVH (not global memory)"
         if "queries" in v and v["queries"]:
             r["nodes_per_query"] = round(v["nodes"] / v["queries"], 3)
             r["prims_per_query"] = round(v["prims"] / v["queries"], 3)
-        if r["hbm_gbs"] > HBM_PEAK_GBS * 1.02:  # an HBM figure above peak is an accounting bug: say so
-            r["accounting_error"] = "HBM GB/s above the HBM peak"
+        if r["global_gbs"] > HBM_PEAK_GBS * 1.02:  # a global-memory rate above the HBM peak is an accounting bug
+            r["accounting_error"] = "global-memory GB/s above the HBM peak"
+        srec = pmc_record(f"{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}/{k}") \
+            if int(os.environ.get("WORLD_SIZE", "1")) == 1 else {}
+        if srec.get("hbm_bytes_per_launch"):  # measured HBM bytes of this stage's kernel (committed PMC passes)
+            r["measured_hbm_bytes_per_launch"] = srec["hbm_bytes_per_launch"]
+            r["measured_hbm_gbs"] = round(srec["hbm_bytes_per_launch"] / (avg * 1e-3) / 1e9, 1)
+            r["measured_source"] = f"profiles/pmc_traffic.json[{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}/{k}]"
         report[k] = r
     dom = max(report, key=lambda k: report[k]["ms"])
-    kernel = {"shade": "wf_shade", "extend": "wf_extend", "shadow": "wf_shadow", "tail": "wf_tail",
-              "path": "nh_path_kernel", "bounce": "wf_bounce (shade + any-hit + closest-hit, fused)"}[dom]
+    wide = node_b == 128  # deep trees: the persistent 4-wide traversal kernel runs both queries
+    rr = os.environ.get("NH_RR_AHEAD", "1") != "0"
+    kernel = {"shade": "wf_shade",
+              "extend": "wf_trace_pt (persistent 4-wide closest hit)" if wide else "wf_extend",
+              "shadow": "wf_trace_pt (persistent 4-wide any hit)" if wide else "wf_shadow",
+              "tail": "wf_tail_rr" if fused and rr else "wf_tail", "path": "nh_path_kernel",
+              "bounce": ("wf_bounce_rr (shade body + any-hit + closest-hit + the next vertex's roulette, fused)" if rr
+                         else "wf_bounce (shade + any-hit + closest-hit, fused)")}[dom]
     d = report[dom]
-    key = f"{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}"
+    key = f"{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}/{dom}"
     single = int(os.environ.get("WORLD_SIZE", "1")) == 1
-    traffic, source = pmc_traffic(key) if single else (None, None)
-    achieved = d["hbm_gbs"]
+    rec = pmc_record(key) if single else {}
+    if rec and rec.get("kernel", "").split("<")[0] != kernel.split(" ")[0]:
+        rec = {}  # the committed counters are for another kernel of this workload
+    traffic = rec.get("hbm_bytes_per_launch")
+    achieved = d["global_gbs"]
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "traffic_source": source or "not collected for this workload (rocprofv3 PMC runs separately)",
+            "traffic_source": (f"profiles/pmc_traffic.json[{key}]: {rec.get('source', '')}" if traffic else
+                               "not collected for this workload (rocprofv3 PMC runs separately)"),
             "kernel": kernel, "avg_launch_ms": d["avg_launch_ms"], "launches": d["launches"],
-            "algorithmic_bytes_per_launch": d["hbm_bytes_per_launch"],
+            "algorithmic_bytes_per_launch": d["global_bytes_per_launch"],
             "bytes_per_sample": round(stages[dom]["hbm_bytes"] / paths, 1), "node_bytes": node_b,
             "lds_scene": lds, "queries_per_sample": round(calib["ray_queries"] / paths, 3),
             "splat_ms_per_launch": round(st["kernel_ms_splat"] / max(st["launches_splat"], 1), 4),
             "stages": report}
-    rec = pmc_record(key) if single else {}
-    if rec.get("valu_issue_frac") is not None and rec.get("kernel", "").split("<")[0] in kernel:
-        # what bounds the kernel, from the same committed PMC passes: VALU issue slots used (one wave64
-        # VALU instruction per CU per cycle) and the share of wave-cycles spent waiting
-        roof["limiter"] = {"valu_issue_frac": rec["valu_issue_frac"], "wait_frac": rec.get("wait_frac"),
-                           "valu_insts_per_launch": rec.get("valu_insts_per_launch"),
-                           "note": ("VALU-issue bound (the LDS-resident traversal and shading arithmetic), not HBM: "
-                                    "its HBM bytes are the path state only" if rec["valu_issue_frac"] > 0.6 else
-                                    "latency bound (waves waiting on dependent loads)"),
-                           "source": traffic_source_of(key)}
+    if traffic:
+        # measured HBM bytes per launch (PMC, separate passes) over this run's launch time
+        roof["traffic_gbs"] = round(traffic / (d["avg_launch_ms"] * 1e-3) / 1e9, 1)
+        roof["traffic_frac"] = round(roof["traffic_gbs"] / HBM_PEAK_GBS, 4)
+    if rec.get("valu_issue_frac") is not None:
+        roof["limiter"] = limiter_record(rec, key)
     return roof
+
+
+def limiter_record(rec, key):
+    """What bounds the kernel, from the committed PMC passes of the same command: the share of the CUs'
+    VALU issue slots used (SQ_INSTS_VALU / (256 CUs x kernel cycles): a wave64 VALU instruction occupies its
+    SIMD for one quad-cycle -- SQ_ACTIVE_INST_VALU ~ SQ_INSTS_VALU in quad-cycles -- so the 4 SIMDs of a CU
+    issue at most one per cycle together), rocprofv3's VALUBusy and VALUUtilization (active lanes per VALU
+    instruction: divergence), and the share of wave-cycles spent waiting (SQ_WAIT_ANY / SQ_WAVE_CYCLES)."""
+    out = {"valu_issue_frac": rec["valu_issue_frac"], "valu_busy_pct": rec.get("valu_busy_pct"),
+           "valu_utilization_pct": rec.get("valu_utilization_pct"), "wait_frac": rec.get("wait_frac"),
+           "valu_insts_per_launch": rec.get("valu_insts_per_launch"),
+           "quad_cycles_per_valu_inst": rec.get("quad_cycles_per_valu_inst"), "source": traffic_source_of(key)}
+    util = rec.get("valu_utilization_pct")
+    if util is not None and util < 60:
+        out["note"] = (f"divergence-bound: only {util:.0f} % of the lanes are active per VALU instruction, with "
+                       f"{rec['valu_issue_frac']:.2f} of the issue slots used and waves waiting "
+                       f"{rec.get('wait_frac', 0):.2f} of their cycles -- neither HBM- nor issue-bound")
+    elif rec["valu_issue_frac"] > 0.6:
+        out["note"] = "VALU-issue bound: its HBM bytes are the path state only"
+    else:
+        out["note"] = "latency bound (waves waiting on dependent loads)"
+    return out
 
 
 def traffic_source_of(key):
@@ -254,19 +292,26 @@ def traffic_source_of(key):
 
 def traversal_record(roof):
     """The metric's "traversal HBM GB/s": the closest-hit traversal kernel of the timed run (the fused
-    bounce kernel when the BVH is traversed inside it)."""
+    bounce kernel when the BVH is traversed inside it): its algorithmic global-memory rate, and for an
+    LDS-staged BVH the algorithmic traversal bytes it read from LDS; measured HBM bytes are roofline.traffic."""
     name = next((k for k in ("extend", "bounce", "path") if k in roof["stages"]), None)
     if name is None:
         return None
     e = roof["stages"][name]
     out = {"kernel": {"extend": "wf_extend", "bounce": "wf_bounce", "path": "nh_path_kernel"}[name],
-           "hbm_gbs": e["hbm_gbs"], "frac_of_hbm_peak": round(e["hbm_gbs"] / HBM_PEAK_GBS, 4),
+           "global_gbs": e["global_gbs"], "frac_of_hbm_peak": round(e["global_gbs"] / HBM_PEAK_GBS, 4),
            "avg_launch_ms": e["avg_launch_ms"]}
-    if "work_gbs" in e:
-        out["work_gbs"] = e["work_gbs"]
-        out["note"] = ("BVH staged in LDS: hbm_gbs is the HBM stream of that kernel (ray/hit queues, or the path state "
-                       "of the fused bounce kernel); work_gbs adds the algorithmic traversal bytes read from LDS")
+    if "lds_work_gbs" in e:
+        out["lds_work_gbs"] = e["lds_work_gbs"]
+        out["note"] = ("BVH staged in LDS: global_gbs is the kernel's global-memory stream (ray/hit queues, or the "
+                       "path state of the fused bounce kernel); lds_work_gbs the traversal bytes read from LDS")
+    if name == roof_dominant(roof) and roof.get("traffic_gbs"):
+        out["measured_hbm_gbs"] = roof["traffic_gbs"]
     return out
+
+
+def roof_dominant(roof):
+    return max(roof["stages"], key=lambda k: roof["stages"][k]["ms"])
 
 
 def cpu_cores():
@@ -449,15 +494,20 @@ def traversal_1m(nh, args, local):
     r = run_workload(nh, a, "bumpy1m", args.traversal_1m_steps, 1, local)
     roof = r["roof"]
     e = roof["stages"]["extend"]
-    traffic, source = pmc_traffic(f"bumpy1m_{r['W']}x{r['H']}_r{r['R']}_{args.traversal}_{args.mode}")
+    key1m = f"bumpy1m_{r['W']}x{r['H']}_r{r['R']}_{args.traversal}_{args.mode}/extend"
+    traffic, source = pmc_traffic(key1m)
+    rec1m = pmc_record(key1m)
     out = {"workload": r["desc"], "msamples_s": round(r["samples"] / r["elapsed"] / 1e6, 3),
            "kernel": "wf_trace_pt (persistent 4-wide closest-hit traversal)" if roof["node_bytes"] == 128 else "wf_extend",
-           "avg_launch_ms": e["avg_launch_ms"], "algorithmic_bytes_per_launch": e["hbm_bytes_per_launch"],
-           "achieved_gbs": e["hbm_gbs"], "frac": round(e["hbm_gbs"] / HBM_PEAK_GBS, 4), "target_frac": 0.40,
+           "avg_launch_ms": e["avg_launch_ms"], "algorithmic_bytes_per_launch": e["global_bytes_per_launch"],
+           "achieved_gbs": e["global_gbs"], "frac": round(e["global_gbs"] / HBM_PEAK_GBS, 4), "target_frac": 0.40,
            "nodes_per_query": e.get("nodes_per_query"), "prims_per_query": e.get("prims_per_query"),
            "node_bytes": roof["node_bytes"],
            "bytes": "algorithmic: nodes x node_bytes + primitive tests x 48 B + 48 B ray/hit per query",
            "traffic": traffic, "traffic_source": source or "not collected for this workload",
+           "traffic_gbs": round(traffic / (e["avg_launch_ms"] * 1e-3) / 1e9, 1) if traffic else None,
+           "l2_hit_rate": rec1m.get("l2_hit_rate"),
+           "limiter": limiter_record(rec1m, key1m) if rec1m.get("valu_issue_frac") is not None else None,
            "note": "the ~176 MB tree is resident in the 256 MB MALL: measured HBM traffic (traffic) is well below "
                    "the algorithmic bytes; this kernel is bound by dependent-load latency",
            "steps": args.traversal_1m_steps, "spp": r["R"] * args.traversal_1m_steps, "timed": roof["timed"]}
