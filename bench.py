@@ -549,6 +549,10 @@ def launcher_selftest(args):
 
 def main():
     args = parse()
+    # one hardware queue per path-pool stream (nori_hip.py raises it the same way; done here too, before torch
+    # may initialise the HIP runtime in a multi-rank run): at least 8 per process
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -74,6 +74,7 @@ struct WfPool {
     bool persistent = false, wide = false, tail = false, draining = false;
     bool fused = false, sorted = false;  // one wf_bounce kernel per bounce (LDS-staged BVH); material-sorted queue
     bool rr = false;                     // fused kernels with the next vertex's Russian roulette ahead (wf_bounce_rr)
+    bool shade_sorted = false;           // wf_shade entries in BSDF-type order (deep BVHs, mixed materials)
     int64_t tail_at = 0, drain_at = 0;
     int it = 0;
     std::vector<uint64_t> in_e, in_s;  // live paths / shadow rays entering each bounce
@@ -129,6 +130,7 @@ struct nh_ctx {
     std::vector<uint32_t> bvh_indices, shape_offset;
     std::vector<int> shape_bsdf_type;  // BSDF type of each shape (material key of the sorted queues)
     int n_bsdf_types = 0;              // distinct BSDF types in the scene
+    bool specular = false;             // a mirror or dielectric BSDF: long discrete chains, long chunk tails
     float *fb = nullptr;
     size_t fb_floats = 0;
     float4 *rec = nullptr;
@@ -399,6 +401,7 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         types |= 1u << t;
     }
     c->n_bsdf_types = __builtin_popcount(types);
+    c->specular = (types & ((1u << NH_BSDF_MIRROR) | (1u << NH_BSDF_DIELECTRIC))) != 0;
     c->V.assign(d->V, d->V + 3 * nv);
     c->F.assign(d->F, d->F + 3 * (size_t)d->n_faces);
     c->width = d->camera.width;
@@ -853,10 +856,16 @@ static SplatLaunch make_splat(const nh_ctx *c, const float4 *rec, const float *r
 
 static size_t block_px(const nh_ctx *c) { return (size_t)(32 + 2 * c->border) * (32 + 2 * c->border); }
 
-// path pools driven by pipeline_run (NH_POOLS: 1 = no overlap, for A/B and tests)
-static int active_pools() {
+// path pools driven by pipeline_run (NH_POOLS: 1 = no overlap, for A/B and tests). Scenes with mirror or
+// dielectric BSDFs get a third pool: their chunks end in tails of discrete chains that survive Russian roulette
+// with probability 0.99 per bounce (path_mis.cpp:58-70), 5-6 ms whatever the chunk size, longer than a C1
+// chunk's bounce phase; with three pools two tails overlap the next chunk (C1 2744 -> 3321 Msamples/s; C2,
+// perf-1M and C5 unchanged). Each pool's stream needs its own hardware queue (GPU_MAX_HW_QUEUES >= 5; with HIP's
+// default of 4, two pool streams share one and a tail blocks the other pool's bounces).
+static int active_pools(const nh_ctx *c) {
     const char *np = std::getenv("NH_POOLS");
-    return std::max(1, std::min(kPools, np ? std::atoi(np) : NH_DEFAULT_POOLS));
+    const int def = c->specular ? NH_DEFAULT_POOLS + 1 : NH_DEFAULT_POOLS;
+    return std::max(1, std::min(kPools, np ? std::atoi(np) : def));
 }
 
 // start job j on idle pool p: buffers, traversal choice, initial queue (all n_paths camera paths)
@@ -866,7 +875,7 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     if (rc) return rc;
     // the other pools in use get the same capacity now (idle ones only: nothing of theirs is in
     // flight), so the first render call, not a later one, pays for their allocation
-    for (int i = 0; i < active_pools(); ++i) {
+    for (int i = 0; i < active_pools(c); ++i) {
         WfPool &o = c->pools[i];
         if (&o == &p || o.state != WfPool::IDLE) continue;
         if ((rc = pool_alloc(c, o, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c)))) return rc;
@@ -920,6 +929,10 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     p.sorted = p.fused && c->n_bsdf_types > 1;
     p.rr = p.fused;
     if (const char *e = std::getenv("NH_RR_AHEAD")) p.rr = p.fused && e[0] != '0';
+    // material-sorted shading on deep BVHs is measured slower (C3 1640 -> 1590, C5 1542 -> 1526 Msamples/s:
+    // the extra hit read and barriers cost more than the divergence saved): off unless NH_SORT_SHADE=1
+    p.shade_sorted = false;
+    if (const char *e = std::getenv("NH_SORT_SHADE")) p.shade_sorted = !p.fused && e[0] == '1';
     if (const char *e = std::getenv("NH_SORT")) p.sorted = p.fused && e[0] == '1';
     c->stats.fused_bounce = p.fused ? 1 : 0;
     c->stats.node_bytes = p.wide ? 16 * nhd::kWideF4 : 64;
@@ -1012,7 +1025,7 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
         p.state = WfPool::SPLAT;
         return NH_OK;
     }
-    nh::launch_wf_shade(c->d_scene, c->tv, L, bound, p.stream);
+    nh::launch_wf_shade(c->d_scene, c->tv, L, p.shade_sorted, bound, p.stream);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(ev[3], p.stream));
     unsigned *h = p.h_counts + (size_t)(it % kRing) * 2 * kCountGroup;
@@ -1187,7 +1200,7 @@ static void pipeline_reset(nh_ctx *c) {
 // Drive the pools. all = run until every chunk has finished; otherwise return once every
 // submitted chunk has started and every busy pool is draining.
 static int pipeline_run(nh_ctx *c, bool all) {
-    const int n_pools = active_pools();
+    const int n_pools = active_pools(c);
     for (;;) {
         bool progress = false;
         hipError_t ev_err = hipSuccess;
@@ -1343,7 +1356,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
             size_t held = 0;
             for (const WfPool &p : c->pools) held += p.cap * (kWfBytesPerPath + 20) + p.staging_cap * sizeof(float4);
-            const size_t avail = (size_t)((double)(free_b + held) * 0.85) / (size_t)active_pools();
+            const size_t avail = (size_t)((double)(free_b + held) * 0.85) / (size_t)active_pools(c);
             budget = std::min(budget, std::max(avail, per_round_bytes));
         }
     }

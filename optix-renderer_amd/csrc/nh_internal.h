@@ -144,7 +144,9 @@ constexpr size_t kSmallSceneBytes = 16384;
 namespace nh {
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                      bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st);
-void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, int bound, hipStream_t st);
+// sort: entries shaded in the order of their hit's BSDF type within each workgroup (material-sorted shading)
+void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool sort, int bound,
+                     hipStream_t st);
 // fused shade + any-hit + closest-hit bounce for LDS-staged BVHs; sort = material-sorted output queue
 void launch_wf_bounce(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                       bool sort, int bound, hipStream_t st);

@@ -678,11 +678,20 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
 // One queue entry per thread; survivors are ranked within the workgroup (wave ballots + LDS
 // atomics), the workgroup reserves its ranges of the next buffer and the shadow queue with one
 // device-scope atomic each, then every thread stores its state at its final slot.
+//
+// SORT (material-sorted shading, scenes mixing BSDF types on deep BVHs): the workgroup first reads its
+// 256 entries' hits, ranks them by the BSDF type of the hit primitive (kPrimMatShift bits of its record;
+// misses last) and thread t then shades the t-th entry of that order, so each wave runs mostly one BSDF's
+// code (microfacet's Beckmann sampling and evaluation, or diffuse) instead of interleaving them lane by lane.
+// Only which thread shades which entry changes; every path's operations are the same.
 #ifndef NH_SHADE_WAVES
 #define NH_SHADE_WAVES 4
 #endif
+template <bool SORT>
 __global__ __launch_bounds__(256, NH_SHADE_WAVES) void wf_shade(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ unsigned s_n[2], s_base[2];
+    __shared__ unsigned s_cls[SORT ? 6 : 1];
+    __shared__ short s_perm[SORT ? 256 : 1];
     const DScene &S = *Sp;
     const QView qv = queue_view(L.cnt_in);
     // one 256-entry chunk per workgroup: the grid covers the host's upper bound of qv.n
@@ -692,13 +701,35 @@ __global__ __launch_bounds__(256, NH_SHADE_WAVES) void wf_shade(const DScene *__
     // at most seg_cap entries (nh_api.hip sizes seg_cap so)
     const int shard = blockIdx.x & (kQueueShards - 1);
     if (threadIdx.x < 2) s_n[threadIdx.x] = 0u;
-    __syncthreads();
-    const int q = base + (int)threadIdx.x;
+    const WfBuf &B = L.st.buf[L.in_q];
+    int q = base + (int)threadIdx.x;
+    if constexpr (SORT) {
+        if (threadIdx.x < 6) s_cls[threadIdx.x] = 0u;
+        __syncthreads();
+        int cls = 5;  // past the queue's end: last
+        if (q < qv.n) {
+            const int k = __float_as_int(B.hit[queue_slot(qv.pre, L.seg_cap, q)].w);
+            cls = k >= 0 ? prim_material(tv.prims[3 * k + 2]) : 4;
+        }
+        int rank = 0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            const int r = wave_append(&s_cls[c], cls == c);
+            if (cls == c) rank = r;
+        }
+        __syncthreads();
+        unsigned off = 0;
+        for (int c = 0; c < cls; ++c) off += s_cls[c];
+        s_perm[off + rank] = (short)threadIdx.x;
+        __syncthreads();
+        q = base + (int)s_perm[threadIdx.x];
+    } else {
+        __syncthreads();
+    }
     bool cont = false, nee = false;
     PState o;
     float4 so, sd;
     if (q < qv.n) {
-        const WfBuf &B = L.st.buf[L.in_q];
         const int s = queue_slot(qv.pre, L.seg_cap, q);
         cont = shade_path(S, tv, L, MemState{B, s}, s, B.hit[s], o, nee, so, sd);
     }
@@ -1226,11 +1257,12 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
 #undef NH_TR
 }
 
-void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, int bound, hipStream_t st) {
+void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, bool sort, int bound, hipStream_t st) {
     // one 256-entry chunk per workgroup up to the bound; a multiple of kQueueShards (see wf_shade)
     int blocks = std::max(1, (bound + 255) / 256);
     blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
-    hipLaunchKernelGGL(wf_shade, dim3(blocks), dim3(256), 0, st, S, tv, L);
+    if (sort) hipLaunchKernelGGL(wf_shade<true>, dim3(blocks), dim3(256), 0, st, S, tv, L);
+    else hipLaunchKernelGGL(wf_shade<false>, dim3(blocks), dim3(256), 0, st, S, tv, L);
 }
 
 }  // namespace nh

@@ -21,6 +21,20 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NH_LIB_PATH: an alternative in-tree build, for A/B measurements in one GPU session
 LIB_PATH = os.environ.get("NH_LIB_PATH") or os.path.join(_HERE, "lib", "libnori_hip.so")
 
+# The wavefront pipeline drives up to three path pools on their own streams; each needs its own hardware
+# queue, or one pool's long tail kernel blocks another's bounces (HIP's default is 4 queues per process, one
+# of which the context's own stream takes). Read once by the HIP runtime when it initialises.
+def _raise_hw_queues(n=8):
+    try:
+        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+    except ValueError:
+        cur = 0
+    if cur < n:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(n)
+
+
+_raise_hw_queues()
+
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"nori_hip: HIP library not built ({LIB_PATH}); run `make` or __graft_entry__.build()")
 _lib = C.CDLL(LIB_PATH)
