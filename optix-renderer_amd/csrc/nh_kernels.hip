@@ -471,7 +471,10 @@ __global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
     if (threadIdx.x < 33) s_tab[threadIdx.x] = P.table[threadIdx.x];
     const size_t rbase = (size_t)k * P.n_list;
     for (int i = threadIdx.x; i < 1024; i += 256) {
-        const int lx = i >> 5, ly = i & 31;  // sample index i = lx*32 + ly: x-major order
+        // thread i loads pixel (lx, ly) = (i % 32, i / 32): neighbouring lanes read neighbouring pixels of a
+        // block row, i.e. consecutive list entries (the pixel list is row-major inside a block), so each
+        // wave's record loads are 16-B-per-lane contiguous runs; the LDS layout below is x-major
+        const int lx = i & 31, ly = i >> 5;
         int box = 0xff;                      // x0 = 255 > x1 = 0: empty
         float vx = 0.f, vy = 0.f, vz = 0.f, px = 0.f, py = 0.f;
         if (lx < sxb && ly < syb) {
