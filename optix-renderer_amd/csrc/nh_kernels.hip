@@ -454,28 +454,27 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
 // gives each block-array pixel the ordered sum of its contributions, in the reference's
 // getSampleIndices order (x outer, y inner), starting from the cleared block (0).
 constexpr int kSplatMaxCols = 40;  // 32 + 2*border, border <= 4
-__global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
-    // sample (lx, ly) lives at lx*33 + ly: neighbouring lanes step lx, the odd stride keeps
-    // them on distinct LDS banks
-    __shared__ float s_val[3][32 * 33];
-    __shared__ float s_pos[2][32 * 33];
-    __shared__ int s_box[32 * 33];  // x0 | x1<<8 | y0<<16 | y1<<24 (block-array coords), x1 < x0: empty
-    __shared__ float s_tab[33];
-    const int slot = blockIdx.x, k = blockIdx.y;
-    const int bid = P.blocks[slot];
-    const int by = bid / P.nbx, bx = bid - by * P.nbx;
-    const int ox = bx * 32, oy = by * 32;
-    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    const int cols = 32 + 2 * P.border;
+constexpr int kStripRows = 6;      // block-array rows one thread sums in the strip variant
+
+// phase 1 of the block splat: every sample's footprint (block-array box), filter position and value into LDS
+// (sample (lx, ly) at lx*33 + ly: x-major, the odd stride keeps neighbouring lx on distinct banks)
+struct SplatLds {
+    float val[3][32 * 33];
+    float pos[2][32 * 33];
+    int box[32 * 33];  // x0 | x1<<8 | y0<<16 | y1<<24 (block-array coords), x1 < x0: empty
+    float tab[33];
+};
+__device__ __forceinline__ void splat_stage(const SplatLaunch &P, SplatLds &L, int ox, int oy, int sxb, int syb, int k,
+                                            int cols) {
     const float r = P.radius;
-    if (threadIdx.x < 33) s_tab[threadIdx.x] = P.table[threadIdx.x];
+    if (threadIdx.x < 33) L.tab[threadIdx.x] = P.table[threadIdx.x];
     const size_t rbase = (size_t)k * P.n_list;
     for (int i = threadIdx.x; i < 1024; i += 256) {
         // thread i loads pixel (lx, ly) = (i % 32, i / 32): neighbouring lanes read neighbouring pixels of a
         // block row, i.e. consecutive list entries (the pixel list is row-major inside a block), so each
-        // wave's record loads are 16-B-per-lane contiguous runs; the LDS layout below is x-major
+        // wave's record loads are 16-B-per-lane contiguous runs; the LDS layout is x-major
         const int lx = i & 31, ly = i >> 5;
-        int box = 0xff;                      // x0 = 255 > x1 = 0: empty
+        int box = 0xff;  // x0 = 255 > x1 = 0: empty
         float vx = 0.f, vy = 0.f, vz = 0.f, px = 0.f, py = 0.f;
         if (lx < sxb && ly < syb) {
             const int li = P.pixel_map[(oy + ly) * P.width + (ox + lx)];
@@ -493,11 +492,22 @@ __global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
             }
         }
         const int j = lx * 33 + ly;
-        s_val[0][j] = vx; s_val[1][j] = vy; s_val[2][j] = vz;
-        s_pos[0][j] = px; s_pos[1][j] = py;
-        s_box[j] = box;
+        L.val[0][j] = vx; L.val[1][j] = vy; L.val[2][j] = vz;
+        L.pos[0][j] = px; L.pos[1][j] = py;
+        L.box[j] = box;
     }
     __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
+    __shared__ SplatLds L;
+    const int slot = blockIdx.x, k = blockIdx.y;
+    const int bid = P.blocks[slot];
+    const int by = bid / P.nbx, bx = bid - by * P.nbx;
+    const int ox = bx * 32, oy = by * 32;
+    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+    const int cols = 32 + 2 * P.border;
+    splat_stage(P, L, ox, oy, sxb, syb, k, cols);
     float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
     const int R = P.reach, bd = P.border;
     for (int q = threadIdx.x; q < cols * cols; q += 256) {
@@ -508,17 +518,71 @@ __global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
         for (int lx = lx0; lx <= lx1; ++lx)
             for (int ly = ly0; ly <= ly1; ++ly) {
                 const int i = lx * 33 + ly;
-                const int box = s_box[i];
+                const int box = L.box[i];
                 const int x0 = box & 0xff, x1 = (box >> 8) & 0xff, y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
                 if (xt < x0 || xt > x1 || yt < y0 || yt > y1) continue;
-                const float wx = s_tab[(int)(fabsf((float)xt - s_pos[0][i]) * P.lookup)];
-                const float wy = s_tab[(int)(fabsf((float)yt - s_pos[1][i]) * P.lookup)];
-                ar += s_val[0][i] * wx * wy;
-                ag += s_val[1][i] * wx * wy;
-                ab += s_val[2][i] * wx * wy;
+                const float wx = L.tab[(int)(fabsf((float)xt - L.pos[0][i]) * P.lookup)];
+                const float wy = L.tab[(int)(fabsf((float)yt - L.pos[1][i]) * P.lookup)];
+                ar += L.val[0][i] * wx * wy;
+                ag += L.val[1][i] * wx * wy;
+                ab += L.val[2][i] * wx * wy;
                 aw += 1.0f * wx * wy;
             }
         out[q] = make_float4(ar, ag, ab, aw);
+    }
+}
+
+// The same block splat with each thread summing a strip of kStripRows block-array pixels of one column: a
+// candidate sample's record, x test and column weight are read / computed once for the strip, and its products
+// (v * wx) once as packed-FP32 pairs; each pixel of the strip then takes its row test, row weight and
+// ((v * wx) * wy) products. Every pixel still sums its samples' contributions in getSampleIndices order (the
+// strip walks samples x-major), so the floats are those of nh_block_splat_kernel.
+typedef float sf2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void nh_block_splat_strip_kernel(SplatLaunch P) {
+    __shared__ SplatLds L;
+    const int slot = blockIdx.x, k = blockIdx.y;
+    const int bid = P.blocks[slot];
+    const int by = bid / P.nbx, bx = bid - by * P.nbx;
+    const int ox = bx * 32, oy = by * 32;
+    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+    const int cols = 32 + 2 * P.border;
+    splat_stage(P, L, ox, oy, sxb, syb, k, cols);
+    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+    const int R = P.reach, bd = P.border;
+    const int n_strips = (cols + kStripRows - 1) / kStripRows;
+    for (int t = threadIdx.x; t < cols * n_strips; t += 256) {
+        const int xt = t % cols, yt0 = (t / cols) * kStripRows;
+        sf2 rg[kStripRows], bw[kStripRows];
+#pragma unroll
+        for (int j = 0; j < kStripRows; ++j) {
+            rg[j] = sf2{0.f, 0.f};
+            bw[j] = sf2{0.f, 0.f};
+        }
+        const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
+        const int ly0 = max(yt0 - bd - R, 0), ly1 = min(yt0 + kStripRows - 1 - bd + R, syb - 1);
+        const float fxt = (float)xt;
+        for (int lx = lx0; lx <= lx1; ++lx)
+            for (int ly = ly0; ly <= ly1; ++ly) {
+                const int i = lx * 33 + ly;
+                const int box = L.box[i];
+                const int x0 = box & 0xff, x1 = (box >> 8) & 0xff;
+                if (xt < x0 || xt > x1) continue;
+                const int y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
+                const float wx = L.tab[(int)(fabsf(fxt - L.pos[0][i]) * P.lookup)];
+                const float py = L.pos[1][i];
+                const sf2 vrg = sf2{L.val[0][i], L.val[1][i]} * wx, vbw = sf2{L.val[2][i], 1.0f} * wx;
+#pragma unroll
+                for (int j = 0; j < kStripRows; ++j) {
+                    const int yt = yt0 + j;
+                    if (yt < y0 || yt > y1) continue;
+                    const float wy = L.tab[(int)(fabsf((float)yt - py) * P.lookup)];
+                    rg[j] += vrg * wy;
+                    bw[j] += vbw * wy;
+                }
+            }
+#pragma unroll
+        for (int j = 0; j < kStripRows; ++j)
+            if (yt0 + j < cols) out[(yt0 + j) * cols + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
     }
 }
 
@@ -685,7 +749,12 @@ void launch_path(const DScene *S, const Traversal &tv, const PathLaunch &L, bool
 }
 
 void launch_splat(const SplatLaunch &P, hipStream_t st) {
-    hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
+    static const bool strip = [] {
+        const char *e = std::getenv("NH_SPLAT_STRIP");
+        return !e || e[0] != '0';
+    }();
+    if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
+    else hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     dim3 grid((mcols + 15) / 16, (mrows + 15) / 16);
     hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, P);
