@@ -586,6 +586,127 @@ __global__ __launch_bounds__(256) void nh_block_splat_strip_kernel(SplatLaunch P
     }
 }
 
+// Block splat for the 2-pixel border (filter radius in (1.5, 2.5): Nori's default Gaussian, Mitchell-Netravali),
+// where a sample at block pixel (lx, ly) can only reach block-array columns lx..lx+4 and rows ly..ly+4.
+// Phase 1 tabulates each sample's filter weights for those five columns and rows -- wx[d] = the reference's
+// m_weightsX entry for column lx+2+d, 0 outside its box -- so phase 2 does no box test and no table lookup.
+// Phase 2 gives each thread a 6-pixel column strip; for every candidate sample (x-major, as getSampleIndices
+// orders them) the rows the sample reaches are compile-time offsets, each taking ((v * wx) * wy) as packed
+// pairs. A sample outside the block, absent or invalid has all weights 0: it adds (+-)0 to sums that start
+// at +0 and can never be -0, and finite (v * wx) * 0 is 0, so every sum is the one the reference forms.
+// Each workgroup walks kTabRounds rounds of one block; the next round's records are loaded during the
+// current round's phase 2.
+constexpr int kTabRounds = 4;
+constexpr int kTabRow = 33;                 // plane row: lx 0..31 + a zero column (lx outside 0..31)
+constexpr int kTabPlane = 40 * kTabRow;     // rows ly = -4..35 (ly + 4): 4 zero rows either side
+constexpr int kTabV = 0, kTabWX = 3, kTabWY = 8, kTabPlanes = 13;
+__global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
+    __shared__ float W[kTabPlanes * kTabPlane];
+    __shared__ float tab[33];
+    const int slot = blockIdx.x;
+    const int bid = P.blocks[slot];
+    const int by = bid / P.nbx, bx = bid - by * P.nbx;
+    const int ox = bx * 32, oy = by * 32;
+    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+    const int k0 = blockIdx.y * kTabRounds, k1 = min(k0 + kTabRounds, P.n_rounds);
+    const float r = P.radius;
+    if (threadIdx.x < 33) tab[threadIdx.x] = P.table[threadIdx.x];
+    // the zero rows and column are never written again
+    for (int i = threadIdx.x; i < kTabPlanes * 40; i += 256) {
+        const int p = i / 40, row = i - p * 40;
+        W[p * kTabPlane + row * kTabRow + 32] = 0.f;
+    }
+    for (int i = threadIdx.x; i < kTabPlanes * 8 * 32; i += 256) {
+        const int p = i >> 8, q = i & 255, row = q >> 5;
+        W[p * kTabPlane + (row < 4 ? row : row + 32) * kTabRow + (q & 31)] = 0.f;
+    }
+    // phase-1 samples of this thread: (lx, ly) = (s & 31, s >> 5), s = threadIdx.x + 256 q (block rows are
+    // consecutive list entries: neighbouring lanes load neighbouring records)
+    int li[4];
+    float4 rec[4];
+    float rjy[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
+        li[q] = (lx < sxb && ly < syb) ? P.pixel_map[(oy + ly) * P.width + (ox + lx)] : -1;
+    }
+    auto fetch = [&](int k) {
+        const size_t rbase = (size_t)k * P.n_list;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (li[q] >= 0) {
+                rec[q] = P.rec_rgbx[rbase + li[q]];
+                rjy[q] = P.rec_jy[rbase + li[q]];
+            }
+    };
+    fetch(k0);
+    // phase-2 strip of this thread: block-array column xt, rows yt0..yt0+5
+    const int seg = threadIdx.x / 36, xt = threadIdx.x - seg * 36, yt0 = seg * kStripRows;
+    for (int k = k0; k < k1; ++k) {
+        __syncthreads();  // the previous round's phase 2 is done with W (and tab / zero rows are in place)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
+            float v[3] = {0.f, 0.f, 0.f}, wx[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, wy[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+            if (li[q] >= 0 && is_valid(f3(rec[q].x, rec[q].y, rec[q].z))) {  // invalid samples drop with their weight
+                const float spx = (float)(ox + lx) + rec[q].w, spy = (float)(oy + ly) + rjy[q];
+                const float px = spx - 0.5f - (float)(ox - 2), py = spy - 0.5f - (float)(oy - 2);
+                const int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
+                const int x1 = min((int)floorf(px + r), 35), y1 = min((int)floorf(py + r), 35);
+#pragma unroll
+                for (int d = 0; d < 5; ++d) {
+                    const int xc = lx + d, yc = ly + d;  // block-array column / row lx+2+(d-2)
+                    if (xc >= x0 && xc <= x1) wx[d] = tab[(int)(fabsf((float)xc - px) * P.lookup)];
+                    if (yc >= y0 && yc <= y1) wy[d] = tab[(int)(fabsf((float)yc - py) * P.lookup)];
+                }
+                v[0] = rec[q].x; v[1] = rec[q].y; v[2] = rec[q].z;
+            }
+            const int j = (ly + 4) * kTabRow + lx;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) W[(kTabV + c) * kTabPlane + j] = v[c];
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {
+                W[(kTabWX + d) * kTabPlane + j] = wx[d];
+                W[(kTabWY + d) * kTabPlane + j] = wy[d];
+            }
+        }
+        __syncthreads();
+        if (k + 1 < k1) fetch(k + 1);  // in flight during phase 2
+        if (threadIdx.x < 36 * 6) {
+            sf2 rg[kStripRows], bw[kStripRows];
+#pragma unroll
+            for (int j = 0; j < kStripRows; ++j) {
+                rg[j] = sf2{0.f, 0.f};
+                bw[j] = sf2{0.f, 0.f};
+            }
+#pragma unroll
+            for (int e = 0; e < 5; ++e) {  // sample column lx = xt - 4 + e: the pixel is its column offset 4 - e
+                const int lx = xt - 4 + e;
+                const float *base = W + yt0 * kTabRow + ((unsigned)lx < 32u ? lx : 32);
+#pragma unroll
+                for (int i = 0; i < kStripRows + 4; ++i) {  // sample row ly = yt0 - 4 + i (plane row yt0 + i)
+                    const float *w = base + i * kTabRow;
+                    const float wx = w[(kTabWX + 4 - e) * kTabPlane];
+                    const sf2 vrg = sf2{w[(kTabV + 0) * kTabPlane], w[(kTabV + 1) * kTabPlane]} * wx;
+                    const sf2 vbw = sf2{w[(kTabV + 2) * kTabPlane], 1.0f} * wx;
+#pragma unroll
+                    for (int dy = 0; dy < 5; ++dy) {  // row offset dy of the sample: strip row i - 4 + dy
+                        const int j = i - 4 + dy;
+                        if (j < 0 || j >= kStripRows) continue;
+                        const float wy = w[(kTabWY + dy) * kTabPlane];
+                        rg[j] += vrg * wy;
+                        bw[j] += vbw * wy;
+                    }
+                }
+            }
+            float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(36 * 36);
+#pragma unroll
+            for (int j = 0; j < kStripRows; ++j)
+                out[(yt0 + j) * 36 + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
+        }
+    }
+}
+
 // Rendered blocks whose merged region ((sx+2b) x (sy+2b) at offset (ox, oy) in master coordinates)
 // covers master pixel (mx, my), in BlockGenerator spiral order: the order ImageBlock::put(ImageBlock&)
 // adds them (src/utils/block.cpp:125-134). Returns their number (<= 4) and slots.
@@ -753,7 +874,14 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
         const char *e = std::getenv("NH_SPLAT_STRIP");
         return !e || e[0] != '0';
     }();
-    if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
+    static const bool tabulated = [] {
+        const char *e = std::getenv("NH_SPLAT_TAB");
+        return !e || e[0] != '0';
+    }();
+    if (tabulated && P.border == 2 && P.reach == 2)
+        hipLaunchKernelGGL(nh_block_splat_tab_kernel, dim3(P.n_blocks, (P.n_rounds + kTabRounds - 1) / kTabRounds),
+                           dim3(256), 0, st, P);
+    else if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     else hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     dim3 grid((mcols + 15) / 16, (mrows + 15) / 16);
