@@ -22,7 +22,7 @@ HIP_FLAGS  := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) $(FP_FLAGS) \
 
 HOST_SRC := $(PKG)/host/xml_lite.cpp $(PKG)/host/scene_loader.cpp $(PKG)/host/bvh_build.cpp $(PKG)/host/image_io.cpp \
             $(PKG)/host/png_decode.cpp
-HIP_SRC  := $(PKG)/csrc/nh_kernels.hip $(PKG)/csrc/nh_wavefront.hip $(PKG)/csrc/nh_denoise.hip \
+HIP_SRC  := $(PKG)/csrc/nh_kernels.hip $(PKG)/csrc/nh_wavefront.hip $(PKG)/csrc/nh_denoise.hip $(PKG)/csrc/nh_splat.hip \
             $(PKG)/csrc/nh_api.hip
 HOST_OBJ := $(patsubst $(PKG)/host/%.cpp,$(OBJDIR)/host_%.o,$(HOST_SRC))
 HIP_OBJ  := $(patsubst $(PKG)/csrc/%.hip,$(OBJDIR)/hip_%.o,$(HIP_SRC))

@@ -272,6 +272,9 @@ typedef struct nh_render_stats {
     /* nh_denoise / nh_denoise_image: summed device time and kernel launches */
     double kernel_ms_denoise;
     uint64_t launches_denoise;
+    /* wavefront chunks whose tail kernel ran on a tail slot's stream, decoupled from the chunk's path pool
+       (RR-ahead pipeline with several pools: the pool took the next chunk meanwhile) */
+    uint64_t tails_async;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;

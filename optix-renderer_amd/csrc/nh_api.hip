@@ -36,6 +36,10 @@ constexpr int kRing = 4;   // bounce-count copies in flight per pool
 // hundreds of bounces) the next ones fill the GPU; NH_POOLS=1..kPools overrides the default (2 measured
 // best: C4 2134-2147 Msamples/s vs 1913-1938 at 3 pools and 2078-2092 at 4; C2 / bumpy-1M unchanged)
 constexpr int kPools = 4;
+// tail slots: a chunk whose last live paths were handed off (RR-ahead pipeline, several pools) finishes its tail
+// kernel and splat on one of these (own stream, small packed path buffer), while its pool takes the next chunk
+constexpr int kTails = 3;
+constexpr int kTailCap = 65536;  // paths a tail slot holds (the fused bounce's tail threshold is at most this)
 #ifndef NH_DEFAULT_POOLS
 #define NH_DEFAULT_POOLS 2
 #endif
@@ -68,6 +72,7 @@ struct WfPool {
     hipEvent_t copy_ev[kRing] = {};
     std::vector<hipEvent_t> events;  // 4 per bounce (timing)
     hipEvent_t ev_begin = nullptr, ev_path = nullptr, ev_splat0 = nullptr, ev_splat = nullptr;
+    hipEvent_t ev_handoff = nullptr;  // the packed tail paths are written (a tail slot's stream waits for it)
     enum State { IDLE, ENQUEUE, COUNTS, SPLAT, FINISH } state = IDLE;
     WfJob job{};
     WfLaunch L{};
@@ -148,7 +153,7 @@ struct nh_ctx {
     nh_render_stats stats{};
     // wavefront pipeline (see "Wavefront pipeline" below): path pools, each on its own stream, and
     // the queue of chunks not yet started
-    WfPool pools[kPools];
+    WfPool pools[kPools + kTails];  // [0, kPools): path pools; then the tail slots
     std::deque<WfJob> jobs;
     uint64_t job_seq = 0, splat_seq = 0;  // chunks are splatted into fb in submission order
     hipEvent_t fb_ev = nullptr;           // the last enqueued write of fb (clear or splat)
@@ -765,7 +770,7 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
 
 constexpr size_t kWfBytesPerPath = 2 * (16 * 6 + 8 + 1) + 36;  // two buffers + shadow queue
 
-static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t staging_f4) {
+static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t rec_n, size_t staging_f4) {
     if (!p.stream) {  // the stream is created last: a pool with a stream has all of these
         if (!p.h_counts && hipHostMalloc(reinterpret_cast<void **>(&p.h_counts),
                                          (kRing * 2 * kCountGroup + kCountSlot) * sizeof(unsigned)) != hipSuccess) {
@@ -776,6 +781,7 @@ static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t staging_f4) {
             if (!e) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         for (hipEvent_t *e : {&p.ev_begin, &p.ev_path, &p.ev_splat0, &p.ev_splat})
             if (!*e) HIP_TRY(c, hipEventCreate(e));
+        if (!p.ev_handoff) HIP_TRY(c, hipEventCreateWithFlags(&p.ev_handoff, hipEventDisableTiming));
         HIP_TRY(c, hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));
     }
     if (p.cap < n) {
@@ -795,16 +801,24 @@ static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t staging_f4) {
         for (WfBuf &B : W.buf)
             ok = ok && alloc(B.ray_o, nq) && alloc(B.ray_d, nq) && alloc(B.hit, nq) && alloc(B.rng, nq) &&
                  alloc(B.li, nq) && alloc(B.thr, nq) && alloc(B.pend, nq) && alloc(B.occl, nq);
-        ok = ok && alloc(W.sh_o, nq) && alloc(W.sh_d, nq) && alloc(W.sh_slot, nq) && alloc(W.counts, 2 * kCountSlot) &&
-             alloc(p.rec, n) && alloc(p.rec_jy, n);
+        ok = ok && alloc(W.sh_o, nq) && alloc(W.sh_d, nq) && alloc(W.sh_slot, nq) && alloc(W.counts, 2 * kCountSlot);
         if (!ok) {
             free_all(p.bufs);
             p.wf = WfState{};
-            p.rec = nullptr;
-            p.rec_jy = nullptr;
             return fail(c, "hipMalloc failed for wavefront path state"), NH_ERR_DEVICE;
         }
         p.cap = n;
+    }
+    // the chunk's sample records: owned by whichever pool or tail slot holds the chunk (they move with it)
+    if (p.rec_cap < rec_n) {
+        (void)hipFree(p.rec);
+        (void)hipFree(p.rec_jy);
+        p.rec = nullptr;
+        p.rec_jy = nullptr;
+        p.rec_cap = 0;
+        HIP_TRY(c, hipMalloc(&p.rec, rec_n * sizeof(float4)));
+        HIP_TRY(c, hipMalloc(&p.rec_jy, rec_n * sizeof(float)));
+        p.rec_cap = rec_n;
     }
     if (p.staging_cap < staging_f4) {
         (void)hipFree(p.staging);
@@ -818,13 +832,15 @@ static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t staging_f4) {
 
 static void pool_free(WfPool &p) {
     free_all(p.bufs);
+    (void)hipFree(p.rec);
+    (void)hipFree(p.rec_jy);
     (void)hipFree(p.staging);
     (void)hipFree(p.spill);
     if (p.h_counts) (void)hipHostFree(p.h_counts);
     for (hipEvent_t e : p.events) (void)hipEventDestroy(e);
     for (hipEvent_t e : p.copy_ev)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {p.ev_begin, p.ev_path, p.ev_splat0, p.ev_splat})
+    for (hipEvent_t e : {p.ev_begin, p.ev_path, p.ev_splat0, p.ev_splat, p.ev_handoff})
         if (e) (void)hipEventDestroy(e);
     if (p.stream) (void)hipStreamDestroy(p.stream);
     p = WfPool{};
@@ -854,7 +870,12 @@ static SplatLaunch make_splat(const nh_ctx *c, const float4 *rec, const float *r
     return P;
 }
 
-static size_t block_px(const nh_ctx *c) { return (size_t)(32 + 2 * c->border) * (32 + 2 * c->border); }
+// float4 entries of one (round, block) ImageBlock in the splat's staging buffer (0: the fused splat stages nothing)
+static size_t block_px(const nh_ctx *c) {
+    const int reach = (int)std::floor(c->filter.radius + 0.5f);
+    if (!nh::splat_uses_staging(c->border, reach)) return 0;
+    return (size_t)(32 + 2 * c->border) * (32 + 2 * c->border);
+}
 
 // path pools driven by pipeline_run (NH_POOLS: 1 = no overlap, for A/B and tests). Scenes with mirror or
 // dielectric BSDFs get a third pool: their chunks end in tails of discrete chains that survive Russian roulette
@@ -871,15 +892,26 @@ static int active_pools(const nh_ctx *c) {
 // start job j on idle pool p: buffers, traversal choice, initial queue (all n_paths camera paths)
 static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     const int n_paths = j.rounds * c->n_list;
-    int rc = pool_alloc(c, p, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c));
+    int rc = pool_alloc(c, p, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c));
     if (rc) return rc;
     // the other pools in use get the same capacity now (idle ones only: nothing of theirs is in
     // flight), so the first render call, not a later one, pays for their allocation
     for (int i = 0; i < active_pools(c); ++i) {
         WfPool &o = c->pools[i];
         if (&o == &p || o.state != WfPool::IDLE) continue;
-        if ((rc = pool_alloc(c, o, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c)))) return rc;
+        if ((rc = pool_alloc(c, o, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c))))
+            return rc;
     }
+    // so do the idle tail slots' record and staging buffers: chunks hand theirs over at a tail hand-off and take the
+    // slot's, and a pool that had to grow them later would free and allocate inside the pipeline (hipFree waits
+    // for the whole device: a 6-9 ms stall behind the running tails)
+    if (active_pools(c) > 1)
+        for (int i = kPools; i < kPools + kTails; ++i) {
+            WfPool &o = c->pools[i];
+            if (o.state != WfPool::IDLE) continue;
+            if ((rc = pool_alloc(c, o, (size_t)kTailCap, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c))))
+                return rc;
+        }
     p.job = j;
     WfLaunch &L = p.L;
     L = WfLaunch{};
@@ -965,6 +997,80 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     return NH_OK;
 }
 
+// The chunk (everything but the pool's stream and path state) moves between a pool and a tail slot: its job and
+// launch parameters, timing events, pinned count ring, bounce counts, sample records and staging.
+static void chunk_swap(WfPool &a, WfPool &b) {
+    std::swap(a.h_counts, b.h_counts);
+    std::swap(a.copy_ev, b.copy_ev);
+    std::swap(a.events, b.events);
+    std::swap(a.ev_begin, b.ev_begin);
+    std::swap(a.ev_path, b.ev_path);
+    std::swap(a.ev_splat0, b.ev_splat0);
+    std::swap(a.ev_splat, b.ev_splat);
+    std::swap(a.job, b.job);
+    std::swap(a.L, b.L);
+    std::swap(a.persistent, b.persistent);
+    std::swap(a.wide, b.wide);
+    std::swap(a.tail, b.tail);
+    std::swap(a.draining, b.draining);
+    std::swap(a.fused, b.fused);
+    std::swap(a.sorted, b.sorted);
+    std::swap(a.rr, b.rr);
+    std::swap(a.shade_sorted, b.shade_sorted);
+    std::swap(a.tail_at, b.tail_at);
+    std::swap(a.drain_at, b.drain_at);
+    std::swap(a.it, b.it);
+    std::swap(a.in_e, b.in_e);
+    std::swap(a.in_s, b.in_s);
+    std::swap(a.rec, b.rec);
+    std::swap(a.rec_jy, b.rec_jy);
+    std::swap(a.rec_cap, b.rec_cap);
+    std::swap(a.staging, b.staging);
+    std::swap(a.staging_cap, b.staging_cap);
+}
+
+// an idle tail slot for pool p's chunk, or null: the tail then runs in place on the pool's stream. Off with one
+// pool (the serialized roofline pass: kernels alone on the GPU) and with NH_TAIL_ASYNC=0.
+static WfPool *free_tail_slot(nh_ctx *c, const WfPool &p, int bound) {
+    if (!p.rr || bound > kTailCap || active_pools(c) < 2) return nullptr;
+    if (const char *e = std::getenv("NH_TAIL_ASYNC"))
+        if (e[0] == '0') return nullptr;
+    for (int i = kPools; i < kPools + kTails; ++i)
+        if (c->pools[i].state == WfPool::IDLE) return &c->pools[i];
+    return nullptr;
+}
+
+// Hand the chunk's tail to tail slot T: pack the (at most bound) live paths into T's buffer on the pool's stream,
+// move the chunk to T, and run its tail kernel on T's stream once the pack is done. The pool is idle at once:
+// stream order keeps its next chunk's kernels behind the pack. The tail's paths, draws and arithmetic are the
+// in-place tail's; the chunk's splat still waits for its turn (submission order), so the image is unchanged.
+static int pool_handoff(nh_ctx *c, WfPool &p, WfPool &T, int bound, hipEvent_t *ev) {
+    int rc = pool_alloc(c, T, (size_t)kTailCap, 0, 0);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemsetAsync(T.wf.counts, 0, kCountSlot * sizeof(unsigned), p.stream));
+    nh::launch_wf_pack_rr(p.L, T.wf.buf[0], T.wf.counts, bound, p.stream);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(p.ev_handoff, p.stream));
+    chunk_swap(p, T);
+    WfLaunch &L = T.L;  // the packed queue: buffer 0 of T, all paths in count shard 0
+    L.st = T.wf;
+    L.in_q = 0;
+    L.cnt_in = T.wf.counts;  // (seg_cap stays the pool's: with one shard it does not address the packed queue, and
+                             // it still bounds the pool's own counts the finish reads back)
+    HIP_TRY(c, hipStreamWaitEvent(T.stream, p.ev_handoff, 0));
+    HIP_TRY(c, hipEventRecord(ev[1], T.stream));
+    HIP_TRY(c, hipEventRecord(ev[2], T.stream));
+    nh::launch_wf_tail_rr(c->d_scene, c->tv, L, T.job.ordered, T.job.stats, bound, T.stream);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipEventRecord(ev[3], T.stream));
+    T.tail = true;
+    T.draining = true;
+    T.state = WfPool::SPLAT;
+    p.state = WfPool::IDLE;
+    c->stats.tails_async++;
+    return NH_OK;
+}
+
 // enqueue bounce p.it (extend, any-hit, then shade or, once few paths are left, the tail kernel)
 static int pool_enqueue(nh_ctx *c, WfPool &p) {
     WfLaunch &L = p.L;
@@ -987,6 +1093,8 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
     HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), p.stream));
     HIP_TRY(c, hipEventRecord(ev[0], p.stream));
     if (p.fused) {  // one kernel per bounce: its input already carries the hits (and no pending light samples)
+        if (it > 0 && (int64_t)bound <= p.tail_at)
+            if (WfPool *T = free_tail_slot(c, p, bound)) return pool_handoff(c, p, *T, bound, ev);
         HIP_TRY(c, hipEventRecord(ev[1], p.stream));
         HIP_TRY(c, hipEventRecord(ev[2], p.stream));
         if (it > 0 && (int64_t)bound <= p.tail_at) {

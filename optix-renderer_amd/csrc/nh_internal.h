@@ -38,6 +38,8 @@ struct SplatLaunch {
     const int *block_slot;  // block id -> slot or -1
     int n_blocks;
     float4 *staging;
+    int debug;              // timing experiments only (NH_SPLAT_DEBUG, images wrong): bits skip the fused splat's
+                            // phase 1 (1), phase 2 (2), record fetch (4), master-border strips (8)
 };
 
 // SimpleDenoiser pass (nh_denoise.hip): interior pixel (i, j) of an image at ptr[i * stride + j]
@@ -74,6 +76,8 @@ void launch_trace_wide(const nhd::DScene *S, const nhd::Traversal &tv, const Ray
 void launch_path(const nhd::DScene *S, const nhd::Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
                  int depth, hipStream_t st);
 void launch_splat(const SplatLaunch &P, hipStream_t st);
+// false: launch_splat adds the records straight into the master (no per-(round, block) staging buffer)
+bool splat_uses_staging(int border, int reach);
 void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st);
 void launch_denoise_variance(const DenoiseLaunch &P, hipStream_t st);
 int denoise_band_rows();
@@ -158,4 +162,6 @@ void launch_wf_tail_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfL
                        hipStream_t st);
 void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                     bool wide, int bound, int depth, hipStream_t st);
+// copies the live RR-ahead paths of L's input queue (at most bound) densely into dst, count into dst_counts[0]
+void launch_wf_pack_rr(const WfLaunch &L, const WfBuf &dst, unsigned *dst_counts, int bound, hipStream_t st);
 }  // namespace nh

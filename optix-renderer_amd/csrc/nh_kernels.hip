@@ -5,11 +5,7 @@
 //                     renderBlock's per-pixel body + PathMISIntegrator::Li / PathMatsIntegrator::Li
 //                     (src/utils/render.cpp:436-458, src/integrators/path_mis.cpp:16-150,
 //                     path_mats.cpp:16-78), writing (radiance, jitter) sample records
-//   nh_block_splat_kernel  ImageBlock::put(pos, value) into each (round, block)'s own
-//                     ImageBlock in LDS, samples in getSampleIndices order (x outer, y inner)
-//   nh_merge_kernel   ImageBlock::put(block) into the master (src/utils/block.cpp:93-134):
-//                     per master pixel, rounds in order, blocks in BlockGenerator spiral order
-//                     -- the serial reference's summation order, bit for bit
+//   (the ImageBlock stage -- splat and merge of the sample records -- is in nh_splat.hip)
 #include <cstdlib>
 
 #include "nh_internal.h"
@@ -448,338 +444,6 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
     if (STATS) flush_stats(st, queries, stat_shard(L.counters));
 }
 
-// ImageBlock::put(pos, value) into the per-block ImageBlock of one (round, block)
-// (src/utils/render.cpp:421-458 + src/utils/block.cpp:93-123). One workgroup per
-// (block, round): phase 1 computes every sample's filter footprint once into LDS; phase 2
-// gives each block-array pixel the ordered sum of its contributions, in the reference's
-// getSampleIndices order (x outer, y inner), starting from the cleared block (0).
-constexpr int kSplatMaxCols = 40;  // 32 + 2*border, border <= 4
-constexpr int kStripRows = 6;      // block-array rows one thread sums in the strip variant
-
-// phase 1 of the block splat: every sample's footprint (block-array box), filter position and value into LDS
-// (sample (lx, ly) at lx*33 + ly: x-major, the odd stride keeps neighbouring lx on distinct banks)
-struct SplatLds {
-    float val[3][32 * 33];
-    float pos[2][32 * 33];
-    int box[32 * 33];  // x0 | x1<<8 | y0<<16 | y1<<24 (block-array coords), x1 < x0: empty
-    float tab[33];
-};
-__device__ __forceinline__ void splat_stage(const SplatLaunch &P, SplatLds &L, int ox, int oy, int sxb, int syb, int k,
-                                            int cols) {
-    const float r = P.radius;
-    if (threadIdx.x < 33) L.tab[threadIdx.x] = P.table[threadIdx.x];
-    const size_t rbase = (size_t)k * P.n_list;
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-        // thread i loads pixel (lx, ly) = (i % 32, i / 32): neighbouring lanes read neighbouring pixels of a
-        // block row, i.e. consecutive list entries (the pixel list is row-major inside a block), so each
-        // wave's record loads are 16-B-per-lane contiguous runs; the LDS layout is x-major
-        const int lx = i & 31, ly = i >> 5;
-        int box = 0xff;  // x0 = 255 > x1 = 0: empty
-        float vx = 0.f, vy = 0.f, vz = 0.f, px = 0.f, py = 0.f;
-        if (lx < sxb && ly < syb) {
-            const int li = P.pixel_map[(oy + ly) * P.width + (ox + lx)];
-            if (li >= 0) {
-                const float4 rec = P.rec_rgbx[rbase + li];
-                if (is_valid(f3(rec.x, rec.y, rec.z))) {  // invalid samples drop with their weight
-                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li];
-                    px = spx - 0.5f - (float)(ox - P.border);
-                    py = spy - 0.5f - (float)(oy - P.border);
-                    int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
-                    int x1 = min((int)floorf(px + r), cols - 1), y1 = min((int)floorf(py + r), cols - 1);
-                    box = x0 | (x1 << 8) | (y0 << 16) | (y1 << 24);
-                    vx = rec.x; vy = rec.y; vz = rec.z;
-                }
-            }
-        }
-        const int j = lx * 33 + ly;
-        L.val[0][j] = vx; L.val[1][j] = vy; L.val[2][j] = vz;
-        L.pos[0][j] = px; L.pos[1][j] = py;
-        L.box[j] = box;
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
-    __shared__ SplatLds L;
-    const int slot = blockIdx.x, k = blockIdx.y;
-    const int bid = P.blocks[slot];
-    const int by = bid / P.nbx, bx = bid - by * P.nbx;
-    const int ox = bx * 32, oy = by * 32;
-    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    const int cols = 32 + 2 * P.border;
-    splat_stage(P, L, ox, oy, sxb, syb, k, cols);
-    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
-    const int R = P.reach, bd = P.border;
-    for (int q = threadIdx.x; q < cols * cols; q += 256) {
-        const int yt = q / cols, xt = q - yt * cols;
-        float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
-        const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
-        const int ly0 = max(yt - bd - R, 0), ly1 = min(yt - bd + R, syb - 1);
-        for (int lx = lx0; lx <= lx1; ++lx)
-            for (int ly = ly0; ly <= ly1; ++ly) {
-                const int i = lx * 33 + ly;
-                const int box = L.box[i];
-                const int x0 = box & 0xff, x1 = (box >> 8) & 0xff, y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
-                if (xt < x0 || xt > x1 || yt < y0 || yt > y1) continue;
-                const float wx = L.tab[(int)(fabsf((float)xt - L.pos[0][i]) * P.lookup)];
-                const float wy = L.tab[(int)(fabsf((float)yt - L.pos[1][i]) * P.lookup)];
-                ar += L.val[0][i] * wx * wy;
-                ag += L.val[1][i] * wx * wy;
-                ab += L.val[2][i] * wx * wy;
-                aw += 1.0f * wx * wy;
-            }
-        out[q] = make_float4(ar, ag, ab, aw);
-    }
-}
-
-// The same block splat with each thread summing a strip of kStripRows block-array pixels of one column: a
-// candidate sample's record, x test and column weight are read / computed once for the strip, and its products
-// (v * wx) once as packed-FP32 pairs; each pixel of the strip then takes its row test, row weight and
-// ((v * wx) * wy) products. Every pixel still sums its samples' contributions in getSampleIndices order (the
-// strip walks samples x-major), so the floats are those of nh_block_splat_kernel.
-typedef float sf2 __attribute__((ext_vector_type(2)));
-__global__ __launch_bounds__(256) void nh_block_splat_strip_kernel(SplatLaunch P) {
-    __shared__ SplatLds L;
-    const int slot = blockIdx.x, k = blockIdx.y;
-    const int bid = P.blocks[slot];
-    const int by = bid / P.nbx, bx = bid - by * P.nbx;
-    const int ox = bx * 32, oy = by * 32;
-    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    const int cols = 32 + 2 * P.border;
-    splat_stage(P, L, ox, oy, sxb, syb, k, cols);
-    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
-    const int R = P.reach, bd = P.border;
-    const int n_strips = (cols + kStripRows - 1) / kStripRows;
-    for (int t = threadIdx.x; t < cols * n_strips; t += 256) {
-        const int xt = t % cols, yt0 = (t / cols) * kStripRows;
-        sf2 rg[kStripRows], bw[kStripRows];
-#pragma unroll
-        for (int j = 0; j < kStripRows; ++j) {
-            rg[j] = sf2{0.f, 0.f};
-            bw[j] = sf2{0.f, 0.f};
-        }
-        const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
-        const int ly0 = max(yt0 - bd - R, 0), ly1 = min(yt0 + kStripRows - 1 - bd + R, syb - 1);
-        const float fxt = (float)xt;
-        for (int lx = lx0; lx <= lx1; ++lx)
-            for (int ly = ly0; ly <= ly1; ++ly) {
-                const int i = lx * 33 + ly;
-                const int box = L.box[i];
-                const int x0 = box & 0xff, x1 = (box >> 8) & 0xff;
-                if (xt < x0 || xt > x1) continue;
-                const int y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
-                const float wx = L.tab[(int)(fabsf(fxt - L.pos[0][i]) * P.lookup)];
-                const float py = L.pos[1][i];
-                const sf2 vrg = sf2{L.val[0][i], L.val[1][i]} * wx, vbw = sf2{L.val[2][i], 1.0f} * wx;
-#pragma unroll
-                for (int j = 0; j < kStripRows; ++j) {
-                    const int yt = yt0 + j;
-                    if (yt < y0 || yt > y1) continue;
-                    const float wy = L.tab[(int)(fabsf((float)yt - py) * P.lookup)];
-                    rg[j] += vrg * wy;
-                    bw[j] += vbw * wy;
-                }
-            }
-#pragma unroll
-        for (int j = 0; j < kStripRows; ++j)
-            if (yt0 + j < cols) out[(yt0 + j) * cols + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
-    }
-}
-
-// Block splat for the 2-pixel border (filter radius in (1.5, 2.5): Nori's default Gaussian, Mitchell-Netravali),
-// where a sample at block pixel (lx, ly) can only reach block-array columns lx..lx+4 and rows ly..ly+4.
-// Phase 1 tabulates each sample's filter weights for those five columns and rows -- wx[d] = the reference's
-// m_weightsX entry for column lx+2+d, 0 outside its box -- so phase 2 does no box test and no table lookup.
-// Phase 2 gives each thread a 6-pixel column strip; for every candidate sample (x-major, as getSampleIndices
-// orders them) the rows the sample reaches are compile-time offsets, each taking ((v * wx) * wy) as packed
-// pairs. A sample outside the block, absent or invalid has all weights 0: it adds (+-)0 to sums that start
-// at +0 and can never be -0, and finite (v * wx) * 0 is 0, so every sum is the one the reference forms.
-// Each workgroup walks kTabRounds rounds of one block; the next round's records are loaded during the
-// current round's phase 2.
-constexpr int kTabRounds = 4;
-constexpr int kTabRow = 33;                 // plane row: lx 0..31 + a zero column (lx outside 0..31)
-constexpr int kTabPlane = 40 * kTabRow;     // rows ly = -4..35 (ly + 4): 4 zero rows either side
-constexpr int kTabV = 0, kTabWX = 3, kTabWY = 8, kTabPlanes = 13;
-__global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
-    __shared__ float W[kTabPlanes * kTabPlane];
-    __shared__ float tab[33];
-    const int slot = blockIdx.x;
-    const int bid = P.blocks[slot];
-    const int by = bid / P.nbx, bx = bid - by * P.nbx;
-    const int ox = bx * 32, oy = by * 32;
-    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    const int k0 = blockIdx.y * kTabRounds, k1 = min(k0 + kTabRounds, P.n_rounds);
-    const float r = P.radius;
-    if (threadIdx.x < 33) tab[threadIdx.x] = P.table[threadIdx.x];
-    // the zero rows and column are never written again
-    for (int i = threadIdx.x; i < kTabPlanes * 40; i += 256) {
-        const int p = i / 40, row = i - p * 40;
-        W[p * kTabPlane + row * kTabRow + 32] = 0.f;
-    }
-    for (int i = threadIdx.x; i < kTabPlanes * 8 * 32; i += 256) {
-        const int p = i >> 8, q = i & 255, row = q >> 5;
-        W[p * kTabPlane + (row < 4 ? row : row + 32) * kTabRow + (q & 31)] = 0.f;
-    }
-    // phase-1 samples of this thread: (lx, ly) = (s & 31, s >> 5), s = threadIdx.x + 256 q (block rows are
-    // consecutive list entries: neighbouring lanes load neighbouring records)
-    int li[4];
-    float4 rec[4];
-    float rjy[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
-        li[q] = (lx < sxb && ly < syb) ? P.pixel_map[(oy + ly) * P.width + (ox + lx)] : -1;
-    }
-    auto fetch = [&](int k) {
-        const size_t rbase = (size_t)k * P.n_list;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (li[q] >= 0) {
-                rec[q] = P.rec_rgbx[rbase + li[q]];
-                rjy[q] = P.rec_jy[rbase + li[q]];
-            }
-    };
-    fetch(k0);
-    // phase-2 strip of this thread: block-array column xt, rows yt0..yt0+5
-    const int seg = threadIdx.x / 36, xt = threadIdx.x - seg * 36, yt0 = seg * kStripRows;
-    for (int k = k0; k < k1; ++k) {
-        __syncthreads();  // the previous round's phase 2 is done with W (and tab / zero rows are in place)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
-            float v[3] = {0.f, 0.f, 0.f}, wx[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, wy[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-            if (li[q] >= 0 && is_valid(f3(rec[q].x, rec[q].y, rec[q].z))) {  // invalid samples drop with their weight
-                const float spx = (float)(ox + lx) + rec[q].w, spy = (float)(oy + ly) + rjy[q];
-                const float px = spx - 0.5f - (float)(ox - 2), py = spy - 0.5f - (float)(oy - 2);
-                const int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
-                const int x1 = min((int)floorf(px + r), 35), y1 = min((int)floorf(py + r), 35);
-#pragma unroll
-                for (int d = 0; d < 5; ++d) {
-                    const int xc = lx + d, yc = ly + d;  // block-array column / row lx+2+(d-2)
-                    if (xc >= x0 && xc <= x1) wx[d] = tab[(int)(fabsf((float)xc - px) * P.lookup)];
-                    if (yc >= y0 && yc <= y1) wy[d] = tab[(int)(fabsf((float)yc - py) * P.lookup)];
-                }
-                v[0] = rec[q].x; v[1] = rec[q].y; v[2] = rec[q].z;
-            }
-            const int j = (ly + 4) * kTabRow + lx;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) W[(kTabV + c) * kTabPlane + j] = v[c];
-#pragma unroll
-            for (int d = 0; d < 5; ++d) {
-                W[(kTabWX + d) * kTabPlane + j] = wx[d];
-                W[(kTabWY + d) * kTabPlane + j] = wy[d];
-            }
-        }
-        __syncthreads();
-        if (k + 1 < k1) fetch(k + 1);  // in flight during phase 2
-        if (threadIdx.x < 36 * 6) {
-            sf2 rg[kStripRows], bw[kStripRows];
-#pragma unroll
-            for (int j = 0; j < kStripRows; ++j) {
-                rg[j] = sf2{0.f, 0.f};
-                bw[j] = sf2{0.f, 0.f};
-            }
-#pragma unroll
-            for (int e = 0; e < 5; ++e) {  // sample column lx = xt - 4 + e: the pixel is its column offset 4 - e
-                const int lx = xt - 4 + e;
-                const float *base = W + yt0 * kTabRow + ((unsigned)lx < 32u ? lx : 32);
-#pragma unroll
-                for (int i = 0; i < kStripRows + 4; ++i) {  // sample row ly = yt0 - 4 + i (plane row yt0 + i)
-                    const float *w = base + i * kTabRow;
-                    const float wx = w[(kTabWX + 4 - e) * kTabPlane];
-                    const sf2 vrg = sf2{w[(kTabV + 0) * kTabPlane], w[(kTabV + 1) * kTabPlane]} * wx;
-                    const sf2 vbw = sf2{w[(kTabV + 2) * kTabPlane], 1.0f} * wx;
-#pragma unroll
-                    for (int dy = 0; dy < 5; ++dy) {  // row offset dy of the sample: strip row i - 4 + dy
-                        const int j = i - 4 + dy;
-                        if (j < 0 || j >= kStripRows) continue;
-                        const float wy = w[(kTabWY + dy) * kTabPlane];
-                        rg[j] += vrg * wy;
-                        bw[j] += vbw * wy;
-                    }
-                }
-            }
-            float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(36 * 36);
-#pragma unroll
-            for (int j = 0; j < kStripRows; ++j)
-                out[(yt0 + j) * 36 + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
-        }
-    }
-}
-
-// Rendered blocks whose merged region ((sx+2b) x (sy+2b) at offset (ox, oy) in master coordinates)
-// covers master pixel (mx, my), in BlockGenerator spiral order: the order ImageBlock::put(ImageBlock&)
-// adds them (src/utils/block.cpp:125-134). Returns their number (<= 4) and slots.
-__device__ __forceinline__ int covering_blocks(const SplatLaunch &P, int mx, int my, int *slot) {
-    const int cols = 32 + 2 * P.border;
-    int blk[4], nb = 0;
-    const int bx_lo = max((mx - cols + 1 + 31) >> 5, 0), bx_hi = min(mx >> 5, P.nbx - 1);
-    const int nby = (P.height + 31) >> 5;
-    const int by_lo = max((my - cols + 1 + 31) >> 5, 0), by_hi = min(my >> 5, nby - 1);
-    for (int by = by_lo; by <= by_hi; ++by)
-        for (int bx = bx_lo; bx <= bx_hi; ++bx) {
-            const int bid = by * P.nbx + bx;
-            const int sl = P.block_slot[bid];
-            if (sl < 0) continue;
-            const int ox = bx * 32, oy = by * 32;
-            const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-            if (mx - ox >= sxb + 2 * P.border || my - oy >= syb + 2 * P.border) continue;
-            blk[nb] = bid;
-            slot[nb] = sl;
-            ++nb;
-        }
-    for (int a = 1; a < nb; ++a)
-        for (int b = a; b > 0 && P.block_rank[blk[b]] < P.block_rank[blk[b - 1]]; --b) {
-            int t = blk[b]; blk[b] = blk[b - 1]; blk[b - 1] = t;
-            t = slot[b]; slot[b] = slot[b - 1]; slot[b - 1] = t;
-        }
-    return nb;
-}
-
-// ImageBlock::put(ImageBlock&) into the master (src/utils/block.cpp:125-134): per master
-// pixel, per round, the overlapping rendered blocks in BlockGenerator spiral order.
-__global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
-    const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
-    const int mx = blockIdx.x * 16 + (threadIdx.x & 15), my = blockIdx.y * 16 + (threadIdx.x >> 4);
-    if (mx >= mcols || my >= mrows) return;
-    const int cols = 32 + 2 * P.border;
-    int slot[4];
-    const int nb = covering_blocks(P, mx, my, slot);
-    if (nb == 0) return;
-    int off[4];
-    for (int q = 0; q < nb; ++q) {
-        const int bid = P.blocks[slot[q]];
-        const int by = bid / P.nbx, bx = bid - by * P.nbx;
-        off[q] = (my - by * 32) * cols + (mx - bx * 32);
-    }
-    float4 *mp = reinterpret_cast<float4 *>(P.fb) + (size_t)my * mcols + mx;
-    float4 m = *mp;
-    const size_t per_round = (size_t)P.n_blocks * (size_t)(cols * cols);
-    for (int k = 0; k < P.n_rounds; ++k) {
-        const float4 *base = P.staging + (size_t)k * per_round;
-        for (int q = 0; q < nb; ++q) {
-            const float4 v = base[(size_t)slot[q] * (cols * cols) + off[q]];
-            m.x += v.x;
-            m.y += v.y;
-            m.z += v.z;
-            m.w += v.w;
-        }
-    }
-    *mp = m;
-}
-
-// invalid-sample count (ImageBlock::put drops, block.cpp:94-99)
-__global__ __launch_bounds__(256) void nh_count_invalid_kernel(const float4 *rec, size_t n, unsigned long long *out) {
-    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    unsigned long long c = 0;
-    if (i < n) {
-        float4 v = rec[i];
-        c = is_valid(f3(v.x, v.y, v.z)) ? 0 : 1;
-    }
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(stat_shard(out) + 4, c);
-}
-
 // ---------------------------------------------------------------------------
 // host-side launchers (called from nh_api.hip)
 // ---------------------------------------------------------------------------
@@ -867,31 +531,6 @@ void launch_path(const DScene *S, const Traversal &tv, const PathLaunch &L, bool
     else if (depth <= 32) launch_path_d<128, 32>(S, tv, L, ordered, stats, st);
     else if (depth <= 64) launch_path_d<64, 64>(S, tv, L, ordered, stats, st);
     else launch_path_d<64, 128>(S, tv, L, ordered, stats, st);
-}
-
-void launch_splat(const SplatLaunch &P, hipStream_t st) {
-    static const bool strip = [] {
-        const char *e = std::getenv("NH_SPLAT_STRIP");
-        return !e || e[0] != '0';
-    }();
-    static const bool tabulated = [] {
-        const char *e = std::getenv("NH_SPLAT_TAB");
-        return !e || e[0] != '0';
-    }();
-    if (tabulated && P.border == 2 && P.reach == 2)
-        hipLaunchKernelGGL(nh_block_splat_tab_kernel, dim3(P.n_blocks, (P.n_rounds + kTabRounds - 1) / kTabRounds),
-                           dim3(256), 0, st, P);
-    else if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
-    else hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
-    const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
-    dim3 grid((mcols + 15) / 16, (mrows + 15) / 16);
-    hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, P);
-}
-
-void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st) {
-    if (n == 0) return;
-    dim3 grid((unsigned)((n + 255) / 256));
-    hipLaunchKernelGGL(nh_count_invalid_kernel, grid, dim3(256), 0, st, rec, n, out);
 }
 
 }  // namespace nh

@@ -1,0 +1,706 @@
+// gfx950 kernels of the ImageBlock stage of the path_mis hot path (src/utils/block.cpp:93-134,
+// src/utils/render.cpp:421-458): the sample records of a chunk of rounds -> the master ImageBlock.
+//
+//   nh_tile_splat_kernel   (2-pixel border, the default) splat + merge fused: per 32x32 master tile, every
+//                          round's block values in BlockGenerator spiral order, straight into the master
+//   nh_block_splat_*       ImageBlock::put(pos, value) into each (round, block)'s own ImageBlock, samples in
+//                          getSampleIndices order (x outer, y inner), staged in HBM
+//   nh_merge_kernel        ImageBlock::put(block) into the master: per master pixel, rounds in order, blocks in
+//                          spiral order -- the serial reference's summation order, bit for bit
+#include <cstdio>
+#include <cstdlib>
+
+#include "nh_internal.h"
+#include "nh_shade.h"
+
+using namespace nhd;
+
+namespace {
+
+// ImageBlock::put(pos, value) into the per-block ImageBlock of one (round, block)
+// (src/utils/render.cpp:421-458 + src/utils/block.cpp:93-123). One workgroup per
+// (block, round): phase 1 computes every sample's filter footprint once into LDS; phase 2
+// gives each block-array pixel the ordered sum of its contributions, in the reference's
+// getSampleIndices order (x outer, y inner), starting from the cleared block (0).
+constexpr int kSplatMaxCols = 40;  // 32 + 2*border, border <= 4
+constexpr int kStripRows = 6;      // block-array rows one thread sums in the strip variant
+
+// phase 1 of the block splat: every sample's footprint (block-array box), filter position and value into LDS
+// (sample (lx, ly) at lx*33 + ly: x-major, the odd stride keeps neighbouring lx on distinct banks)
+struct SplatLds {
+    float val[3][32 * 33];
+    float pos[2][32 * 33];
+    int box[32 * 33];  // x0 | x1<<8 | y0<<16 | y1<<24 (block-array coords), x1 < x0: empty
+    float tab[33];
+};
+__device__ __forceinline__ void splat_stage(const SplatLaunch &P, SplatLds &L, int ox, int oy, int sxb, int syb, int k,
+                                            int cols) {
+    const float r = P.radius;
+    if (threadIdx.x < 33) L.tab[threadIdx.x] = P.table[threadIdx.x];
+    const size_t rbase = (size_t)k * P.n_list;
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        // thread i loads pixel (lx, ly) = (i % 32, i / 32): neighbouring lanes read neighbouring pixels of a
+        // block row, i.e. consecutive list entries (the pixel list is row-major inside a block), so each
+        // wave's record loads are 16-B-per-lane contiguous runs; the LDS layout is x-major
+        const int lx = i & 31, ly = i >> 5;
+        int box = 0xff;  // x0 = 255 > x1 = 0: empty
+        float vx = 0.f, vy = 0.f, vz = 0.f, px = 0.f, py = 0.f;
+        if (lx < sxb && ly < syb) {
+            const int li = P.pixel_map[(oy + ly) * P.width + (ox + lx)];
+            if (li >= 0) {
+                const float4 rec = P.rec_rgbx[rbase + li];
+                if (is_valid(f3(rec.x, rec.y, rec.z))) {  // invalid samples drop with their weight
+                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li];
+                    px = spx - 0.5f - (float)(ox - P.border);
+                    py = spy - 0.5f - (float)(oy - P.border);
+                    int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
+                    int x1 = min((int)floorf(px + r), cols - 1), y1 = min((int)floorf(py + r), cols - 1);
+                    box = x0 | (x1 << 8) | (y0 << 16) | (y1 << 24);
+                    vx = rec.x; vy = rec.y; vz = rec.z;
+                }
+            }
+        }
+        const int j = lx * 33 + ly;
+        L.val[0][j] = vx; L.val[1][j] = vy; L.val[2][j] = vz;
+        L.pos[0][j] = px; L.pos[1][j] = py;
+        L.box[j] = box;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
+    __shared__ SplatLds L;
+    const int slot = blockIdx.x, k = blockIdx.y;
+    const int bid = P.blocks[slot];
+    const int by = bid / P.nbx, bx = bid - by * P.nbx;
+    const int ox = bx * 32, oy = by * 32;
+    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+    const int cols = 32 + 2 * P.border;
+    splat_stage(P, L, ox, oy, sxb, syb, k, cols);
+    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+    const int R = P.reach, bd = P.border;
+    for (int q = threadIdx.x; q < cols * cols; q += 256) {
+        const int yt = q / cols, xt = q - yt * cols;
+        float ar = 0.f, ag = 0.f, ab = 0.f, aw = 0.f;
+        const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
+        const int ly0 = max(yt - bd - R, 0), ly1 = min(yt - bd + R, syb - 1);
+        for (int lx = lx0; lx <= lx1; ++lx)
+            for (int ly = ly0; ly <= ly1; ++ly) {
+                const int i = lx * 33 + ly;
+                const int box = L.box[i];
+                const int x0 = box & 0xff, x1 = (box >> 8) & 0xff, y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
+                if (xt < x0 || xt > x1 || yt < y0 || yt > y1) continue;
+                const float wx = L.tab[(int)(fabsf((float)xt - L.pos[0][i]) * P.lookup)];
+                const float wy = L.tab[(int)(fabsf((float)yt - L.pos[1][i]) * P.lookup)];
+                ar += L.val[0][i] * wx * wy;
+                ag += L.val[1][i] * wx * wy;
+                ab += L.val[2][i] * wx * wy;
+                aw += 1.0f * wx * wy;
+            }
+        out[q] = make_float4(ar, ag, ab, aw);
+    }
+}
+
+// The same block splat with each thread summing a strip of kStripRows block-array pixels of one column: a
+// candidate sample's record, x test and column weight are read / computed once for the strip, and its products
+// (v * wx) once as packed-FP32 pairs; each pixel of the strip then takes its row test, row weight and
+// ((v * wx) * wy) products. Every pixel still sums its samples' contributions in getSampleIndices order (the
+// strip walks samples x-major), so the floats are those of nh_block_splat_kernel.
+typedef float sf2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void nh_block_splat_strip_kernel(SplatLaunch P) {
+    __shared__ SplatLds L;
+    const int slot = blockIdx.x, k = blockIdx.y;
+    const int bid = P.blocks[slot];
+    const int by = bid / P.nbx, bx = bid - by * P.nbx;
+    const int ox = bx * 32, oy = by * 32;
+    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+    const int cols = 32 + 2 * P.border;
+    splat_stage(P, L, ox, oy, sxb, syb, k, cols);
+    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+    const int R = P.reach, bd = P.border;
+    const int n_strips = (cols + kStripRows - 1) / kStripRows;
+    for (int t = threadIdx.x; t < cols * n_strips; t += 256) {
+        const int xt = t % cols, yt0 = (t / cols) * kStripRows;
+        sf2 rg[kStripRows], bw[kStripRows];
+#pragma unroll
+        for (int j = 0; j < kStripRows; ++j) {
+            rg[j] = sf2{0.f, 0.f};
+            bw[j] = sf2{0.f, 0.f};
+        }
+        const int lx0 = max(xt - bd - R, 0), lx1 = min(xt - bd + R, sxb - 1);
+        const int ly0 = max(yt0 - bd - R, 0), ly1 = min(yt0 + kStripRows - 1 - bd + R, syb - 1);
+        const float fxt = (float)xt;
+        for (int lx = lx0; lx <= lx1; ++lx)
+            for (int ly = ly0; ly <= ly1; ++ly) {
+                const int i = lx * 33 + ly;
+                const int box = L.box[i];
+                const int x0 = box & 0xff, x1 = (box >> 8) & 0xff;
+                if (xt < x0 || xt > x1) continue;
+                const int y0 = (box >> 16) & 0xff, y1 = (box >> 24) & 0xff;
+                const float wx = L.tab[(int)(fabsf(fxt - L.pos[0][i]) * P.lookup)];
+                const float py = L.pos[1][i];
+                const sf2 vrg = sf2{L.val[0][i], L.val[1][i]} * wx, vbw = sf2{L.val[2][i], 1.0f} * wx;
+#pragma unroll
+                for (int j = 0; j < kStripRows; ++j) {
+                    const int yt = yt0 + j;
+                    if (yt < y0 || yt > y1) continue;
+                    const float wy = L.tab[(int)(fabsf((float)yt - py) * P.lookup)];
+                    rg[j] += vrg * wy;
+                    bw[j] += vbw * wy;
+                }
+            }
+#pragma unroll
+        for (int j = 0; j < kStripRows; ++j)
+            if (yt0 + j < cols) out[(yt0 + j) * cols + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
+    }
+}
+
+// Block splat for the 2-pixel border (filter radius in (1.5, 2.5): Nori's default Gaussian, Mitchell-Netravali),
+// where a sample at block pixel (lx, ly) can only reach block-array columns lx..lx+4 and rows ly..ly+4.
+// Phase 1 tabulates each sample's filter weights for those five columns and rows -- wx[d] = the reference's
+// m_weightsX entry for column lx+2+d, 0 outside its box -- so phase 2 does no box test and no table lookup.
+// Phase 2 gives each thread a 6-pixel column strip; for every candidate sample (x-major, as getSampleIndices
+// orders them) the rows the sample reaches are compile-time offsets, each taking ((v * wx) * wy) as packed
+// pairs. A sample outside the block, absent or invalid has all weights 0: it adds (+-)0 to sums that start
+// at +0 and can never be -0, and finite (v * wx) * 0 is 0, so every sum is the one the reference forms.
+// Each workgroup walks kTabRounds rounds of one block; the next round's records are loaded during the
+// current round's phase 2.
+constexpr int kTabRounds = 4;
+constexpr int kTabRow = 33;                 // plane row: lx 0..31 + a zero column (lx outside 0..31)
+constexpr int kTabPlane = 40 * kTabRow;     // rows ly = -4..35 (ly + 4): 4 zero rows either side
+constexpr int kTabV = 0, kTabWX = 3, kTabWY = 8, kTabPlanes = 13;
+__global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
+    __shared__ float W[kTabPlanes * kTabPlane];
+    __shared__ float tab[33];
+    const int slot = blockIdx.x;
+    const int bid = P.blocks[slot];
+    const int by = bid / P.nbx, bx = bid - by * P.nbx;
+    const int ox = bx * 32, oy = by * 32;
+    const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+    const int k0 = blockIdx.y * kTabRounds, k1 = min(k0 + kTabRounds, P.n_rounds);
+    const float r = P.radius;
+    if (threadIdx.x < 33) tab[threadIdx.x] = P.table[threadIdx.x];
+    // the zero rows and column are never written again
+    for (int i = threadIdx.x; i < kTabPlanes * 40; i += 256) {
+        const int p = i / 40, row = i - p * 40;
+        W[p * kTabPlane + row * kTabRow + 32] = 0.f;
+    }
+    for (int i = threadIdx.x; i < kTabPlanes * 8 * 32; i += 256) {
+        const int p = i >> 8, q = i & 255, row = q >> 5;
+        W[p * kTabPlane + (row < 4 ? row : row + 32) * kTabRow + (q & 31)] = 0.f;
+    }
+    // phase-1 samples of this thread: (lx, ly) = (s & 31, s >> 5), s = threadIdx.x + 256 q (block rows are
+    // consecutive list entries: neighbouring lanes load neighbouring records)
+    int li[4];
+    float4 rec[4];
+    float rjy[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
+        li[q] = (lx < sxb && ly < syb) ? P.pixel_map[(oy + ly) * P.width + (ox + lx)] : -1;
+    }
+    auto fetch = [&](int k) {
+        const size_t rbase = (size_t)k * P.n_list;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (li[q] >= 0) {
+                rec[q] = P.rec_rgbx[rbase + li[q]];
+                rjy[q] = P.rec_jy[rbase + li[q]];
+            }
+    };
+    fetch(k0);
+    // phase-2 strip of this thread: block-array column xt, rows yt0..yt0+5
+    const int seg = threadIdx.x / 36, xt = threadIdx.x - seg * 36, yt0 = seg * kStripRows;
+    for (int k = k0; k < k1; ++k) {
+        __syncthreads();  // the previous round's phase 2 is done with W (and tab / zero rows are in place)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
+            float v[3] = {0.f, 0.f, 0.f}, wx[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, wy[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+            if (li[q] >= 0 && is_valid(f3(rec[q].x, rec[q].y, rec[q].z))) {  // invalid samples drop with their weight
+                const float spx = (float)(ox + lx) + rec[q].w, spy = (float)(oy + ly) + rjy[q];
+                const float px = spx - 0.5f - (float)(ox - 2), py = spy - 0.5f - (float)(oy - 2);
+                const int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
+                const int x1 = min((int)floorf(px + r), 35), y1 = min((int)floorf(py + r), 35);
+#pragma unroll
+                for (int d = 0; d < 5; ++d) {
+                    const int xc = lx + d, yc = ly + d;  // block-array column / row lx+2+(d-2)
+                    if (xc >= x0 && xc <= x1) wx[d] = tab[(int)(fabsf((float)xc - px) * P.lookup)];
+                    if (yc >= y0 && yc <= y1) wy[d] = tab[(int)(fabsf((float)yc - py) * P.lookup)];
+                }
+                v[0] = rec[q].x; v[1] = rec[q].y; v[2] = rec[q].z;
+            }
+            const int j = (ly + 4) * kTabRow + lx;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) W[(kTabV + c) * kTabPlane + j] = v[c];
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {
+                W[(kTabWX + d) * kTabPlane + j] = wx[d];
+                W[(kTabWY + d) * kTabPlane + j] = wy[d];
+            }
+        }
+        __syncthreads();
+        if (k + 1 < k1) fetch(k + 1);  // in flight during phase 2
+        if (threadIdx.x < 36 * 6) {
+            sf2 rg[kStripRows], bw[kStripRows];
+#pragma unroll
+            for (int j = 0; j < kStripRows; ++j) {
+                rg[j] = sf2{0.f, 0.f};
+                bw[j] = sf2{0.f, 0.f};
+            }
+#pragma unroll
+            for (int e = 0; e < 5; ++e) {  // sample column lx = xt - 4 + e: the pixel is its column offset 4 - e
+                const int lx = xt - 4 + e;
+                const float *base = W + yt0 * kTabRow + ((unsigned)lx < 32u ? lx : 32);
+#pragma unroll
+                for (int i = 0; i < kStripRows + 4; ++i) {  // sample row ly = yt0 - 4 + i (plane row yt0 + i)
+                    const float *w = base + i * kTabRow;
+                    const float wx = w[(kTabWX + 4 - e) * kTabPlane];
+                    const sf2 vrg = sf2{w[(kTabV + 0) * kTabPlane], w[(kTabV + 1) * kTabPlane]} * wx;
+                    const sf2 vbw = sf2{w[(kTabV + 2) * kTabPlane], 1.0f} * wx;
+#pragma unroll
+                    for (int dy = 0; dy < 5; ++dy) {  // row offset dy of the sample: strip row i - 4 + dy
+                        const int j = i - 4 + dy;
+                        if (j < 0 || j >= kStripRows) continue;
+                        const float wy = w[(kTabWY + dy) * kTabPlane];
+                        rg[j] += vrg * wy;
+                        bw[j] += vbw * wy;
+                    }
+                }
+            }
+            float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(36 * 36);
+#pragma unroll
+            for (int j = 0; j < kStripRows; ++j)
+                out[(yt0 + j) * 36 + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
+        }
+    }
+}
+
+// Fused splat + merge for the 2-pixel border: one workgroup per 32x32 tile of MASTER pixels walks the chunk's
+// rounds in order and adds every round's block values straight into the master pixels it owns, so no block
+// ImageBlock is ever stored (the staged pair wrote and re-read 36x36 block arrays per (round, block)).
+//
+// Why the sums are the reference's. Master pixel (mx, my) receives, per round, ImageBlock::put(block) of every
+// rendered block whose (32+4)^2 array covers it, in BlockGenerator spiral order (block.cpp:125-134); the value
+// a block holds there is the sum, from +0 in getSampleIndices order (x outer, y inner), of
+// (Color4f(v) * wx) * wy over the block's samples whose footprint covers the pixel (block.cpp:93-123). With a
+// 2-pixel border and reach the footprint of the sample at image pixel (sx, sy) is exactly master columns
+// sx..sx+4 and rows sy..sy+4 (never clipped by its block array), so master pixel (mx, my) sees the samples of
+// the 5x5 window sx in [mx-4, mx], sy in [my-4, my]: those of its own block and, near a block edge, of the
+// left / upper / upper-left neighbours. A tile owns master columns [32bx, 32bx+32) (the last tile: up to the
+// master edge) and rows alike, so its windows reach samples [32bx-4, 32bx+32) x [32by-4, 32by+32): the 36x36
+// sample region staged per round -- the quadrants cx < 4 / cy < 4 belong to the neighbour blocks. Per round
+// the tile forms, for each of the (up to) four blocks in spiral order, that block's partial sum over the
+// window (samples of other blocks masked to weight 0: (v * 0) * wy = +0 added to a sum that can never be -0
+// changes nothing) and adds it to the master value held in registers; a block that does not cover the pixel
+// contributes exactly +0. The weights are those of nh_block_splat_tab_kernel (each sample's five column and
+// row weights, computed in its own block's coordinates), the products ((v * wx) * wy) the same floats.
+//
+// Work split: 512 threads, each owning a strip of 2 master rows of one column (its 2 float4 master values live
+// in registers across the rounds). Strips whose windows hold only their own block's samples (columns 4..31,
+// rows 4..31 of the tile: 392 of 512) run one unmasked pass in waves 0-5; the 120 strips at the tile's left and
+// top edges run masked passes, one per neighbour block present, in waves 6-7; master pixels past the 32x32
+// tile (the master border of the last block column / row) take a second, masked strip per thread, updated in
+// place in the framebuffer.
+constexpr int kTileThreads = 512;
+constexpr int kRgn = 36, kRgnPx = kRgn * kRgn;   // sample region of a tile, row-major (cy * 36 + cx)
+constexpr int kTV = 0, kTWX = 3, kTWY = 8, kTPlanes = 13;
+
+// One block's partial sums for a 2-row strip (column c, rows r0, r0+1 of the tile; region window columns
+// c..c+4, rows r0..r0+5). MASK: only the samples of region quadrant (xs, ys) count (xs = 0: cx < 4, the left
+// block; ys = 0: cy < 4, the upper block) and samples outside the region (master border strips) are skipped.
+template <bool MASK>
+__device__ __forceinline__ void tile_strip_pass(const float *__restrict__ W, int c, int r0, int xs, int ys, sf2 rg[2],
+                                                sf2 bw[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        rg[j] = sf2{0.f, 0.f};
+        bw[j] = sf2{0.f, 0.f};
+    }
+    // the column loop stays rolled: unrolled, the scheduler hoists all 30 samples' loads and spills
+#pragma unroll 1
+    for (int e = 0; e < 5; ++e) {  // sample column cx = c + e, x-major as getSampleIndices; its weight index 4 - e
+        const int cx = c + e;
+        const bool xin = !MASK || ((cx < 4) == (xs == 0) && cx < kRgn);
+        const int base = r0 * kRgn + cx;
+        const float *Wx = W + (kTWX + 4 - e) * kRgnPx;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {  // sample row cy = r0 + i
+            const int cy = r0 + i;
+            const bool in = !MASK || (xin && (cy < 4) == (ys == 0) && cy < kRgn);
+            const int a = MASK ? (in ? base + i * kRgn : 0) : base + i * kRgn;
+            float wx = Wx[a];
+            if (MASK) wx = in ? wx : 0.f;
+            const sf2 vrg = sf2{W[(kTV + 0) * kRgnPx + a], W[(kTV + 1) * kRgnPx + a]} * wx;
+            const sf2 vbw = sf2{W[(kTV + 2) * kRgnPx + a], 1.0f} * wx;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {  // strip row r0 + j: the sample's row weight index j + 4 - i
+                const int dy = j + 4 - i;
+                if (dy < 0 || dy > 4) continue;
+                const float wy = W[(kTWY + dy) * kRgnPx + a];
+                rg[j] += vrg * wy;
+                bw[j] += vbw * wy;
+            }
+        }
+    }
+}
+
+// One sweep of a 2-row strip's window (column c < 32, rows r0, r0+1): the running sums R (r, g) / B (b, w) take
+// the contributions of sample rows i in [I0, I1), in getSampleIndices order (columns e outer). MASKY: per lane
+// only the rows of one block -- upper (r0 + i < 4) when UPPER, own otherwise; a masked row adds (v*wx)*0 = +0
+// to sums that start at +0 and are never -0, which changes nothing. XS: at column e == xsplit (per lane: the
+// window's first own-block column) the sums so far are the left block's: they go to stash and restart from +0.
+template <bool MASKY, bool UPPER, int I0, int I1, bool XS>
+__device__ __forceinline__ void tile_sweep(const float *__restrict__ W, int c, int r0, int xsplit, float4 *stash,
+                                           sf2 R[2], sf2 B[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) R[j] = B[j] = sf2{0.f, 0.f};
+#pragma unroll 1
+    for (int e = 0; e < 5; ++e) {  // sample column cx = c + e; its weight index 4 - e
+        if (XS && e == xsplit) {   // few lanes (divergent)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                stash[j * 64] = make_float4(R[j].x, R[j].y, B[j].x, B[j].y);
+                R[j] = B[j] = sf2{0.f, 0.f};
+            }
+        }
+        const int a0 = r0 * kRgn + c + e;
+        const float *Wx = W + (kTWX + 4 - e) * kRgnPx;
+#pragma unroll
+        for (int i = I0; i < I1; ++i) {  // sample row cy = r0 + i
+            const int a = a0 + i * kRgn;
+            const float wx = Wx[a];
+            const sf2 vrg = sf2{W[(kTV + 0) * kRgnPx + a], W[(kTV + 1) * kRgnPx + a]} * wx;
+            const sf2 vbw = sf2{W[(kTV + 2) * kRgnPx + a], 1.0f} * wx;
+            const bool keep = !MASKY || ((r0 + i < 4) == UPPER);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {  // strip row r0 + j: the sample's row weight index j + 4 - i
+                const int dy = j + 4 - i;
+                if (dy < 0 || dy > 4) continue;
+                float wy = W[(kTWY + dy) * kRgnPx + a];
+                if (MASKY) wy = keep ? wy : 0.f;
+                R[j] += vrg * wy;
+                B[j] += vbw * wy;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(4))) void nh_tile_splat_kernel(SplatLaunch P) {
+    __shared__ float W[kTPlanes * kRgnPx];
+    __shared__ float tab[33];
+    __shared__ float4 stash[2 * 6 * 64];  // waves 0 / 7: partials of the UL, U, L blocks [wave][quadrant][row][lane]
+    const int tile = blockIdx.x;
+    const int by = tile / P.nbx, bx = tile - by * P.nbx;
+    const int nby = (P.height + 31) >> 5;
+    // the blocks whose samples reach this tile, by region quadrant q = xs + 2 ys: 0 upper-left, 1 upper, 2 left,
+    // 3 own; -1 = outside the image or not rendered by this context (its samples are absent: pixel_map -1)
+    // (scalars, no arrays: a runtime-indexed array would live in scratch)
+    unsigned present = 0;  // bit q: quadrant q's block is rendered
+    int rk0, rk1, rk2, rk3;
+    {
+        auto rank_of = [&](int q) {
+            const int qx = bx - 1 + (q & 1), qy = by - 1 + (q >> 1);
+            if (qx < 0 || qy < 0 || P.block_slot[qy * P.nbx + qx] < 0) return 0x7fffffff;
+            present |= 1u << q;
+            return P.block_rank[qy * P.nbx + qx];
+        };
+        rk0 = rank_of(0); rk1 = rank_of(1); rk2 = rank_of(2); rk3 = rank_of(3);
+    }
+    if (!present) return;  // whole workgroup: no rendered block reaches the tile
+    // position of each quadrant in spiral order (ties cannot occur between present blocks: ranks are distinct)
+    auto pos_of = [&](int rk, int q) {
+        return (rk0 < rk || (rk0 == rk && 0 < q)) + (rk1 < rk || (rk1 == rk && 1 < q)) +
+               (rk2 < rk || (rk2 == rk && 2 < q)) + (rk3 < rk || (rk3 == rk && 3 < q));
+    };
+    const unsigned ordp = (0u << (2 * pos_of(rk0, 0))) | (1u << (2 * pos_of(rk1, 1))) | (2u << (2 * pos_of(rk2, 2))) |
+                          (3u << (2 * pos_of(rk3, 3)));  // 2 bits per position: the quadrant added t-th
+    const int mcols = P.width + 4, mrows = P.height + 4;
+    const int ncols = bx == P.nbx - 1 ? mcols - 32 * bx : 32, nrows = by == nby - 1 ? mrows - 32 * by : 32;
+    const float r = P.radius;
+    if (threadIdx.x < 33) tab[threadIdx.x] = P.table[threadIdx.x];
+
+    // phase-1 samples of this thread: region slot t = threadIdx.x + 512 q (x fastest: neighbouring lanes load
+    // neighbouring pixels of one block row, consecutive list entries)
+    int li[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int t = threadIdx.x + kTileThreads * q;
+        const int sx = 32 * bx - 4 + t % kRgn, sy = 32 * by - 4 + t / kRgn;
+        li[q] = (t < kRgnPx && sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) ? P.pixel_map[sy * P.width + sx] : -1;
+    }
+    float4 rec[3];
+    float rjy[3];
+    auto fetch = [&](int k) {  // every slot assigned (absent: zeros), so no earlier value stays live
+        const size_t rbase = (size_t)k * P.n_list;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            rec[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            rjy[q] = 0.f;
+            if (li[q] >= 0) {
+                rec[q] = P.rec_rgbx[rbase + li[q]];
+                rjy[q] = P.rec_jy[rbase + li[q]];
+            }
+        }
+    };
+
+    // phase-2 strips: u = 0 the tile's 32x32 pixels, u = 1 the master border beyond them (last block column / row)
+    const int wave = threadIdx.x >> 6;
+    int sc[2], sr[2];
+    {
+        const int l = threadIdx.x;
+        int c, s;
+        // waves 0-6: columns 4..31 (own block in x), 28 per strip row; wave 7: columns 0..3 (x-split)
+        if (l < 448) { c = 4 + l % 28; s = l / 28; }
+        else { c = (l - 448) & 3; s = (l - 448) >> 2; }
+        sc[0] = c;
+        sr[0] = 2 * s;
+        const int nstr = (nrows + 1) >> 1, xc = max(ncols - 32, 0), n_right = xc * nstr;
+        const int n_bottom = 32 * max(nstr - 16, 0);
+        sc[1] = -1;
+        sr[1] = 0;
+        if (l < n_right) { sc[1] = 32 + l % xc; sr[1] = 2 * (l / xc); }
+        else if (l < n_right + n_bottom) { sc[1] = (l - n_right) & 31; sr[1] = 2 * (16 + ((l - n_right) >> 5)); }
+    }
+    const bool ring = __any(sc[1] >= 0);  // any master-border strip in this wave
+    // master values of the tile strip in registers across the rounds; a border strip (few, edge tiles only) is
+    // updated in place in the framebuffer each round (same thread, program order)
+    float4 m[2];
+    float4 *const fb4 = reinterpret_cast<float4 *>(P.fb);
+    auto fb_at = [&](int c, int row) -> float4 * { return fb4 + (size_t)(32 * by + row) * mcols + 32 * bx + c; };
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+        m[j] = (sc[0] < ncols && sr[0] + j < nrows) ? *fb_at(sc[0], sr[0] + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+
+    fetch(0);
+    for (int k = 0; k < P.n_rounds; ++k) {
+        __syncthreads();  // the previous round's phase 2 is done with W (and tab is in place)
+        auto stage = [&](const int q) {
+            if (P.debug & 1) return;
+            const int t = threadIdx.x + kTileThreads * q;
+            const int cx = t % kRgn, cy = t / kRgn;
+            const int sx = 32 * bx - 4 + cx, sy = 32 * by - 4 + cy;
+            const int lx = sx & 31, ly = sy & 31, ox = sx - lx, oy = sy - ly;  // the sample's own block
+            float v[3] = {0.f, 0.f, 0.f}, wx[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, wy[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+            if (li[q] >= 0 && is_valid(f3(rec[q].x, rec[q].y, rec[q].z))) {  // invalid samples drop with their weight
+                const float spx = (float)(ox + lx) + rec[q].w, spy = (float)(oy + ly) + rjy[q];
+                const float px = spx - 0.5f - (float)(ox - 2), py = spy - 0.5f - (float)(oy - 2);
+                const int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
+                const int x1 = min((int)floorf(px + r), 35), y1 = min((int)floorf(py + r), 35);
+#pragma unroll
+                for (int d = 0; d < 5; ++d) {
+                    const int xc = lx + d, yc = ly + d;  // block-array column / row = master column sx + d / row sy + d
+                    if (xc >= x0 && xc <= x1) wx[d] = tab[(int)(fabsf((float)xc - px) * P.lookup)];
+                    if (yc >= y0 && yc <= y1) wy[d] = tab[(int)(fabsf((float)yc - py) * P.lookup)];
+                }
+                v[0] = rec[q].x; v[1] = rec[q].y; v[2] = rec[q].z;
+            }
+            const int j = cy * kRgn + cx;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) W[(kTV + ch) * kRgnPx + j] = v[ch];
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {
+                W[(kTWX + d) * kRgnPx + j] = wx[d];
+                W[(kTWY + d) * kRgnPx + j] = wy[d];
+            }
+        };
+        stage(0);
+        stage(1);
+        if (threadIdx.x + 2 * kTileThreads < kRgnPx) stage(2);
+        __syncthreads();
+        // next round's records in flight during phase 2 (waves with master-border strips fetch them after their
+        // extra passes: the records' registers and the border passes' would not fit together)
+        if (!ring && k + 1 < P.n_rounds && !(P.debug & 4)) fetch(k + 1);
+        if (!(P.debug & 2)) {
+            // Each block's partial sums, then master += each present block's partial in spiral order. Waves 1-6:
+            // one unmasked sweep (own block only). Wave 0 (top rows) and wave 7 (left columns): a sweep of the upper
+            // block's rows, then one of the own block's rows; wave 7's sweeps hand their left-block parts (UL, L) to
+            // the stash at the column where the window enters the own block. Partials other than the own block's
+            // wait in the LDS stash (registers).
+            const int xsplit = (sc[0] < 4 && (present & 5u)) ? 4 - sc[0] : -1;  // left-block columns: e < 4 - c
+            float4 *st = stash + (wave == 7 ? 6 * 64 : 0) + (threadIdx.x & 63);  // [quadrant UL, U, L][row][lane]
+            sf2 R[2], B[2];
+            if (wave == 7 || wave == 0) {
+                if (wave == 7) tile_sweep<true, true, 0, 4, true>(W, sc[0], sr[0], xsplit, st, R, B);
+                else tile_sweep<true, true, 0, 4, false>(W, sc[0], sr[0], -1, st, R, B);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) st[(2 + j) * 64] = make_float4(R[j].x, R[j].y, B[j].x, B[j].y);
+                if (wave == 7) tile_sweep<true, false, 0, 6, true>(W, sc[0], sr[0], xsplit, st + 4 * 64, R, B);
+                else tile_sweep<true, false, 0, 6, false>(W, sc[0], sr[0], -1, st, R, B);
+            } else {
+                tile_sweep<false, false, 0, 6, false>(W, sc[0], sr[0], -1, st, R, B);
+            }
+#pragma unroll 1
+            for (int t = 0; t < 4; ++t) {
+                const int q = (int)(ordp >> (2 * t)) & 3;
+                if (!((present >> q) & 1u)) continue;  // absent: its partial is +0
+                if (q != 3 && wave != 7 && (q != 1 || wave != 0)) continue;  // no strip of this wave reaches it
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    float4 pv;
+                    if (q == 3) pv = make_float4(R[j].x, R[j].y, B[j].x, B[j].y);
+                    else if (q == 1) pv = st[(2 + j) * 64];
+                    else pv = xsplit > 0 ? st[((q == 0 ? 0 : 4) + j) * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    m[j].x += pv.x;
+                    m[j].y += pv.y;
+                    m[j].z += pv.z;
+                    m[j].w += pv.w;
+                }
+            }
+        }
+        if (ring && !(P.debug & 8)) {  // master border strips of the last block column / row, in place in the framebuffer
+#pragma unroll 1
+            for (int t = 0; t < 4; ++t) {
+                const int q = (int)(ordp >> (2 * t)) & 3;
+                if (!((present >> q) & 1u)) continue;
+                const int xs = q & 1, ys = q >> 1;
+                if ((xs == 0 && !__any(sc[1] >= 0 && sc[1] < 4)) || (ys == 0 && !__any(sc[1] >= 0 && sr[1] < 4))) continue;
+                if (sc[1] < 0) continue;
+                sf2 rg[2], bw[2];
+                tile_strip_pass<true>(W, sc[1], sr[1], xs, ys, rg, bw);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    if (sc[1] >= ncols || sr[1] + j >= nrows) continue;
+                    float4 *mp = fb_at(sc[1], sr[1] + j);
+                    float4 mv = *mp;
+                    mv.x += rg[j].x;
+                    mv.y += rg[j].y;
+                    mv.z += bw[j].x;
+                    mv.w += bw[j].y;
+                    *mp = mv;
+                }
+            }
+            if (k + 1 < P.n_rounds) fetch(k + 1);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+        if (sc[0] < ncols && sr[0] + j < nrows) *fb_at(sc[0], sr[0] + j) = m[j];
+}
+
+// Rendered blocks whose merged region ((sx+2b) x (sy+2b) at offset (ox, oy) in master coordinates)
+// covers master pixel (mx, my), in BlockGenerator spiral order: the order ImageBlock::put(ImageBlock&)
+// adds them (src/utils/block.cpp:125-134). Returns their number (<= 4) and slots.
+__device__ __forceinline__ int covering_blocks(const SplatLaunch &P, int mx, int my, int *slot) {
+    const int cols = 32 + 2 * P.border;
+    int blk[4], nb = 0;
+    const int bx_lo = max((mx - cols + 1 + 31) >> 5, 0), bx_hi = min(mx >> 5, P.nbx - 1);
+    const int nby = (P.height + 31) >> 5;
+    const int by_lo = max((my - cols + 1 + 31) >> 5, 0), by_hi = min(my >> 5, nby - 1);
+    for (int by = by_lo; by <= by_hi; ++by)
+        for (int bx = bx_lo; bx <= bx_hi; ++bx) {
+            const int bid = by * P.nbx + bx;
+            const int sl = P.block_slot[bid];
+            if (sl < 0) continue;
+            const int ox = bx * 32, oy = by * 32;
+            const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+            if (mx - ox >= sxb + 2 * P.border || my - oy >= syb + 2 * P.border) continue;
+            blk[nb] = bid;
+            slot[nb] = sl;
+            ++nb;
+        }
+    for (int a = 1; a < nb; ++a)
+        for (int b = a; b > 0 && P.block_rank[blk[b]] < P.block_rank[blk[b - 1]]; --b) {
+            int t = blk[b]; blk[b] = blk[b - 1]; blk[b - 1] = t;
+            t = slot[b]; slot[b] = slot[b - 1]; slot[b - 1] = t;
+        }
+    return nb;
+}
+
+// ImageBlock::put(ImageBlock&) into the master (src/utils/block.cpp:125-134): per master
+// pixel, per round, the overlapping rendered blocks in BlockGenerator spiral order.
+__global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
+    const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
+    const int mx = blockIdx.x * 16 + (threadIdx.x & 15), my = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (mx >= mcols || my >= mrows) return;
+    const int cols = 32 + 2 * P.border;
+    int slot[4];
+    const int nb = covering_blocks(P, mx, my, slot);
+    if (nb == 0) return;
+    int off[4];
+    for (int q = 0; q < nb; ++q) {
+        const int bid = P.blocks[slot[q]];
+        const int by = bid / P.nbx, bx = bid - by * P.nbx;
+        off[q] = (my - by * 32) * cols + (mx - bx * 32);
+    }
+    float4 *mp = reinterpret_cast<float4 *>(P.fb) + (size_t)my * mcols + mx;
+    float4 m = *mp;
+    const size_t per_round = (size_t)P.n_blocks * (size_t)(cols * cols);
+    for (int k = 0; k < P.n_rounds; ++k) {
+        const float4 *base = P.staging + (size_t)k * per_round;
+        for (int q = 0; q < nb; ++q) {
+            const float4 v = base[(size_t)slot[q] * (cols * cols) + off[q]];
+            m.x += v.x;
+            m.y += v.y;
+            m.z += v.z;
+            m.w += v.w;
+        }
+    }
+    *mp = m;
+}
+
+// invalid-sample count (ImageBlock::put drops, block.cpp:94-99)
+__global__ __launch_bounds__(256) void nh_count_invalid_kernel(const float4 *rec, size_t n, unsigned long long *out) {
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    unsigned long long c = 0;
+    if (i < n) {
+        float4 v = rec[i];
+        c = is_valid(f3(v.x, v.y, v.z)) ? 0 : 1;
+    }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(stat_shard(out) + 4, c);
+}
+
+}  // namespace
+
+namespace nh {
+
+// A/B knobs, read per launch (one per chunk) so a process can switch them: NH_SPLAT_FUSED=1 -> the fused tile
+// splat (below); NH_SPLAT_TAB=0 -> the staged pair's column-strip splat, NH_SPLAT_STRIP=0 -> one pixel per thread
+static bool splat_knob(const char *name) {
+    const char *e = std::getenv(name);
+    return !e || e[0] != '0';
+}
+
+// The fused tile splat is bit-identical but slower than the staged pair (0.485 vs 0.275 + 0.100 ms per C2 chunk,
+// rocprofv3, one pool): its 16 rounds per tile are a serial chain of record fetches (0.245 ms with both phases
+// skipped) and the left / top edge strips lengthen each round. Opt-in: NH_SPLAT_FUSED=1.
+bool splat_uses_staging(int border, int reach) {
+    const char *e = std::getenv("NH_SPLAT_FUSED");
+    return !(e && e[0] == '1' && border == 2 && reach == 2);
+}
+
+void launch_splat(const SplatLaunch &P, hipStream_t st) {
+    const bool tabulated = splat_knob("NH_SPLAT_TAB"), strip = splat_knob("NH_SPLAT_STRIP");
+    if (!splat_uses_staging(P.border, P.reach)) {  // splat + merge in one pass, no block staging
+        const int n_tiles = P.nbx * ((P.height + 31) / 32);
+        SplatLaunch Q = P;
+        if (const char *e = std::getenv("NH_SPLAT_DEBUG")) Q.debug = std::atoi(e);
+        static bool told = false;
+        if (!told && std::getenv("NH_SPLAT_OCC")) {
+            told = true;
+            int a = 0, b = 0;
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, nh_tile_splat_kernel, kTileThreads, 0);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, nh_block_splat_tab_kernel, 256, 0);
+            std::fprintf(stderr, "[nh] workgroups per CU: tile splat %d, tab splat %d\n", a, b);
+        }
+        hipLaunchKernelGGL(nh_tile_splat_kernel, dim3(n_tiles), dim3(kTileThreads), 0, st, Q);
+        return;
+    }
+    if (tabulated && P.border == 2 && P.reach == 2)
+        hipLaunchKernelGGL(nh_block_splat_tab_kernel, dim3(P.n_blocks, (P.n_rounds + kTabRounds - 1) / kTabRounds),
+                           dim3(256), 0, st, P);
+    else if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
+    else hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
+    const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
+    dim3 grid((mcols + 15) / 16, (mrows + 15) / 16);
+    hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, P);
+}
+
+void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st) {
+    if (n == 0) return;
+    dim3 grid((unsigned)((n + 255) / 256));
+    hipLaunchKernelGGL(nh_count_invalid_kernel, grid, dim3(256), 0, st, rec, n, out);
+}
+
+}  // namespace nh

@@ -1048,10 +1048,12 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScen
 }
 
 // the chunk's last paths (RR-ahead state) finished in place, one thread per path, as wf_tail
-template <bool ORDERED, bool STATS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAVES))) void wf_tail_rr(
+// TB: threads per workgroup. A tail workgroup keeps its LDS (stacks + scene copy) until its longest path ends
+// (~1000 specular bounces), so 64-thread workgroups pin a quarter of what 256-thread ones do.
+template <bool ORDERED, bool STATS, int TB>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAVES))) void wf_tail_rr(
     const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
-    __shared__ uint32_t stk[16 * 256];
+    __shared__ uint32_t stk[16 * TB];
     extern __shared__ float4 lds_scene[];
     const DScene &S = *Sp;
     const Traversal tv = stage_small_scene<true>(tv_g, L, lds_scene);
@@ -1059,19 +1061,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAV
     const WfBuf &B = L.st.buf[L.in_q];
     TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
     unsigned long long q_e = 0, q_s = 0;
-    for (int q = blockIdx.x * 256 + threadIdx.x; q < qv.n; q += gridDim.x * 256) {
+    for (int q = blockIdx.x * TB + threadIdx.x; q < qv.n; q += gridDim.x * TB) {
         const int s = queue_slot(qv.pre, L.seg_cap, q);
         PathV v;
         Hit h;
         Its its;
         load_post_head(S, tv, L, B, s, v, h, its);
-        while (rr_step<ORDERED, STATS>(S, tv, L, v, its, h, stk + threadIdx.x, 256, st_e, st_s, q_e, q_s)) {
+        while (rr_step<ORDERED, STATS>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s, q_e, q_s)) {
         }
     }
     if (STATS) {  // the tail's own counter slots (kStatTail*), so stage rates stay per kernel
         flush_trav_stats(stat_shard(L.counters) + kStatTail, q_e, st_e);
         flush_trav_stats(stat_shard(L.counters) + kStatTailAny, q_s, st_s);
     }
+}
+
+// Asynchronous tail hand-off: the chunk's live paths (RR-ahead state, 88 B each) are copied into a small buffer
+// of their own, densely from slot 0 (all in count shard 0; the other shards and groups are zeroed by the host),
+// so the pool's path state is free for the next chunk while this chunk's tail kernel runs on another stream.
+__global__ __launch_bounds__(256) void wf_pack_rr(WfLaunch L, WfBuf dst, unsigned *dst_counts) {
+    const QView qv = queue_view(L.cnt_in);
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q == 0) dst_counts[0] = (unsigned)qv.n;
+    if (q >= qv.n) return;
+    const WfBuf &B = L.st.buf[L.in_q];
+    const int s = queue_slot(qv.pre, L.seg_cap, q);
+    dst.ray_o[q] = B.ray_o[s];
+    dst.ray_d[q] = B.ray_d[s];
+    dst.li[q] = B.li[s];
+    dst.thr[q] = B.thr[s];
+    dst.rng[q] = B.rng[s];
+    dst.hit[q] = B.hit[s];
 }
 
 // Tail of a chunk: once few paths are alive, per-bounce launches cost more than the work they
@@ -1249,12 +1269,22 @@ void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L
 
 void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
                        hipStream_t st) {
-    const dim3 grid(std::min(std::max(1, (bound + 255) / 256), kTraceBlocksMax));
+    const char *e = std::getenv("NH_TAIL_WG");  // threads per tail workgroup: 64 (default) or 256
+    const int tb = e && std::atoi(e) == 256 ? 256 : 64;
+    const dim3 grid(std::min(std::max(1, (bound + tb - 1) / tb), kTraceBlocksMax));
     const size_t lds = 16 * ((size_t)small_pairs_offset_f4(L) + (size_t)kPairF4 * (L.small_prims / 3));
-#define NH_TR(O, T) hipLaunchKernelGGL((wf_tail_rr<O, T>), grid, dim3(256), lds, st, S, tv, L)
+#define NH_TR(O, T)                                                                                 \
+    do {                                                                                            \
+        if (tb == 256) hipLaunchKernelGGL((wf_tail_rr<O, T, 256>), grid, dim3(256), lds, st, S, tv, L); \
+        else hipLaunchKernelGGL((wf_tail_rr<O, T, 64>), grid, dim3(64), lds, st, S, tv, L);          \
+    } while (0)
     if (ordered) { if (stats) NH_TR(true, true); else NH_TR(true, false); }
     else { if (stats) NH_TR(false, true); else NH_TR(false, false); }
 #undef NH_TR
+}
+
+void launch_wf_pack_rr(const WfLaunch &L, const WfBuf &dst, unsigned *dst_counts, int bound, hipStream_t st) {
+    hipLaunchKernelGGL(wf_pack_rr, dim3(std::max(1, (bound + 255) / 256)), dim3(256), 0, st, L, dst, dst_counts);
 }
 
 void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, bool sort, int bound, hipStream_t st) {

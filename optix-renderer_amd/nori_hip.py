@@ -159,7 +159,7 @@ class nh_render_stats(C.Structure):
         (n, C.c_uint64) for n in ("tail_queries", "tail_nodes_visited", "tail_boxes_tested", "tail_prims_tested",
                                   "tail_shadow_queries", "tail_shadow_nodes_visited", "tail_shadow_boxes_tested",
                                   "tail_shadow_prims_tested", "lds_scene", "fused_bounce", "comm_inits")] + [
-        ("kernel_ms_denoise", C.c_double), ("launches_denoise", C.c_uint64)]
+        ("kernel_ms_denoise", C.c_double), ("launches_denoise", C.c_uint64), ("tails_async", C.c_uint64)]
 
 
 def _sig(name, res, *args):

@@ -8,7 +8,7 @@ for i in $(seq 1 $n); do
   for cfg in $cfgs; do
     for v in $vars; do
       log=gpurun_out/abe_${cfg}_${v}_$i.log
-      env $v timeout -k 10 300 python bench.py --config $cfg --no-cpu --no-denoise --traversal-1m-steps 0 "$@" > $log 2>&1 || { echo "fail $cfg $v"; tail -5 $log; exit 99; }
+      env ${v//,/ } timeout -k 10 300 python bench.py --config $cfg --no-cpu --no-denoise --traversal-1m-steps 0 "$@" > $log 2>&1 || { echo "fail $cfg $v"; tail -5 $log; exit 99; }
       python3 -c "
 import json
 l=json.loads([x for x in open('$log') if x.startswith('{')][0]); r=l['roofline'] or {}

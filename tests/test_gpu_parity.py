@@ -214,6 +214,37 @@ def test_render_deterministic_and_sharded(gpu, tmp_path):
     assert rel_l2(ctx.framebuffer(), full) < 1e-6
 
 
+@pytest.mark.parametrize("res,spp,blocks", [((100, 70), 6, None), ((33, 31), 4, None), ((200, 40), 5, [0, 2, 3, 5, 6, 9, 11]),
+                                            ((64, 64), 3, [1, 2]), ((96, 96), 2, [4])])
+def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, spp, blocks):
+    """The fused splat + merge (NH_SPLAT_FUSED=1: one workgroup per master tile, rounds in order, blocks in spiral
+    order, no staging) gives the staged splat + merge pair's framebuffer bit for bit, and the oracle's: partial blocks and the master
+    border of the last block column / row (100x70, 33x31), block subsets whose neighbours are absent (every tile
+    quadrant case), several chunks (1 MiB path budget) and both render modes."""
+    xml = scenegen.cbox_xml(str(tmp_path), "c2")
+    s = nh.Scene(xml)
+    s.set_resolution(*res)
+    b = nh.Bvh(s)
+    out = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("NH_SPLAT_FUSED", fused)
+        for mode in (nh.MODE_MEGAKERNEL, nh.MODE_WAVEFRONT):
+            for budget in (None, "1"):
+                if budget:
+                    monkeypatch.setenv("NH_WF_BUDGET_MB", budget)
+                    monkeypatch.setenv("NH_RECORD_BUDGET_MB", budget)
+                ctx = nh.Context(0)
+                ctx.upload(s, b)
+                ctx.render(0, spp, seed=21, clear=True, mode=mode, blocks=blocks)
+                out[(fused, mode, budget)] = ctx.framebuffer()
+                monkeypatch.delenv("NH_WF_BUDGET_MB", raising=False)
+                monkeypatch.delenv("NH_RECORD_BUDGET_MB", raising=False)
+    ref = no.OracleScene(s).render(0, spp, seed=21, blocks=blocks)
+    assert np.abs(ref).sum() > 0
+    for k, g in out.items():
+        np.testing.assert_array_equal(g, ref, err_msg=str(k))
+
+
 def test_wavefront_matches_megakernel(gpu, tmp_path, monkeypatch):
     """Same per-path random streams and arithmetic: the two schedules give bitwise-equal
     framebuffers and identical traversal work, also when the wavefront splits the rounds into
@@ -419,6 +450,37 @@ def test_pipelined_chunks_match_one_pool(gpu, tmp_path, monkeypatch):
     np.testing.assert_array_equal(out[0], out[1])
     r = no.OracleScene(s).render(0, 12, seed=9)
     assert rel_l2(out[0], r) < TOL_REL_L2
+
+
+def test_async_tails_match_in_place(gpu, tmp_path, monkeypatch):
+    """Chunk tails handed off to tail slots (the live paths packed into the slot's buffer, the tail kernel and
+    splat on the slot's stream, the pool taking the next chunk meanwhile) give the in-place tails' and the
+    one-pool framebuffer bit for bit, over several calls of several chunks each; the hand-offs are counted."""
+    xml = scenegen.cbox_xml(str(tmp_path), "c1")
+    s = nh.Scene(xml)
+    s.set_resolution(160, 128)
+    b = nh.Bvh(s)
+    monkeypatch.setenv("NH_WF_BUDGET_MB", "16")  # 2-3 rounds per chunk
+    out = []
+    for knobs in ({}, {"NH_POOLS": "2"}, {"NH_TAIL_ASYNC": "0"}, {"NH_POOLS": "1"}):
+        for k, v in knobs.items():
+            monkeypatch.setenv(k, v)
+        ctx = nh.Context(0)
+        ctx.upload(s, b)
+        ctx.render(0, 0, clear=True, mode=nh.MODE_WAVEFRONT)
+        for s0 in range(0, 24, 8):
+            ctx.render(s0, s0 + 8, seed=4, traversal=nh.TRAVERSAL_ORDERED, mode=nh.MODE_WAVEFRONT)
+        ctx.synchronize()
+        out.append((ctx.framebuffer(), ctx.stats()))
+        for k in knobs:
+            monkeypatch.delenv(k)
+    assert out[0][1]["tails_async"] > 3 and out[1][1]["tails_async"] > 3
+    assert out[2][1]["tails_async"] == 0 and out[3][1]["tails_async"] == 0
+    assert out[0][1]["launches_splat"] > 6
+    for fb, _ in out[1:]:
+        np.testing.assert_array_equal(out[0][0], fb)
+    r = no.OracleScene(s).render(0, 24, seed=4)
+    assert rel_l2(out[0][0], r) < TOL_REL_L2
 
 
 def test_fast_reciprocal_exhaustive(gpu):
