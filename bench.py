@@ -404,6 +404,8 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
     if args.dump_framebuffer and rank == 0:
         np.save(args.dump_framebuffer, reduced if reduced is not None else ctx.framebuffer())
     st = ctx.stats()
+    # chunks of the timed steps and how many of their tails ran decoupled from their path pool (tail slots)
+    chunks = {"chunks": int(st["launches_splat"]), "tails_async": int(st["tails_async"])}
     roof_pass = None
     if a.mode == "wavefront" and a.pools != 1 and calib is not None and a.roofline_steps > 0:
         pools_env = os.environ.get("NH_POOLS")
@@ -428,7 +430,7 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
         roof = roofline(a, calib, st, W, H, R)
         roof["timed"] = roof_pass or "the timed region"
     return {"scene": scene, "W": W, "H": H, "R": R, "desc": scene_desc, "elapsed": elapsed, "samples": samples,
-            "roof": roof, "bvh_s": bvh_s, "upload_s": upload_s, "ctx": ctx}
+            "roof": roof, "bvh_s": bvh_s, "upload_s": upload_s, "ctx": ctx, "chunks": chunks}
 
 
 def reduce_framebuffer(ctx, dist, args, local, rank):
@@ -618,7 +620,8 @@ def main():
                        "pools": args.pools or int(os.environ.get("NH_POOLS", "0")) or "library default (2)",
                        "parallelism": (f"{par} + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce"
                                        if world > 1 else "single GPU"),
-                       "bvh_build_s": round(r["bvh_s"], 3), "upload_s": round(r["upload_s"], 3)},
+                       "bvh_build_s": round(r["bvh_s"], 3), "upload_s": round(r["upload_s"], 3),
+                       "timed_chunks": r["chunks"]},
             "roofline": roof,
             "traversal": traversal_record(roof) if roof else None,
             "traversal_1m": t1m,

@@ -626,7 +626,21 @@ __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
     float4 *mp = reinterpret_cast<float4 *>(P.fb) + (size_t)my * mcols + mx;
     float4 m = *mp;
     const size_t per_round = (size_t)P.n_blocks * (size_t)(cols * cols);
-    for (int k = 0; k < P.n_rounds; ++k) {
+    int k = 0;
+    if (nb == 1) {  // one covering block (most pixels): four rounds' loads in flight, added in round order
+        const float4 *src = P.staging + (size_t)slot[0] * (cols * cols) + off[0];
+        for (; k + 4 <= P.n_rounds; k += 4) {
+            const float4 v0 = src[(size_t)k * per_round], v1 = src[(size_t)(k + 1) * per_round],
+                         v2 = src[(size_t)(k + 2) * per_round], v3 = src[(size_t)(k + 3) * per_round];
+            for (const float4 &v : {v0, v1, v2, v3}) {
+                m.x += v.x;
+                m.y += v.y;
+                m.z += v.z;
+                m.w += v.w;
+            }
+        }
+    }
+    for (; k < P.n_rounds; ++k) {
         const float4 *base = P.staging + (size_t)k * per_round;
         for (int q = 0; q < nb; ++q) {
             const float4 v = base[(size_t)slot[q] * (cols * cols) + off[q]];
