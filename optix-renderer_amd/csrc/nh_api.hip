@@ -889,6 +889,12 @@ static int active_pools(const nh_ctx *c) {
     return std::max(1, std::min(kPools, np ? std::atoi(np) : def));
 }
 
+// asynchronous tails: NH_TAIL_ASYNC=1 (default off until measured faster than in-place tails)
+static bool tail_async_enabled() {
+    const char *e = std::getenv("NH_TAIL_ASYNC");
+    return e && e[0] == '1';
+}
+
 // start job j on idle pool p: buffers, traversal choice, initial queue (all n_paths camera paths)
 static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     const int n_paths = j.rounds * c->n_list;
@@ -905,7 +911,7 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
     // so do the idle tail slots' record and staging buffers: chunks hand theirs over at a tail hand-off and take the
     // slot's, and a pool that had to grow them later would free and allocate inside the pipeline (hipFree waits
     // for the whole device: a 6-9 ms stall behind the running tails)
-    if (active_pools(c) > 1)
+    if (active_pools(c) > 1 && tail_async_enabled())
         for (int i = kPools; i < kPools + kTails; ++i) {
             WfPool &o = c->pools[i];
             if (o.state != WfPool::IDLE) continue;
@@ -1030,11 +1036,10 @@ static void chunk_swap(WfPool &a, WfPool &b) {
 }
 
 // an idle tail slot for pool p's chunk, or null: the tail then runs in place on the pool's stream. Off with one
-// pool (the serialized roofline pass: kernels alone on the GPU) and with NH_TAIL_ASYNC=0.
+// pool (the serialized roofline pass: kernels alone on the GPU) and unless NH_TAIL_ASYNC=1.
 static WfPool *free_tail_slot(nh_ctx *c, const WfPool &p, int bound) {
     if (!p.rr || bound > kTailCap || active_pools(c) < 2) return nullptr;
-    if (const char *e = std::getenv("NH_TAIL_ASYNC"))
-        if (e[0] == '0') return nullptr;
+    if (!tail_async_enabled()) return nullptr;
     for (int i = kPools; i < kPools + kTails; ++i)
         if (c->pools[i].state == WfPool::IDLE) return &c->pools[i];
     return nullptr;

@@ -462,7 +462,7 @@ def test_async_tails_match_in_place(gpu, tmp_path, monkeypatch):
     b = nh.Bvh(s)
     monkeypatch.setenv("NH_WF_BUDGET_MB", "16")  # 2-3 rounds per chunk
     out = []
-    for knobs in ({}, {"NH_POOLS": "2"}, {"NH_TAIL_ASYNC": "0"}, {"NH_POOLS": "1"}):
+    for knobs in ({"NH_TAIL_ASYNC": "1"}, {"NH_TAIL_ASYNC": "1", "NH_POOLS": "2"}, {}, {"NH_POOLS": "1"}):
         for k, v in knobs.items():
             monkeypatch.setenv(k, v)
         ctx = nh.Context(0)
