@@ -1050,8 +1050,11 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScen
 // the chunk's last paths (RR-ahead state) finished in place, one thread per path, as wf_tail
 // TB: threads per workgroup. A tail workgroup keeps its LDS (stacks + scene copy) until its longest path ends
 // (~1000 specular bounces), so 64-thread workgroups pin a quarter of what 256-thread ones do.
-template <bool ORDERED, bool STATS, int TB>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAVES))) void wf_tail_rr(
+// W: waves per SIMD the registers must allow. W = 1 (240-255 VGPRs) holds half a SIMD's register file per tail
+// wave for the tail's whole length, which halves the occupancy of the next chunks' bounce kernels (128 VGPRs)
+// beside it; W = 4 (the bounce kernel's budget) leaves them their 4 waves.
+template <bool ORDERED, bool STATS, int TB, int W>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf_tail_rr(
     const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[16 * TB];
     extern __shared__ float4 lds_scene[];
@@ -1271,12 +1274,15 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
                        hipStream_t st) {
     const char *e = std::getenv("NH_TAIL_WG");  // threads per tail workgroup: 64 (default) or 256
     const int tb = e && std::atoi(e) == 256 ? 256 : 64;
+    const char *w = std::getenv("NH_TAIL_RR_WAVES");  // register budget: 4 waves/SIMD (default) or 1
+    const bool w1 = w && std::atoi(w) == 1;
     const dim3 grid(std::min(std::max(1, (bound + tb - 1) / tb), kTraceBlocksMax));
     const size_t lds = 16 * ((size_t)small_pairs_offset_f4(L) + (size_t)kPairF4 * (L.small_prims / 3));
-#define NH_TR(O, T)                                                                                 \
-    do {                                                                                            \
-        if (tb == 256) hipLaunchKernelGGL((wf_tail_rr<O, T, 256>), grid, dim3(256), lds, st, S, tv, L); \
-        else hipLaunchKernelGGL((wf_tail_rr<O, T, 64>), grid, dim3(64), lds, st, S, tv, L);          \
+#define NH_TR(O, T)                                                                                         \
+    do {                                                                                                    \
+        if (tb == 256) hipLaunchKernelGGL((wf_tail_rr<O, T, 256, 1>), grid, dim3(256), lds, st, S, tv, L);      \
+        else if (w1) hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 1>), grid, dim3(64), lds, st, S, tv, L);         \
+        else hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 4>), grid, dim3(64), lds, st, S, tv, L);                 \
     } while (0)
     if (ordered) { if (stats) NH_TR(true, true); else NH_TR(true, false); }
     else { if (stats) NH_TR(false, true); else NH_TR(false, false); }
