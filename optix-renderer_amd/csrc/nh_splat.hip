@@ -155,6 +155,35 @@ __global__ __launch_bounds__(256) void nh_block_splat_strip_kernel(SplatLaunch P
     }
 }
 
+// Rendered blocks whose merged region ((sx+2b) x (sy+2b) at offset (ox, oy) in master coordinates)
+// covers master pixel (mx, my), in BlockGenerator spiral order: the order ImageBlock::put(ImageBlock&)
+// adds them (src/utils/block.cpp:125-134). Returns their number (<= 4) and slots.
+__device__ __forceinline__ int covering_blocks(const SplatLaunch &P, int mx, int my, int *slot) {
+    const int cols = 32 + 2 * P.border;
+    int blk[4], nb = 0;
+    const int bx_lo = max((mx - cols + 1 + 31) >> 5, 0), bx_hi = min(mx >> 5, P.nbx - 1);
+    const int nby = (P.height + 31) >> 5;
+    const int by_lo = max((my - cols + 1 + 31) >> 5, 0), by_hi = min(my >> 5, nby - 1);
+    for (int by = by_lo; by <= by_hi; ++by)
+        for (int bx = bx_lo; bx <= bx_hi; ++bx) {
+            const int bid = by * P.nbx + bx;
+            const int sl = P.block_slot[bid];
+            if (sl < 0) continue;
+            const int ox = bx * 32, oy = by * 32;
+            const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
+            if (mx - ox >= sxb + 2 * P.border || my - oy >= syb + 2 * P.border) continue;
+            blk[nb] = bid;
+            slot[nb] = sl;
+            ++nb;
+        }
+    for (int a = 1; a < nb; ++a)
+        for (int b = a; b > 0 && P.block_rank[blk[b]] < P.block_rank[blk[b - 1]]; --b) {
+            int t = blk[b]; blk[b] = blk[b - 1]; blk[b - 1] = t;
+            t = slot[b]; slot[b] = slot[b - 1]; slot[b - 1] = t;
+        }
+    return nb;
+}
+
 // Block splat for the 2-pixel border (filter radius in (1.5, 2.5): Nori's default Gaussian, Mitchell-Netravali),
 // where a sample at block pixel (lx, ly) can only reach block-array columns lx..lx+4 and rows ly..ly+4.
 // Phase 1 tabulates each sample's filter weights for those five columns and rows -- wx[d] = the reference's
@@ -169,6 +198,11 @@ constexpr int kTabRounds = 4;
 constexpr int kTabRow = 33;                 // plane row: lx 0..31 + a zero column (lx outside 0..31)
 constexpr int kTabPlane = 40 * kTabRow;     // rows ly = -4..35 (ly + 4): 4 zero rows either side
 constexpr int kTabV = 0, kTabWX = 3, kTabWY = 8, kTabPlanes = 13;
+// DIRECT: one workgroup walks all the chunk's rounds of its block, and block-array pixels whose master pixel no
+// other rendered block covers (the block's 28x28 interior, and the master border of edge blocks) add each round's
+// value straight into the master in round order -- the merge's sum for a pixel with one covering block -- so only
+// the pixels shared with neighbouring blocks go through the staging buffer and nh_merge_kernel.
+template <bool DIRECT>
 __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
     __shared__ float W[kTabPlanes * kTabPlane];
     __shared__ float tab[33];
@@ -177,7 +211,7 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
     const int by = bid / P.nbx, bx = bid - by * P.nbx;
     const int ox = bx * 32, oy = by * 32;
     const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    const int k0 = blockIdx.y * kTabRounds, k1 = min(k0 + kTabRounds, P.n_rounds);
+    const int k0 = DIRECT ? 0 : blockIdx.y * kTabRounds, k1 = DIRECT ? P.n_rounds : min(k0 + kTabRounds, P.n_rounds);
     const float r = P.radius;
     if (threadIdx.x < 33) tab[threadIdx.x] = P.table[threadIdx.x];
     // the zero rows and column are never written again
@@ -211,6 +245,21 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
     fetch(k0);
     // phase-2 strip of this thread: block-array column xt, rows yt0..yt0+5
     const int seg = threadIdx.x / 36, xt = threadIdx.x - seg * 36, yt0 = seg * kStripRows;
+    const int mcols = P.width + 4, mrows = P.height + 4;
+    bool own[kStripRows];
+    float4 m[kStripRows];
+    float4 *const fb4 = reinterpret_cast<float4 *>(P.fb);
+#pragma unroll
+    for (int j = 0; j < kStripRows; ++j) {
+        own[j] = false;
+        m[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (DIRECT && threadIdx.x < 36 * 6) {
+            const int mx = ox + xt, my = oy + yt0 + j;  // block-array position -> master pixel
+            int sl[4];
+            own[j] = mx < mcols && my < mrows && covering_blocks(P, mx, my, sl) == 1 && sl[0] == slot;
+            if (own[j]) m[j] = fb4[(size_t)my * mcols + mx];
+        }
+    }
     for (int k = k0; k < k1; ++k) {
         __syncthreads();  // the previous round's phase 2 is done with W (and tab / zero rows are in place)
 #pragma unroll
@@ -248,7 +297,8 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
                 rg[j] = sf2{0.f, 0.f};
                 bw[j] = sf2{0.f, 0.f};
             }
-#pragma unroll
+            // (DIRECT keeps this loop rolled: unrolled, the hoisted loads and the master values spill)
+#pragma unroll DIRECT ? 1 : 5
             for (int e = 0; e < 5; ++e) {  // sample column lx = xt - 4 + e: the pixel is its column offset 4 - e
                 const int lx = xt - 4 + e;
                 const float *base = W + yt0 * kTabRow + ((unsigned)lx < 32u ? lx : 32);
@@ -270,10 +320,22 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
             }
             float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(36 * 36);
 #pragma unroll
-            for (int j = 0; j < kStripRows; ++j)
-                out[(yt0 + j) * 36 + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
+            for (int j = 0; j < kStripRows; ++j) {
+                if (DIRECT && own[j]) {  // round k of a pixel only this block covers: the master, in round order
+                    m[j].x += rg[j].x;
+                    m[j].y += rg[j].y;
+                    m[j].z += bw[j].x;
+                    m[j].w += bw[j].y;
+                } else {
+                    out[(yt0 + j) * 36 + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
+                }
+            }
         }
     }
+    if (DIRECT)
+#pragma unroll
+        for (int j = 0; j < kStripRows; ++j)
+            if (own[j]) fb4[(size_t)(oy + yt0 + j) * mcols + ox + xt] = m[j];
 }
 
 // Fused splat + merge for the 2-pixel border: one workgroup per 32x32 tile of MASTER pixels walks the chunk's
@@ -578,35 +640,6 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(4)
         if (sc[0] < ncols && sr[0] + j < nrows) *fb_at(sc[0], sr[0] + j) = m[j];
 }
 
-// Rendered blocks whose merged region ((sx+2b) x (sy+2b) at offset (ox, oy) in master coordinates)
-// covers master pixel (mx, my), in BlockGenerator spiral order: the order ImageBlock::put(ImageBlock&)
-// adds them (src/utils/block.cpp:125-134). Returns their number (<= 4) and slots.
-__device__ __forceinline__ int covering_blocks(const SplatLaunch &P, int mx, int my, int *slot) {
-    const int cols = 32 + 2 * P.border;
-    int blk[4], nb = 0;
-    const int bx_lo = max((mx - cols + 1 + 31) >> 5, 0), bx_hi = min(mx >> 5, P.nbx - 1);
-    const int nby = (P.height + 31) >> 5;
-    const int by_lo = max((my - cols + 1 + 31) >> 5, 0), by_hi = min(my >> 5, nby - 1);
-    for (int by = by_lo; by <= by_hi; ++by)
-        for (int bx = bx_lo; bx <= bx_hi; ++bx) {
-            const int bid = by * P.nbx + bx;
-            const int sl = P.block_slot[bid];
-            if (sl < 0) continue;
-            const int ox = bx * 32, oy = by * 32;
-            const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-            if (mx - ox >= sxb + 2 * P.border || my - oy >= syb + 2 * P.border) continue;
-            blk[nb] = bid;
-            slot[nb] = sl;
-            ++nb;
-        }
-    for (int a = 1; a < nb; ++a)
-        for (int b = a; b > 0 && P.block_rank[blk[b]] < P.block_rank[blk[b - 1]]; --b) {
-            int t = blk[b]; blk[b] = blk[b - 1]; blk[b - 1] = t;
-            t = slot[b]; slot[b] = slot[b - 1]; slot[b - 1] = t;
-        }
-    return nb;
-}
-
 // ImageBlock::put(ImageBlock&) into the master (src/utils/block.cpp:125-134): per master
 // pixel, per round, the overlapping rendered blocks in BlockGenerator spiral order.
 __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
@@ -616,7 +649,7 @@ __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
     const int cols = 32 + 2 * P.border;
     int slot[4];
     const int nb = covering_blocks(P, mx, my, slot);
-    if (nb == 0) return;
+    if (nb == 0 || (P.direct && nb == 1)) return;  // direct: the tab splat already added this pixel's rounds
     int off[4];
     for (int q = 0; q < nb; ++q) {
         const int bid = P.blocks[slot[q]];
@@ -695,20 +728,27 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
             told = true;
             int a = 0, b = 0;
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, nh_tile_splat_kernel, kTileThreads, 0);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, nh_block_splat_tab_kernel, 256, 0);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, nh_block_splat_tab_kernel<false>, 256, 0);
             std::fprintf(stderr, "[nh] workgroups per CU: tile splat %d, tab splat %d\n", a, b);
         }
         hipLaunchKernelGGL(nh_tile_splat_kernel, dim3(n_tiles), dim3(kTileThreads), 0, st, Q);
         return;
     }
-    if (tabulated && P.border == 2 && P.reach == 2)
-        hipLaunchKernelGGL(nh_block_splat_tab_kernel, dim3(P.n_blocks, (P.n_rounds + kTabRounds - 1) / kTabRounds),
-                           dim3(256), 0, st, P);
+    SplatLaunch Q = P;
+    Q.direct = 0;
+    if (tabulated && P.border == 2 && P.reach == 2) {
+        const char *d = std::getenv("NH_SPLAT_DIRECT");  // opt-in until measured
+        Q.direct = d && d[0] == '1' ? 1 : 0;
+        if (Q.direct) hipLaunchKernelGGL(nh_block_splat_tab_kernel<true>, dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
+        else
+            hipLaunchKernelGGL(nh_block_splat_tab_kernel<false>, dim3(P.n_blocks, (P.n_rounds + kTabRounds - 1) / kTabRounds),
+                               dim3(256), 0, st, Q);
+    }
     else if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     else hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     dim3 grid((mcols + 15) / 16, (mrows + 15) / 16);
-    hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, P);
+    hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, Q);
 }
 
 void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st) {

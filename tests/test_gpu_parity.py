@@ -218,7 +218,8 @@ def test_render_deterministic_and_sharded(gpu, tmp_path):
                                             ((64, 64), 3, [1, 2]), ((96, 96), 2, [4])])
 def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, spp, blocks):
     """The fused splat + merge (NH_SPLAT_FUSED=1: one workgroup per master tile, rounds in order, blocks in spiral
-    order, no staging) gives the staged splat + merge pair's framebuffer bit for bit, and the oracle's: partial blocks and the master
+    order, no staging) and the staged pair with and without direct interior pixels (NH_SPLAT_DIRECT: pixels one
+    block covers go straight to the master) give the same framebuffer bit for bit, and the oracle's: partial blocks and the master
     border of the last block column / row (100x70, 33x31), block subsets whose neighbours are absent (every tile
     quadrant case), several chunks (1 MiB path budget) and both render modes."""
     xml = scenegen.cbox_xml(str(tmp_path), "c2")
@@ -226,8 +227,9 @@ def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, 
     s.set_resolution(*res)
     b = nh.Bvh(s)
     out = {}
-    for fused in ("0", "1"):
+    for fused, direct in (("0", "1"), ("0", "0"), ("1", "1")):  # staged (direct interior / all staged), fused
         monkeypatch.setenv("NH_SPLAT_FUSED", fused)
+        monkeypatch.setenv("NH_SPLAT_DIRECT", direct)
         for mode in (nh.MODE_MEGAKERNEL, nh.MODE_WAVEFRONT):
             for budget in (None, "1"):
                 if budget:
@@ -236,7 +238,7 @@ def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, 
                 ctx = nh.Context(0)
                 ctx.upload(s, b)
                 ctx.render(0, spp, seed=21, clear=True, mode=mode, blocks=blocks)
-                out[(fused, mode, budget)] = ctx.framebuffer()
+                out[(fused, direct, mode, budget)] = ctx.framebuffer()
                 monkeypatch.delenv("NH_WF_BUDGET_MB", raising=False)
                 monkeypatch.delenv("NH_RECORD_BUDGET_MB", raising=False)
     ref = no.OracleScene(s).render(0, spp, seed=21, blocks=blocks)
