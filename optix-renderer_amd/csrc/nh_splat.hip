@@ -202,7 +202,7 @@ constexpr int kTabV = 0, kTabWX = 3, kTabWY = 8, kTabPlanes = 13;
 // other rendered block covers (the block's 28x28 interior, and the master border of edge blocks) add each round's
 // value straight into the master in round order -- the merge's sum for a pixel with one covering block -- so only
 // the pixels shared with neighbouring blocks go through the staging buffer and nh_merge_kernel.
-template <bool DIRECT>
+template <bool DIRECT, int ROUNDS = kTabRounds>
 __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
     __shared__ float W[kTabPlanes * kTabPlane];
     __shared__ float tab[33];
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
     const int by = bid / P.nbx, bx = bid - by * P.nbx;
     const int ox = bx * 32, oy = by * 32;
     const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    const int k0 = DIRECT ? 0 : blockIdx.y * kTabRounds, k1 = DIRECT ? P.n_rounds : min(k0 + kTabRounds, P.n_rounds);
+    const int k0 = DIRECT ? 0 : blockIdx.y * ROUNDS, k1 = DIRECT ? P.n_rounds : min(k0 + ROUNDS, P.n_rounds);
     const float r = P.radius;
     if (threadIdx.x < 33) tab[threadIdx.x] = P.table[threadIdx.x];
     // the zero rows and column are never written again
@@ -739,10 +739,15 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
     if (tabulated && P.border == 2 && P.reach == 2) {
         const char *d = std::getenv("NH_SPLAT_DIRECT");  // opt-in until measured
         Q.direct = d && d[0] == '1' ? 1 : 0;
-        if (Q.direct) hipLaunchKernelGGL(nh_block_splat_tab_kernel<true>, dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
-        else
-            hipLaunchKernelGGL(nh_block_splat_tab_kernel<false>, dim3(P.n_blocks, (P.n_rounds + kTabRounds - 1) / kTabRounds),
-                               dim3(256), 0, st, Q);
+        const char *rv = std::getenv("NH_SPLAT_ROUNDS");  // rounds per workgroup: 1, 2, 4 (default) or 8
+        const int tr = rv ? std::atoi(rv) : kTabRounds;
+        const dim3 g(P.n_blocks, (P.n_rounds + tr - 1) / tr);
+        if (Q.direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
+        else if (tr == 1) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 1>), g, dim3(256), 0, st, Q);
+        else if (tr == 2) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 2>), g, dim3(256), 0, st, Q);
+        else if (tr == 8) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8>), g, dim3(256), 0, st, Q);
+        else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, kTabRounds>), dim3(P.n_blocks, (P.n_rounds + kTabRounds - 1) / kTabRounds),
+                                dim3(256), 0, st, Q);
     }
     else if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     else hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
