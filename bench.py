@@ -32,6 +32,14 @@ The JSON line also carries:
   denoise       (N=1) Denoiser::denoise on the rendered master block (render.cpp:368-369): the GPU
                 SimpleDenoiser with scenes/project/denoiser/denoiser-test.xml's parameters, HIP-event time,
                 beside the serial CPU oracle on a crop of the same image
+  strong_c4     (every N) the north star's scaling target (BASELINE configs[3]): the fixed C4 image (2048^2,
+                mirror + dielectric spheres + area light, path_mis) at --strong-spp spp, split over the ranks by
+                32x32 blocks, one nh_render call per rank plus the RCCL reduce inside the timed region, max over
+                ranks; the driver's SCALE run gets the strong-scaling curve from this sub-record
+  megakernel    (N=1) BASELINE configs[1]'s comparison: C2 through the one-kernel-per-sample path
+  denoiser_test (N=1) scenes/project/denoiser/denoiser-test.xml (800x600, checkerboard floor, curvy bowl, two area
+                lights) as the reference's report times it (reports/project-report/denoising.html:79-81): 1024 spp
+                ground truth ("5 minutes"), 16 spp ("roughly 20 seconds") + SimpleDenoiser ("about one second")
 """
 import argparse
 import json
@@ -60,6 +68,10 @@ def parse():
     p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                    help="weak: N x --rounds rounds per step over each rank's 1/N of the blocks (default); strong: "
                         "a fixed image (C4 2048^2 unless --config) and --rounds x --steps spp split by blocks")
+    p.add_argument("--strong-spp", type=int, default=256,
+                   help="spp of the strong_c4 sub-record (fixed 2048^2 C4 image split over the ranks; 0 = skip)")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the N=1 megakernel and denoiser_test sub-records")
     p.add_argument("--traversal-1m-steps", type=int, default=4,
                    help="N=1: also time the perf-1M traversal kernel (0 = skip)")
     p.add_argument("--width", type=int, default=None)
@@ -404,6 +416,7 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
     if args.dump_framebuffer and rank == 0:
         np.save(args.dump_framebuffer, reduced if reduced is not None else ctx.framebuffer())
     st = ctx.stats()
+    pools = int(st.get("pools_active", 0)) if a.mode == "wavefront" else 0  # path pools of the timed steps
     # chunks of the timed steps and how many of their tails ran decoupled from their path pool (tail slots)
     chunks = {"chunks": int(st["launches_splat"]), "tails_async": int(st["tails_async"])}
     roof_pass = None
@@ -430,7 +443,8 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
         roof = roofline(a, calib, st, W, H, R)
         roof["timed"] = roof_pass or "the timed region"
     return {"scene": scene, "W": W, "H": H, "R": R, "desc": scene_desc, "elapsed": elapsed, "samples": samples,
-            "roof": roof, "bvh_s": bvh_s, "upload_s": upload_s, "ctx": ctx, "chunks": chunks}
+            "roof": roof, "bvh_s": bvh_s, "upload_s": upload_s, "ctx": ctx, "chunks": chunks,
+            "pools": pools}
 
 
 def reduce_framebuffer(ctx, dist, args, local, rank):
@@ -521,6 +535,105 @@ def traversal_1m(nh, args, local):
     return out
 
 
+def strong_c4_record(nh, args, world, rank, local, dist):
+    """The north star's >= 6x scaling target on its own configuration (BASELINE configs[3]): the
+    fixed C4 image (2048^2 Cornell box, mirror + dielectric spheres, area light, path_mis) at --strong-spp spp,
+    32x32 blocks dealt round-robin to the ranks (the reference's fixed sample budget, render.cpp:281-347, split
+    by tile). Each rank renders all spp of its blocks in one nh_render call (the library chunks it), then the RCCL
+    reduce of the framebuffer to rank 0 -- both inside the timed region; max over ranks. A first identical call
+    (untimed) sizes the path pools for the same chunks."""
+    a = argparse.Namespace(**vars(args))
+    a.config, a.width, a.height = "c4", None, None
+    tmp = tempfile.mkdtemp(prefix="nh_strong_")
+    xml, W, H, desc = build_scene(a, tmp)
+    scene = nh.Scene(xml)
+    bvh = nh.Bvh(scene, n_threads=16)
+    ctx = nh.Context(local)
+    ctx.upload(scene, bvh)
+    blocks = nh.tile_shard(W, H, world, rank) if world > 1 else None
+    spp = args.strong_spp
+    trav = nh.TRAVERSAL_ORDERED if args.traversal == "ordered" else nh.TRAVERSAL_REFERENCE
+    ctx.render(spp, 2 * spp, seed=args.seed, blocks=blocks, traversal=trav, clear=True, mode=nh.MODE_WAVEFRONT)
+    ctx.render(0, 0, seed=args.seed, blocks=blocks, traversal=trav, clear=True)
+    ctx.synchronize()
+    ctx.reset_stats()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ctx.render(0, spp, seed=args.seed, blocks=blocks, traversal=trav, clear=False, mode=nh.MODE_WAVEFRONT)
+    if dist is not None:
+        reduce_framebuffer(ctx, dist, args, local, rank)
+    ctx.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        elapsed = max_over_ranks(elapsed, dist, args, local)
+    st = ctx.stats()
+    ctx.close()
+    samples = W * H * spp
+    return {"workload": f"{desc}, {spp} spp, path_mis (fixed image, BASELINE configs[3])", "n_gpus": world,
+            "spp": spp, "samples": samples, "ms": round(elapsed * 1e3, 3),
+            "msamples_s": round(samples / elapsed / 1e6, 3), "scaling": "strong",
+            "partition": f"32x32 blocks round-robin over {world} rank(s), one nh_render call each"
+                         + (f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce" if world > 1 else ""),
+            "chunks_rank0": int(st["launches_splat"]), "pools_rank0": int(st.get("pools_active", 0))}
+
+
+def megakernel_record(nh, args, local):
+    """BASELINE configs[1] names "megakernel vs wavefront": the same C2 workload through nh_path_kernel (one thread
+    per (pixel, round) runs the whole path_mis loop), --rounds rounds per step."""
+    a = argparse.Namespace(**vars(args))
+    a.mode, a.dump_framebuffer, a.no_calibrate, a.pools = "megakernel", None, True, 0
+    r = run_workload(nh, a, "c2", 2, 1, local)
+    st = r["ctx"].stats()
+    r["ctx"].close()
+    return {"workload": f"{r['desc']}, {r['R'] * 2} spp, path_mis", "mode": "megakernel",
+            "msamples_s": round(r["samples"] / r["elapsed"] / 1e6, 3),
+            "ms_per_step": round(r["elapsed"] / 2 * 1e3, 3),
+            "path_kernel_ms_per_launch": round(st["kernel_ms_path"] / max(st["launches_path"], 1), 4)}
+
+
+def denoiser_test_record(nh, local):
+    """scenes/project/denoiser/denoiser-test.xml (tests/golden/textured_scenes.json.gz: 800x600, checkerboard_color
+    floor, curvy bowl, two area lights, SimpleDenoiser sigma_d 6 / sigma_vr 1.5 / range 7), timed as the reference's
+    report states its numbers (reports/project-report/denoising.html:79-81): the 1024 spp ground truth ("It took 5
+    minutes"), the 16 spp input ("roughly 20 seconds") and the denoise ("about one second"). The authors' machine is
+    not stated; the published figures are quoted as given."""
+    import scenegen
+    d = scenegen.materialize(tempfile.mkdtemp(prefix="nh_dn_"))
+    scene = nh.Scene(os.path.join(d, "scenes/project/denoiser/denoiser-test.xml"))
+    W, H = scene.width, scene.height
+    bvh = nh.Bvh(scene, n_threads=16)
+    ctx = nh.Context(local)
+    ctx.upload(scene, bvh)
+    trav, mode = nh.TRAVERSAL_ORDERED, nh.MODE_WAVEFRONT
+    ctx.render(0, 1024, seed=1, traversal=trav, clear=True, mode=mode)  # warm: pools sized for the same chunks
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    ctx.render(0, 1024, seed=2, traversal=trav, clear=True, mode=mode)
+    ctx.synchronize()
+    t_gt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ctx.render(0, 16, seed=3, traversal=trav, clear=True, mode=mode)
+    ctx.synchronize()
+    t16 = time.perf_counter() - t0
+    ctx.reset_stats()
+    t0 = time.perf_counter()
+    ctx.denoise()
+    t_dn = time.perf_counter() - t0
+    ms_dn = ctx.stats()["kernel_ms_denoise"]
+    ctx.close()
+    pub_gt, pub_16 = 5 * 60.0, 20.0
+    return {"scene": "scenes/project/denoiser/denoiser-test.xml", "image": f"{W}x{H}", "integrator": "path_mis",
+            "textures": "checkerboard_color albedo (floor)",
+            "groundtruth_1024spp_s": round(t_gt, 4), "groundtruth_msamples_s": round(W * H * 1024 / t_gt / 1e6, 3),
+            "input_16spp_s": round(t16, 4), "denoise_s": round(t_dn, 4), "denoise_kernel_ms": round(ms_dn, 3),
+            "published": {"groundtruth_1024spp_s": pub_gt, "input_16spp_s": pub_16, "denoise_s": 1.0,
+                          "groundtruth_msamples_s": round(W * H * 1024 / pub_gt / 1e6, 3),
+                          "source": "reports/project-report/denoising.html:79-81 (Nori CPU path_mis; machine not "
+                                    "stated)"},
+            "speedup_groundtruth": round(pub_gt / t_gt, 1)}
+
+
 def free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -555,10 +668,9 @@ def launcher_selftest(args):
 
 def main():
     args = parse()
-    # one hardware queue per path-pool stream (nori_hip.py raises it the same way; done here too, before torch
-    # may initialise the HIP runtime in a multi-rank run): at least 8 per process
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    # one hardware queue per path-pool stream (nori_hip.py sets the same default; done here too, before torch may
+    # initialise the HIP runtime in a multi-rank run). An explicit setting is respected; the line records it.
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -586,6 +698,9 @@ def main():
     blocks = nh.tile_shard(W, H, world, rank) if world > 1 else None
     r = run_workload(nh, args, args.config, args.steps, args.warmup, local, blocks=blocks, world=world, rank=rank,
                      dist=dist)
+    strong = None
+    if args.strong_spp > 0 and not (args.scaling == "strong" and args.config == "c4"):
+        strong = strong_c4_record(nh, args, world, rank, local, dist)
     if rank == 0:
         W, H, R = r["W"], r["H"], r["R"]
         value = r["samples"] / r["elapsed"] / 1e6
@@ -600,6 +715,12 @@ def main():
         if world == 1 and args.traversal_1m_steps > 0 and args.config != "bumpy1m":
             r["ctx"].close()
             t1m = traversal_1m(nh, args, local)
+        mk = dn_scene = None
+        if world == 1 and not args.no_extras:
+            r["ctx"].close()
+            if args.mode == "wavefront":
+                mk = megakernel_record(nh, args, local)
+            dn_scene = denoiser_test_record(nh, local)
         spp = R * args.steps
         if args.scaling == "strong":
             par = f"tile-shard x{world}, strong scaling: fixed {W}x{H} image, {spp} spp split by blocks"
@@ -621,7 +742,8 @@ def main():
             "config": {"workload": f"{r['desc']}, {spp} spp, path_mis", "config": args.config,
                        "width": W, "height": H, "spp": spp, "rounds_per_step": R,
                        "mode": args.mode, "traversal": args.traversal,
-                       "pools": args.pools or int(os.environ.get("NH_POOLS", "0")) or "library default (2)",
+                       "pools": r["pools"] or None,
+                       "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),
                        "parallelism": (f"{par} + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce"
                                        if world > 1 else "single GPU"),
                        "bvh_build_s": round(r["bvh_s"], 3), "upload_s": round(r["upload_s"], 3),
@@ -631,6 +753,9 @@ def main():
             "traversal_1m": t1m,
             "cpu_baseline": cpu,
             "denoise": dn,
+            "strong_c4": strong,
+            "megakernel": mk,
+            "denoiser_test": dn_scene,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

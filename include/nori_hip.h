@@ -89,7 +89,30 @@ typedef struct nh_bsdf {
     float int_ior, ext_ior;  /* dielectric / microfacet */
     float kd[3];             /* microfacet diffuse base */
     float ks;                /* microfacet: 1 - max(kd) */
+    uint32_t albedo_texture; /* diffuse: 1 + index into nh_scene_desc.textures of its Texture<Color3f> albedo
+                                child (diffuse.cpp:70-91); 0 = the constant albedo above */
 } nh_bsdf;
+
+/* A Texture<Color3f> child of a BSDF, evaluated at the hit's uv (Intersection::uv, BSDFQueryRecord::uv):
+ *   NH_TEXTURE_CONSTANT     ConstantTexture (src/textures/consttexture.cpp): value1
+ *   NH_TEXTURE_CHECKERBOARD Checkerboard<Color3f> (src/textures/checkerboard.cpp:29-47): value1 / value2 by the
+ *                           parity of the cell of uv / scale - delta
+ *   NH_TEXTURE_PNG          PNGTexture (src/textures/PNGTexture.cpp:125-160): nearest texel of an sRGB-decoded RGBA
+ *                           image (row 0 of the PNG first) at texel_offset in nh_scene_desc.texels */
+enum { NH_TEXTURE_CONSTANT = 0, NH_TEXTURE_CHECKERBOARD = 1, NH_TEXTURE_PNG = 2 };
+typedef struct nh_texture {
+    int32_t type;            /* NH_TEXTURE_* */
+    float value1[3];         /* constant value / checkerboard value1 */
+    float value2[3];         /* checkerboard value2 */
+    float delta[2];          /* checkerboard Point2f delta */
+    float scale[2];          /* checkerboard Vector2f scale */
+    int32_t width, height;   /* png */
+    uint64_t texel_offset;   /* png: first texel (4 floats) in nh_scene_desc.texels */
+    float scale_u, scale_v;  /* png scaleU / scaleV */
+    float offset_u, offset_v;/* png offsetU / offsetV (non-spherical lookups) */
+    int32_t spherical;       /* png sphericalTexture (eulerAngles = 0) */
+    int32_t pad;
+} nh_texture;
 
 /* One Nori Emitter (src/emitters/{arealight,pointlight}.cpp). */
 typedef struct nh_emitter {
@@ -171,6 +194,10 @@ typedef struct nh_scene_desc {
     const float *area_cdf;        /* concatenated per-mesh area CDFs */
     nh_envmap env;                /* valid when envmap >= 0 */
     nh_denoiser denoiser;         /* type NH_DENOISER_NONE when the scene has none */
+    uint32_t n_textures;          /* BSDF albedo textures (nh_bsdf.albedo_texture) */
+    const nh_texture *textures;
+    uint64_t n_texels;            /* RGBA texels of every png texture, 4 floats each */
+    const float *texels;
 } nh_scene_desc;
 
 /* ---- BVH in the reference's own layout (include/nori/bvh.h:127-165) ---- */
@@ -275,6 +302,8 @@ typedef struct nh_render_stats {
     /* wavefront chunks whose tail kernel ran on a tail slot's stream, decoupled from the chunk's path pool
        (RR-ahead pipeline with several pools: the pool took the next chunk meanwhile) */
     uint64_t tails_async;
+    /* wavefront path pools the last render drove (NH_POOLS, else 2, or 3 for scenes with mirror / dielectric BSDFs) */
+    uint64_t pools_active;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;
@@ -290,6 +319,9 @@ int nh_scene_get_desc(const nh_scene *scene, nh_scene_desc *out);
 int nh_scene_set_resolution(nh_scene *scene, int32_t width, int32_t height);
 int nh_scene_set_sample_count(nh_scene *scene, int32_t spp);
 int nh_scene_set_bsdf(nh_scene *scene, uint32_t shape, const nh_bsdf *bsdf);
+/* append a texture to the scene's texture table (png: texels = width*height*4 floats, copied); returns its
+   index + 1 for nh_bsdf.albedo_texture, or 0 on error (nh_host_last_error) */
+uint32_t nh_scene_add_texture(nh_scene *scene, const nh_texture *tex, const float *texels);
 int nh_scene_set_integrator(nh_scene *scene, int32_t integrator);
 void nh_scene_free(nh_scene *scene);
 const char *nh_host_last_error(void);

@@ -51,6 +51,8 @@ struct WfJob {
     int s0, rounds;
     uint64_t seed;
     bool ordered, stats;
+    bool staged;   // splat layout, decided once when the chunk's buffers are sized (NH_SPLAT_FUSED read then only):
+                   // per-(round, block) staging + merge, or the fused tile splat with no staging
 };
 
 // A path pool: the device state one chunk needs (double-buffered path state, shadow queue, sample
@@ -331,6 +333,27 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         o.ar = b.albedo[0]; o.ag = b.albedo[1]; o.ab = b.albedo[2];
         o.alpha = b.alpha; o.int_ior = b.int_ior; o.ext_ior = b.ext_ior; o.ks = b.ks;
         o.kr = b.kd[0]; o.kg = b.kd[1]; o.kb = b.kd[2];
+        if (b.albedo_texture > d->n_textures || (b.albedo_texture && !d->textures))
+            return fail(c, "BSDF albedo texture index out of range"), NH_ERR_INVALID;
+        o.tex = b.type == NH_BSDF_DIFFUSE ? (int)b.albedo_texture : 0;
+    }
+    std::vector<nhd::DTex> dt(d->n_textures);
+    for (uint32_t i = 0; i < d->n_textures; ++i) {
+        const nh_texture &t = d->textures[i];
+        nhd::DTex &o = dt[i];
+        std::memset(&o, 0, sizeof(o));
+        if (t.type < NH_TEXTURE_CONSTANT || t.type > NH_TEXTURE_PNG) return fail(c, "unknown texture type"), NH_ERR_INVALID;
+        if (t.type == NH_TEXTURE_PNG &&
+            (t.width <= 0 || t.height <= 0 || !d->texels ||
+             t.texel_offset + (uint64_t)t.width * (uint64_t)t.height > d->n_texels))
+            return fail(c, "png texture outside the scene's texels"), NH_ERR_INVALID;
+        o.type = t.type;
+        o.w = t.width; o.h = t.height; o.spherical = t.spherical;
+        o.v1r = t.value1[0]; o.v1g = t.value1[1]; o.v1b = t.value1[2];
+        o.v2r = t.value2[0]; o.v2g = t.value2[1]; o.v2b = t.value2[2];
+        o.dx = t.delta[0]; o.dy = t.delta[1]; o.sx = t.scale[0]; o.sy = t.scale[1];
+        o.su = t.scale_u; o.sv = t.scale_v; o.ou = t.offset_u; o.ov = t.offset_v;
+        o.off = (long long)t.texel_offset;
     }
     std::vector<DEmitter> de(d->n_emitters);
     for (uint32_t i = 0; i < d->n_emitters; ++i) {
@@ -359,6 +382,12 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     if ((rc = upload(c, c->scene_bufs, d->BT, 3 * nv, &S.BT))) return rc;
     if ((rc = upload(c, c->scene_bufs, d->F, 3 * (size_t)d->n_faces, &S.F))) return rc;
     if ((rc = upload(c, c->scene_bufs, d->area_cdf, (size_t)d->n_area_cdf, &S.area_cdf))) return rc;
+    if (!dt.empty() && (rc = upload(c, c->scene_bufs, dt.data(), dt.size(), &S.texs))) return rc;
+    if (d->n_texels) {
+        const float *tx = nullptr;
+        if ((rc = upload(c, c->scene_bufs, d->texels, 4 * (size_t)d->n_texels, &tx))) return rc;
+        S.texels = reinterpret_cast<const float4 *>(tx);
+    }
     S.envmap = d->envmap;
     if (d->envmap >= 0) {
         const nh_envmap &e = d->env;
@@ -846,8 +875,10 @@ static void pool_free(WfPool &p) {
     p = WfPool{};
 }
 
-static SplatLaunch make_splat(const nh_ctx *c, const float4 *rec, const float *rec_jy, float4 *staging, int rounds) {
+static SplatLaunch make_splat(const nh_ctx *c, const float4 *rec, const float *rec_jy, float4 *staging, int rounds,
+                              bool staged) {
     SplatLaunch P{};
+    P.staged = staged ? 1 : 0;
     P.fb = c->fb;
     P.width = c->width;
     P.height = c->height;
@@ -870,10 +901,13 @@ static SplatLaunch make_splat(const nh_ctx *c, const float4 *rec, const float *r
     return P;
 }
 
+// the splat layout of a chunk starting now: staged pair, or the fused tile splat (NH_SPLAT_FUSED=1)
+static bool splat_staged(const nh_ctx *c) {
+    return nh::splat_uses_staging(c->border, (int)std::floor(c->filter.radius + 0.5f));
+}
 // float4 entries of one (round, block) ImageBlock in the splat's staging buffer (0: the fused splat stages nothing)
-static size_t block_px(const nh_ctx *c) {
-    const int reach = (int)std::floor(c->filter.radius + 0.5f);
-    if (!nh::splat_uses_staging(c->border, reach)) return 0;
+static size_t block_px(const nh_ctx *c, bool staged) {
+    if (!staged) return 0;
     return (size_t)(32 + 2 * c->border) * (32 + 2 * c->border);
 }
 
@@ -896,16 +930,18 @@ static bool tail_async_enabled() {
 }
 
 // start job j on idle pool p: buffers, traversal choice, initial queue (all n_paths camera paths)
-static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
+static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
+    WfJob j = job;
+    j.staged = splat_staged(c);  // the staging below is sized for this layout; the chunk's splat uses the same
     const int n_paths = j.rounds * c->n_list;
-    int rc = pool_alloc(c, p, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c));
+    int rc = pool_alloc(c, p, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c, j.staged));
     if (rc) return rc;
     // the other pools in use get the same capacity now (idle ones only: nothing of theirs is in
     // flight), so the first render call, not a later one, pays for their allocation
     for (int i = 0; i < active_pools(c); ++i) {
         WfPool &o = c->pools[i];
         if (&o == &p || o.state != WfPool::IDLE) continue;
-        if ((rc = pool_alloc(c, o, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c))))
+        if ((rc = pool_alloc(c, o, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c, j.staged))))
             return rc;
     }
     // so do the idle tail slots' record and staging buffers: chunks hand theirs over at a tail hand-off and take the
@@ -915,7 +951,7 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &j) {
         for (int i = kPools; i < kPools + kTails; ++i) {
             WfPool &o = c->pools[i];
             if (o.state != WfPool::IDLE) continue;
-            if ((rc = pool_alloc(c, o, (size_t)kTailCap, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c))))
+            if ((rc = pool_alloc(c, o, (size_t)kTailCap, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c, j.staged))))
                 return rc;
         }
     p.job = j;
@@ -1190,7 +1226,7 @@ static int pool_splat(nh_ctx *c, WfPool &p) {
     if (p.job.stats) nh::launch_count_invalid(p.rec, (size_t)p.L.n_paths, c->counters, p.stream);
     if (c->fb_ev_set) HIP_TRY(c, hipStreamWaitEvent(p.stream, c->fb_ev, 0));
     HIP_TRY(c, hipEventRecord(p.ev_splat0, p.stream));
-    nh::launch_splat(make_splat(c, p.rec, p.rec_jy, p.staging, p.job.rounds), p.stream);
+    nh::launch_splat(make_splat(c, p.rec, p.rec_jy, p.staging, p.job.rounds, p.job.staged), p.stream);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(p.ev_splat, p.stream));
     HIP_TRY(c, hipEventRecord(c->fb_ev, p.stream));
@@ -1217,9 +1253,11 @@ static int pool_finish(nh_ctx *c, WfPool &p) {
         std::fprintf(stderr, "[nh] chunk seq %llu: %d paths, %d bounces%s, %.3f ms, live/bounce(ms):",
                      (unsigned long long)p.job.seq, p.L.n_paths, p.it + 1, p.tail ? " (last = tail kernel)" : "", t_all);
         for (int b = 0; b <= p.it && b < (int)p.in_e.size(); ++b) {
-            float d = 0.f;
+            float d = 0.f, e = 0.f, sh = 0.f;
             (void)hipEventElapsedTime(&d, p.events[(size_t)b * 4], p.events[(size_t)b * 4 + 3]);
-            std::fprintf(stderr, " %llu(%.3f)", (unsigned long long)p.in_e[b], d);
+            (void)hipEventElapsedTime(&e, p.events[(size_t)b * 4], p.events[(size_t)b * 4 + 1]);
+            (void)hipEventElapsedTime(&sh, p.events[(size_t)b * 4 + 1], p.events[(size_t)b * 4 + 2]);
+            std::fprintf(stderr, " %llu(%.3f e%.3f s%.3f)", (unsigned long long)p.in_e[b], d, e, sh);
         }
         std::fprintf(stderr, "\n");
     }
@@ -1282,9 +1320,13 @@ static int event_done(hipEvent_t e, hipError_t &err) {
 // Device errors of this context's work so far (HIP errors are sticky per thread): checked at the end of
 // nh_render / nh_synchronize, so a fault in a render's kernels is reported by the call that submitted or
 // completed them, not by the next unrelated call (a denoise, a framebuffer read).
+// Judged from this context's own streams only: the thread's last-error slot may hold another context's (or the
+// host application's) error, which must not fail this call nor be cleared by it. Launch errors of this context's
+// kernels are caught right after each launch (HIP_TRY(hipGetLastError())); a fault while they run shows in
+// the status of their stream.
 static int check_device(nh_ctx *c, const char *where) {
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) {
+    hipError_t e = hipSuccess;
+    {
         for (WfPool &p : c->pools) {
             if (!p.stream) continue;
             const hipError_t q = hipStreamQuery(p.stream);
@@ -1314,6 +1356,7 @@ static void pipeline_reset(nh_ctx *c) {
 // submitted chunk has started and every busy pool is draining.
 static int pipeline_run(nh_ctx *c, bool all) {
     const int n_pools = active_pools(c);
+    c->stats.pools_active = (uint64_t)n_pools;
     for (;;) {
         bool progress = false;
         hipError_t ev_err = hipSuccess;
@@ -1451,7 +1494,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     if (q->collect_stats)
         HIP_TRY(c, hipMemsetAsync(c->counters, 0, kStatShards * kStatStride * sizeof(unsigned long long), c->stream));
     const size_t per_round = (size_t)c->n_list;
-    const size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px(c) * 16 +
+    const size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px(c, splat_staged(c)) * 16 +
                                    (wavefront ? per_round * kWfBytesPerPath : 0);
     // device memory per chunk: sample records + block ImageBlocks (+ path state, per pool). Every
     // wavefront chunk ends in a tail whose length is set by its longest path (C4: ~5-7 ms of
@@ -1468,8 +1511,12 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
             size_t held = 0;
-            for (const WfPool &p : c->pools) held += p.cap * (kWfBytesPerPath + 20) + p.staging_cap * sizeof(float4);
-            const size_t avail = (size_t)((double)(free_b + held) * 0.85) / (size_t)active_pools(c);
+            for (const WfPool &p : c->pools)
+                held += p.cap * kWfBytesPerPath + p.rec_cap * 20 + p.staging_cap * sizeof(float4);
+            // asynchronous tails: each tail slot also holds a whole chunk's sample records and staging (and
+            // kTailCap paths of state), so it counts as one more chunk-sized share
+            const int shares = active_pools(c) + (active_pools(c) > 1 && tail_async_enabled() ? kTails : 0);
+            const size_t avail = (size_t)((double)(free_b + held) * 0.85) / (size_t)shares;
             budget = std::min(budget, std::max(avail, per_round_bytes));
         }
     }
@@ -1501,11 +1548,12 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
             HIP_TRY(c, hipMalloc(&c->rec_jy, cap * sizeof(float)));
             c->rec_cap = cap;
         }
-        if (c->staging_cap < (size_t)chunk * c->n_blocks * block_px(c)) {
+        const bool staged = splat_staged(c);
+        if (c->staging_cap < (size_t)chunk * c->n_blocks * block_px(c, staged)) {
             (void)hipFree(c->staging);
             c->staging = nullptr;
             c->staging_cap = 0;
-            const size_t cap = (size_t)chunk * c->n_blocks * block_px(c);
+            const size_t cap = (size_t)chunk * c->n_blocks * block_px(c, staged);
             HIP_TRY(c, hipMalloc(&c->staging, cap * sizeof(float4)));
             c->staging_cap = cap;
         }
@@ -1534,7 +1582,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev.b, c->stream));
             if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters, c->stream);
-            nh::launch_splat(make_splat(c, c->rec, c->rec_jy, c->staging, k), c->stream);
+            nh::launch_splat(make_splat(c, c->rec, c->rec_jy, c->staging, k, staged), c->stream);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev.d, c->stream));
             evs.push_back(ev);

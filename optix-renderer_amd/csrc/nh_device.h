@@ -138,7 +138,18 @@ struct alignas(16) DBsdf {
     int type;
     float ar, ag, ab;      // diffuse albedo
     float alpha, int_ior, ext_ior, ks;
-    float kr, kg, kb, pad; // microfacet kd
+    float kr, kg, kb;      // microfacet kd
+    int tex;               // diffuse: 1 + albedo texture index (DScene::texs), 0 = the constant albedo
+};
+// Texture<Color3f> albedo (nh_texture): consttexture.cpp / checkerboard.cpp / PNGTexture.cpp
+enum : int { TEX_CONSTANT = 0, TEX_CHECKERBOARD = 1, TEX_PNG = 2 };
+struct alignas(16) DTex {
+    int type, w, h, spherical;
+    float v1r, v1g, v1b, v2r;
+    float v2g, v2b, dx, dy;
+    float sx, sy, su, sv;
+    float ou, ov;
+    long long off;  // png: first texel in DScene::texels
 };
 struct alignas(16) DEmitter {
     int type, shape;
@@ -177,6 +188,9 @@ struct DScene {
     int env_w, env_h, env_spherical, env_constant;
     float env_norm, env_su, env_sv, env_ou, env_ov;
     float env_r, env_g, env_b;
+    // BSDF albedo textures (DBsdf::tex) and the png texels they index
+    const DTex *texs;
+    const float4 *texels;
 };
 
 NHD F3 ldv(const float *a, uint32_t i) { return f3(a[3 * i], a[3 * i + 1], a[3 * i + 2]); }
@@ -272,10 +286,12 @@ NHD float smith_g1(const DBsdf &b, F3 v, F3 m) {  // microfacet.cpp:69-89
     float a2 = a * a;
     return (3.535f * a + 2.181f * a2) / (1.0f + 2.276f * a + 2.577f * a2);
 }
-NHD F3 bsdf_eval(const DBsdf &b, F3 wi, F3 wo, int measure) {
+// alb: the diffuse albedo at the query's uv (m_albedo->eval(bRec.uv): the constant albedo, or its texture's
+// value, nh_shade.h bsdf_albedo); unused by the other BSDFs
+NHD F3 bsdf_eval(const DBsdf &b, F3 wi, F3 wo, int measure, F3 alb) {
     if (b.type == BSDF_DIFFUSE) {  // diffuse.cpp:94-103
         if (measure != M_SOLID_ANGLE || wi.z <= 0 || wo.z <= 0) return f3(0, 0, 0);
-        return f3(b.ar * kInvPi, b.ag * kInvPi, b.ab * kInvPi);
+        return f3(alb.x * kInvPi, alb.y * kInvPi, alb.z * kInvPi);
     }
     if (b.type == BSDF_MICROFACET) {  // microfacet.cpp:92-105
         if (wo.z < 0.f) return f3(0, 0, 0);
@@ -303,7 +319,7 @@ NHD float bsdf_pdf(const DBsdf &b, F3 wi, F3 wo, int measure) {
     return 0.0f;
 }
 // returns the sample weight; wo/measure out (wo stays (0,0,0) on early returns, vector.h:49)
-NHD F3 bsdf_sample(const DBsdf &b, F3 wi, float sx, float sy, F3 &wo, int &measure) {
+NHD F3 bsdf_sample(const DBsdf &b, F3 wi, float sx, float sy, F3 &wo, int &measure, F3 alb) {
     wo = f3(0, 0, 0);
     measure = M_UNKNOWN;
     switch (b.type) {
@@ -311,7 +327,7 @@ NHD F3 bsdf_sample(const DBsdf &b, F3 wi, float sx, float sy, F3 &wo, int &measu
             if (wi.z <= 0) return f3(0, 0, 0);
             measure = M_SOLID_ANGLE;
             wo = cosine_hemisphere(sx, sy);
-            return f3(b.ar, b.ag, b.ab);
+            return alb;
         case BSDF_MIRROR:  // mirror.cpp:41-57
             if (wi.z <= 0) return f3(0, 0, 0);
             wo = f3(-wi.x, -wi.y, wi.z);
@@ -353,7 +369,7 @@ NHD F3 bsdf_sample(const DBsdf &b, F3 wi, float sx, float sy, F3 &wo, int &measu
                 wo = cosine_hemisphere(sx, s1);
             }
             if (wo.z <= 0.f) return f3(0, 0, 0);
-            F3 e = bsdf_eval(b, wi, wo, M_UNKNOWN);
+            F3 e = bsdf_eval(b, wi, wo, M_UNKNOWN, alb);
             float p = bsdf_pdf(b, wi, wo, M_UNKNOWN);
             return f3(e.x / p * wo.z, e.y / p * wo.z, e.z / p * wo.z);
         }

@@ -38,6 +38,9 @@ struct SplatLaunch {
     const int *block_slot;  // block id -> slot or -1
     int n_blocks;
     float4 *staging;
+    int staged;             // 1: staged pair (splat into staging, then merge); 0: the fused tile splat (no staging).
+                            // Fixed when the chunk's staging was sized, so a knob change mid-pipeline cannot
+                            // mismatch the two
     int direct;             // the tab splat added the rounds of pixels with one covering block to fb (merge skips them)
     int debug;              // timing experiments only (NH_SPLAT_DEBUG, images wrong): bits skip the fused splat's
                             // phase 1 (1), phase 2 (2), record fetch (4), master-border strips (8)

@@ -51,6 +51,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
         hit_info(S, tv, h, o, d, its);
         const DShape shape = S.shapes[its.shape];
         const DBsdf bsdf = S.bsdfs[shape.bsdf];
+        const F3 alb = bsdf_albedo(S, bsdf, its.u, its.v);
         if (shape.emitter >= 0) {  // path_mis.cpp:51-56
             const DEmitter em = S.emitters[shape.emitter];
             const F3 wi = normalized(sub(its.p, o));
@@ -73,7 +74,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
         float pdfems = 0.f, pdfems_mats = 0.f;
         if (nee) {
             const F3 we = to_local(its.sh, es.wi);
-            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
+            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE, alb);
             const float cs = we.z;
             li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
                         ems_col.z * cs * f.z * n_lights);
@@ -84,7 +85,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
         const float bx = rng.next1d(), by = rng.next1d();
         F3 wo;
         int measure;
-        const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
+        const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure, alb);
         const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);  // used only if the probe hits an emitter
         const F3 nd = to_world(its.sh, wo);
         const F3 no = its.p;
@@ -164,6 +165,7 @@ __device__ F3 li_path_mats(const DScene &S, const Traversal &tv, Rng &rng, F3 o,
         hit_info(S, tv, h, o, d, its);
         const DShape shape = S.shapes[its.shape];
         const DBsdf bsdf = S.bsdfs[shape.bsdf];
+        const F3 alb = bsdf_albedo(S, bsdf, its.u, its.v);
         if (shape.emitter >= 0) {
             F3 wi = normalized(sub(its.p, o));
             li = add(li, mulc(t, emitter_eval(S.emitters[shape.emitter], o, its.sh.n, wi)));
@@ -175,7 +177,7 @@ __device__ F3 li_path_mats(const DScene &S, const Traversal &tv, Rng &rng, F3 o,
         const float bx = rng.next1d(), by = rng.next1d();
         F3 wo;
         int measure;
-        F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure);
+        F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure, alb);
         t = mulc(t, col);
         d = to_world(its.sh, wo);
         o = its.p;
@@ -261,6 +263,7 @@ __global__ __launch_bounds__(64) void nh_trace_wide_kernel(const DScene *__restr
     hit_info(S, tv, h, o, d, its);                                                               \
     const DShape shape = S.shapes[its.shape];                                                    \
     const DBsdf bsdf = S.bsdfs[shape.bsdf];                                                      \
+    const F3 alb = bsdf_albedo(S, bsdf, its.u, its.v);                                           \
     F3 result = f3(0, 0, 0);                                                                     \
     if (shape.emitter >= 0)                                                                      \
         result = add(result, emitter_eval(S.emitters[shape.emitter], o, its.sh.n, normalized(sub(its.p, o))));
@@ -281,7 +284,7 @@ __device__ F3 li_direct_ems(const DScene &S, const Traversal &tv, Rng &rng, F3 o
         if (STATS) queries++;
         if (trace<DEPTH, ORDERED, true, STATS>(tv, S, es.so, es.sd, es.smint, es.smaxt, hs, stk, stride, st)) continue;
         const F3 we = to_local(its.sh, es.wi);
-        const F3 f = bsdf_eval(bsdf, wo, we, M_SOLID_ANGLE);
+        const F3 f = bsdf_eval(bsdf, wo, we, M_SOLID_ANGLE, alb);
         result = add(result, mulc(scl(fabsf(we.z), li), f));
     }
     return result;
@@ -296,7 +299,7 @@ __device__ F3 li_direct_mats(const DScene &S, const Traversal &tv, Rng &rng, F3 
     const float bx = rng.next1d(), by = rng.next1d();
     F3 wo;
     int measure;
-    const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure);
+    const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(d)), bx, by, wo, measure, alb);
     if (is_zero(col)) return result;
     const F3 nd = to_world(its.sh, wo);
     Hit h2;
@@ -335,7 +338,7 @@ __device__ F3 li_direct_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o
         if (STATS) queries++;
         if (!trace<DEPTH, ORDERED, true, STATS>(tv, S, es.so, es.sd, es.smint, es.smaxt, hs, stk, stride, st)) {
             const F3 we = to_local(its.sh, es.wi);
-            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
+            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE, alb);
             const float cs = we.z;
             const float pdf_ems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
             const float pdf_mat = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
@@ -348,7 +351,7 @@ __device__ F3 li_direct_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o
     const float bx = rng.next1d(), by = rng.next1d();
     F3 wo;
     int measure;
-    const F3 col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
+    const F3 col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure, alb);
     if (measure == M_UNKNOWN) measure = M_SOLID_ANGLE;  // bqr_mat.measure = ESolidAngle before sample (:102)
     if (!is_zero(col)) {
         const F3 nd = to_world(its.sh, wo);
@@ -390,6 +393,7 @@ __device__ F3 li_direct_simple(const DScene &S, const Traversal &tv, Rng &rng, F
     Its its;
     hit_info(S, tv, h, o, d, its);
     const DBsdf bsdf = S.bsdfs[S.shapes[its.shape].bsdf];
+    const F3 alb = bsdf_albedo(S, bsdf, its.u, its.v);
     const F3 wo = to_local(its.sh, normalized(sub(o, its.p)));
     F3 result = f3(0, 0, 0);
     for (int l = 0; l < S.n_emitters; ++l) {
@@ -400,7 +404,7 @@ __device__ F3 li_direct_simple(const DScene &S, const Traversal &tv, Rng &rng, F
         Hit hs;
         if (STATS) queries++;
         if (trace<DEPTH, ORDERED, true, STATS>(tv, S, es.so, es.sd, es.smint, es.smaxt, hs, stk, stride, st)) continue;
-        const F3 f = bsdf_eval(bsdf, wi, wo, M_SOLID_ANGLE);
+        const F3 f = bsdf_eval(bsdf, wi, wo, M_SOLID_ANGLE, alb);
         const float cs = fabsf(dot(es.wi, its.sh.n)) / f_sqrt(dot(es.wi, es.wi));
         result = add(result, mulc(scl(cs, li), f));
     }

@@ -77,6 +77,53 @@ __device__ __forceinline__ void spherical_coordinates(F3 v, float &theta, float 
     phi = f_atan2(v.y, v.x);
     if (phi < 0) phi += 2 * kPi;
 }
+// static_cast<unsigned int>(float) / int(float) as the reference's x86-64 build executes them (cvttss2si: to 64
+// bits and the low word for unsigned, |x| >= 2^63 or NaN -> 0; to 32 bits for int, out of range or NaN -> INT_MIN)
+__device__ __forceinline__ unsigned x86_f2u(float x) { return fabsf(x) < 0x1p63f ? (unsigned)(long long)x : 0u; }
+__device__ __forceinline__ int x86_f2i(float x) { return fabsf(x) < 0x1p31f ? (int)x : (int)0x80000000; }
+
+// the texel lookup of PNGTexture::eval (PNGTexture.cpp:147-155): nearest texel, row 0 of the image first
+__device__ __forceinline__ F3 png_lookup(const float4 *texels, unsigned W, unsigned H, float su, float sv, float u,
+                                         float v) {
+    const unsigned w = x86_f2u(u * su * (float)W);
+    const unsigned h = H - x86_f2u(v * sv * (float)H);
+    const float4 c = texels[(h * W + w) % (W * H)];
+    return f3(c.x, c.y, c.z);
+}
+
+// the albedo texture of a diffuse BSDF at the hit's uv (diffuse.cpp:101/:139, m_albedo->eval(bRec.uv)):
+// ConstantTexture, Checkerboard<Color3f> (checkerboard.cpp:29-47) or PNGTexture (PNGTexture.cpp:125-160)
+__device__ __noinline__ F3 tex_eval(const DScene &S, int ti, float u, float v) {
+    const DTex t = S.texs[ti];
+    if (t.type == TEX_CHECKERBOARD) {
+        const float ox = u / t.sx - t.dx, oy = v / t.sy - t.dy;
+        const int x = x86_f2i(ox) + (ox < 0.f), y = x86_f2i(oy) + (oy < 0.f);
+        // (x + y) % 2 == 0 with the reference's wrap-around addition: the sum's low bit
+        return (((unsigned)x + (unsigned)y) & 1u) == 0 ? f3(t.v1r, t.v1g, t.v1b) : f3(t.v2r, t.v2g, t.v2b);
+    }
+    if (t.type == TEX_PNG) {
+        if (t.spherical) {
+            F3 wi = spherical_direction(v * kPi, u * 2.f * kPi);
+            wi = f3(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
+                    0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+            float th, ph;
+            spherical_coordinates(wi, th, ph);
+            u = ph / (2.f * kPi);
+            v = th / kPi;
+        } else {
+            u += t.ou;
+            v += t.ov;
+        }
+        return png_lookup(S.texels + t.off, (unsigned)t.w, (unsigned)t.h, t.su, t.sv, u, v);
+    }
+    return f3(t.v1r, t.v1g, t.v1b);
+}
+// the diffuse albedo of BSDF b at uv: its constant colour unless it has a texture
+__device__ __forceinline__ F3 bsdf_albedo(const DScene &S, const DBsdf &b, float u, float v) {
+    if (__builtin_expect(b.tex != 0, 0)) return tex_eval(S, b.tex - 1, u, v);
+    return f3(b.ar, b.ag, b.ab);
+}
+
 __device__ __forceinline__ F3 env_tex(const DScene &S, float u, float v) {
     if (S.env_constant) {
         const float4 c = S.env_rgba[0];
@@ -95,12 +142,7 @@ __device__ __forceinline__ F3 env_tex(const DScene &S, float u, float v) {
         u += S.env_ou;
         v += S.env_ov;
     }
-    const unsigned W = (unsigned)S.env_w, H = (unsigned)S.env_h;
-    const float fu = u * S.env_su * (float)W, fv = v * S.env_sv * (float)H;
-    const unsigned w = fu > 0.f ? (unsigned)fu : 0u, hh = fv > 0.f ? (unsigned)fv : 0u;
-    const unsigned h = H - hh;
-    const float4 c = S.env_rgba[(h * W + w) % (W * H)];
-    return f3(c.x, c.y, c.z);
+    return png_lookup(S.env_rgba, (unsigned)S.env_w, (unsigned)S.env_h, S.env_su, S.env_sv, u, v);
 }
 __device__ __forceinline__ F3 env_eval(const DScene &S, F3 wi) {  // EnvMap::eval
     float th, ph;

@@ -719,7 +719,7 @@ bool splat_uses_staging(int border, int reach) {
 
 void launch_splat(const SplatLaunch &P, hipStream_t st) {
     const bool tabulated = splat_knob("NH_SPLAT_TAB"), strip = splat_knob("NH_SPLAT_STRIP");
-    if (!splat_uses_staging(P.border, P.reach)) {  // splat + merge in one pass, no block staging
+    if (!P.staged) {  // splat + merge in one pass, no block staging
         const int n_tiles = P.nbx * ((P.height + 31) / 32);
         SplatLaunch Q = P;
         if (const char *e = std::getenv("NH_SPLAT_DEBUG")) Q.debug = std::atoi(e);
@@ -740,7 +740,8 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
         const char *d = std::getenv("NH_SPLAT_DIRECT");  // opt-in until measured
         Q.direct = d && d[0] == '1' ? 1 : 0;
         const char *rv = std::getenv("NH_SPLAT_ROUNDS");  // rounds per workgroup: 1, 2, 4 (default) or 8
-        const int tr = rv ? std::atoi(rv) : kTabRounds;
+        int tr = rv ? std::atoi(rv) : kTabRounds;
+        if (tr != 1 && tr != 2 && tr != 4 && tr != 8) tr = kTabRounds;  // 0 / garbage: the default (no 0 divisor)
         const dim3 g(P.n_blocks, (P.n_rounds + tr - 1) / tr);
         if (Q.direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
         else if (tr == 1) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 1>), g, dim3(256), 0, st, Q);

@@ -519,12 +519,13 @@ __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv,
                                            bool &nee, float4 &so, float4 &sd) {
     const DShape shape = S.shapes[its.shape];
     const DBsdf bsdf = S.bsdfs[shape.bsdf];
+    const F3 alb = bsdf_albedo(S, bsdf, its.u, its.v);
     nee = false;
     if (S.integrator == 1) {  // path_mats: BSDF sample only
         const float bx = v.rng.next1d(), by = v.rng.next1d();
         F3 wo;
         int measure;
-        const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(v.d)), bx, by, wo, measure);
+        const F3 col = bsdf_sample(bsdf, to_local(its.sh, neg(v.d)), bx, by, wo, measure, alb);
         const F3 nd = to_world(its.sh, wo);
         v.t = mulc(v.t, col);  // path_mats.cpp: the throughput update of this bounce
         o.pdfmat = 0.f;
@@ -544,7 +545,7 @@ __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv,
         float pdfems = 0.f, pdfems_mats = 0.f;
         if (nee) {
             const F3 we = to_local(its.sh, es.wi);
-            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE);
+            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE, alb);
             const float cs = we.z;
             li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights, ems_col.z * cs * f.z * n_lights);
             pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
@@ -555,7 +556,7 @@ __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv,
         const float bx = v.rng.next1d(), by = v.rng.next1d();
         F3 wo;
         int measure;
-        const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure);
+        const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure, alb);
         const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
         const F3 nd = to_world(its.sh, wo);
         // w_ems of this bounce (:103-106): the occluded shadow ray leaves both pdfs 0 (w_ems keeps its

@@ -127,12 +127,13 @@ V3 to_v3(const std::string &s) {
 // PropertyList (src/utils/proplist.cpp)
 // ---------------------------------------------------------------------------
 struct Prop {
-    enum Kind { Bool, Int, Float, String, Point, Vector, Color, Transform } kind;
+    enum Kind { Bool, Int, Float, String, Point, Vector, Color, Transform, Point2, Vector2 } kind;
     bool b = false;
     int i = 0;
     float f = 0;
     std::string s;
     V3 v;
+    float v2[2] = {0, 0};  // Point2 / Vector2 (parser.cpp:268-294: <point> / <vector> of 2 components)
     M4 t;
 };
 
@@ -172,6 +173,16 @@ struct PropList {
     M4 get_transform(const std::string &n, const M4 &def) const { auto p = get(n, Prop::Transform); return p ? p->t : def; }
     bool get_bool(const std::string &n, bool def) const { auto p = get(n, Prop::Bool); return p ? p->b : def; }
     V3 get_vector(const std::string &n, V3 def) const { auto p = get(n, Prop::Vector); return p ? p->v : def; }
+    void get_point2(const std::string &n, float def0, float def1, float out[2]) const {
+        auto p = get(n, Prop::Point2);
+        out[0] = p ? p->v2[0] : def0;
+        out[1] = p ? p->v2[1] : def1;
+    }
+    void get_vector2(const std::string &n, float def0, float def1, float out[2]) const {
+        auto p = get(n, Prop::Vector2);
+        out[0] = p ? p->v2[0] : def0;
+        out[1] = p ? p->v2[1] : def1;
+    }
 };
 
 // ---------------------------------------------------------------------------
@@ -216,6 +227,8 @@ struct SceneData {
     std::vector<float> area_cdf;
     nh_envmap env{};
     std::vector<float> env_rgba, env_cdf;
+    std::vector<nh_texture> textures;  // BSDF albedo textures (nh_bsdf.albedo_texture = index + 1)
+    std::vector<float> texels;         // RGBA texels of the png textures
     nh_denoiser denoiser{};  // type NH_DENOISER_NONE unless the scene has a <denoiser>
     // camera parameters kept for re-projection on resize
     float fov = 30.f, near_clip = 1e-4f, far_clip = 1e4f, focal = 10.f, fstop = 0.f, lens = 0.f;
@@ -329,10 +342,20 @@ std::unique_ptr<Obj> parse_node(const XmlNode &n, PropList *parent_props, const 
     else if (n.name == "float") { p.kind = Prop::Float; p.f = to_float(val); }
     else if (n.name == "string") { p.kind = Prop::String; p.s = val; }
     else if (n.name == "point" || n.name == "vector") {
+        // parser.cpp:268-294: two components make a Point2f / Vector2f, three a Point3f / Vector3f
         auto tk = tokenize(val);
-        if (tk.size() != 3) throw SceneError(n.name + " \"" + name + "\" must have 3 components");
-        p.kind = n.name == "point" ? Prop::Point : Prop::Vector;
-        p.v = to_v3(val);
+        const bool pt = n.name == "point";
+        if (tk.size() == 2) {
+            p.kind = pt ? Prop::Point2 : Prop::Vector2;
+            p.v2[0] = to_float(tk[0]);
+            p.v2[1] = to_float(tk[1]);
+        } else if (tk.size() == 3) {
+            p.kind = pt ? Prop::Point : Prop::Vector;
+            p.v = to_v3(val);
+        } else {
+            throw SceneError(std::string(pt ? "Point" : "Vector") + " " + name + " (value: " + val +
+                             ") is not of size 2 or 3");
+        }
     } else if (n.name == "color") { p.kind = Prop::Color; p.v = to_v3(val); }
     parent_props->set(name, p);
     return nullptr;
@@ -575,15 +598,69 @@ void camera_update(SceneData &sd) {
 
 namespace {
 
-nh_bsdf make_bsdf(const Obj &o) {
+// PNGTexture::loadFromFile for sRGB images (PNGTexture.cpp:70-84): lodepng RGBA8 -> InverseGammaCorrect(v / 255)
+void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w, unsigned &h);
+
+// A Texture<Color3f> child (src/textures/consttexture.cpp, checkerboard.cpp, PNGTexture.cpp) -> nh_texture
+nh_texture make_texture(const Obj &t, const std::string &base_dir, SceneData &sd) {
+    nh_texture x{};
+    const PropList &p = t.props;
+    if (t.type == "constant_color") {  // ConstantTexture<Color3f>: value [0]
+        x.type = NH_TEXTURE_CONSTANT;
+        V3 c = p.get_color("value", v3(0, 0, 0));
+        x.value1[0] = c.x; x.value1[1] = c.y; x.value1[2] = c.z;
+    } else if (t.type == "checkerboard_color") {  // Checkerboard<Color3f> (checkerboard.cpp:80-87)
+        x.type = NH_TEXTURE_CHECKERBOARD;
+        p.get_point2("delta", 0.f, 0.f, x.delta);
+        p.get_vector2("scale", 1.f, 1.f, x.scale);
+        V3 a = p.get_color("value1", v3(0, 0, 0)), b = p.get_color("value2", v3(1, 1, 1));
+        x.value1[0] = a.x; x.value1[1] = a.y; x.value1[2] = a.z;
+        x.value2[0] = b.x; x.value2[1] = b.y; x.value2[2] = b.z;
+    } else if (t.type == "png_texture") {  // PNGTexture (PNGTexture.cpp:23-34, 125-160)
+        x.type = NH_TEXTURE_PNG;
+        if (!p.get_bool("sRGB", p.get_string("name", "") != "normal"))
+            throw SceneError("png_texture: normal-map (sRGB=false) lookups are not supported as an albedo");
+        V3 eul = p.get_vector("eulerAngles", v3(0, 0, 0));
+        x.spherical = p.get_bool("sphericalTexture", false) ? 1 : 0;
+        if (x.spherical && (eul.x != 0 || eul.y != 0 || eul.z != 0))
+            throw SceneError("png_texture: eulerAngles are not supported");
+        x.scale_u = p.get_float("scaleU", 1.f);
+        x.scale_v = p.get_float("scaleV", 1.f);
+        x.offset_u = p.get_float("offsetU", 0.f);
+        x.offset_v = p.get_float("offsetV", 0.f);
+        unsigned w = 0, h = 0;
+        std::vector<float> px;
+        load_png_texels(join_path(base_dir, p.get_string("filename")), px, w, h);
+        x.width = (int32_t)w;
+        x.height = (int32_t)h;
+        x.texel_offset = sd.texels.size() / 4;
+        sd.texels.insert(sd.texels.end(), px.begin(), px.end());
+    } else {
+        throw SceneError("texture \"" + t.type + "\" is not supported as a diffuse albedo");
+    }
+    return x;
+}
+
+nh_bsdf make_bsdf(const Obj &o, const std::string &base_dir, SceneData &sd) {
     nh_bsdf b{};
     const PropList &p = o.props;
     if (o.type == "diffuse") {
+        // Diffuse (diffuse.cpp:32-91): an "albedo" colour becomes a constant texture; a <texture name="albedo">
+        // child is the albedo otherwise; neither: the constant 0.5 fallback of cloneAndInit
         b.type = NH_BSDF_DIFFUSE;
-        for (auto &ch : o.children)
-            if (ch->tag == "texture") throw SceneError("textured diffuse albedo is not supported yet");
+        const bool has_color = p.has("albedo");
         V3 a = p.get_color("albedo", v3(0.5f, 0.5f, 0.5f));
         b.albedo[0] = a.x; b.albedo[1] = a.y; b.albedo[2] = a.z;
+        bool have = has_color;
+        for (auto &ch : o.children) {
+            if (ch->tag != "texture") throw SceneError("Diffuse::addChild(<" + ch->tag + ">) is not supported!");
+            if (ch->props.get_string("name", "") != "albedo")
+                throw SceneError("The name of this texture does not match any field!");
+            if (have) throw SceneError("There is already an albedo defined!");
+            have = true;
+            sd.textures.push_back(make_texture(*ch, base_dir, sd));
+            b.albedo_texture = (uint32_t)sd.textures.size();
+        }
     } else if (o.type == "mirror") {
         b.type = NH_BSDF_MIRROR;
     } else if (o.type == "dielectric") {
@@ -637,6 +714,23 @@ float inverse_gamma(float x) {  // PNGTexture.cpp:442-447
     return (float)std::pow((double)((x + 0.055f) * 1.f / 1.055f), (double)2.4f);
 }
 
+void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w, unsigned &h) {
+    const auto dot = fn.find_last_of('.');
+    const std::string ext = dot == std::string::npos ? std::string() : fn.substr(dot);
+    if (ext == ".hdr") throw SceneError("PNGTexture: .hdr images (HDRLoader) are not supported by the HIP path");
+    if (ext != ".png") throw SceneError("PNGTexture: file extension " + ext + " unknown.");
+    if (!std::ifstream(fn).good()) throw SceneError("PNGTexture: image file not found " + fn);
+    std::vector<uint8_t> px;
+    std::string err;
+    if (!png_decode_rgba8(fn, px, w, h, err)) throw SceneError("PNGTexture: " + err);
+    out.resize(px.size());
+    for (size_t i = 0; i < px.size(); ++i) out[i] = inverse_gamma(static_cast<float>(px[i]) / 255.f);
+}
+
+// static_cast<unsigned int>(float) as the reference's x86-64 build executes it: cvttss2si to 64 bits and the low
+// word (trunc(x) mod 2^32 for |x| < 2^63, else 0) -- stated explicitly, the C++ cast is undefined for such values
+unsigned x86_f2u(float x) { return std::fabs(x) < 0x1p63f ? (unsigned)(uint64_t)(int64_t)x : 0u; }
+
 // PNGTexture::eval (PNGTexture.cpp:125-160) / ConstantTexture::eval; eulerAngles = 0 only
 V3 env_tex_eval(const nh_envmap &e, const float *rgba, float u, float v) {
     if (e.constant) return v3(rgba[0], rgba[1], rgba[2]);
@@ -654,9 +748,8 @@ V3 env_tex_eval(const nh_envmap &e, const float *rgba, float u, float v) {
         v += e.offset_v;
     }
     const unsigned W = (unsigned)e.width, H = (unsigned)e.height;
-    const float fu = u * e.scale_u * (float)W, fv = v * e.scale_v * (float)H;
-    const unsigned w = fu > 0.f ? (unsigned)fu : 0u, hh = fv > 0.f ? (unsigned)fv : 0u;
-    const unsigned h = H - hh;
+    const unsigned w = x86_f2u(u * e.scale_u * (float)W);
+    const unsigned h = H - x86_f2u(v * e.scale_v * (float)H);
     const unsigned index = (h * W + w) % (W * H);
     return v3(rgba[4 * (size_t)index], rgba[4 * (size_t)index + 1], rgba[4 * (size_t)index + 2]);
 }
@@ -694,18 +787,10 @@ void build_envmap(const Obj &o, const std::string &base_dir, SceneData &sd, nh_e
         e.offset_u = p.get_float("offsetU", 0.f);
         e.offset_v = p.get_float("offsetV", 0.f);
         e.spherical = p.get_bool("sphericalTexture", false) ? 1 : 0;
-        const auto dot = fn.find_last_of('.');
-        if (dot == std::string::npos || fn.substr(dot) != ".png")
-            throw SceneError("PNGTexture: file extension " + (dot == std::string::npos ? std::string() : fn.substr(dot)) +
-                             " unknown.");
-        std::vector<uint8_t> px;
         unsigned w = 0, h = 0;
-        std::string err;
-        if (!png_decode_rgba8(fn, px, w, h, err)) throw SceneError("PNGTexture: " + err);
+        load_png_texels(fn, sd.env_rgba, w, h);
         e.width = (int32_t)w;
         e.height = (int32_t)h;
-        sd.env_rgba.resize(px.size());
-        for (size_t i = 0; i < px.size(); ++i) sd.env_rgba[i] = inverse_gamma(static_cast<float>(px[i]) / 255.f);
     } else {
         throw SceneError("texture \"" + tex->type + "\" is not supported for environment maps");
     }
@@ -785,7 +870,7 @@ void build_scene(const Obj &scene, const std::string &base_dir, SceneData &sd) {
             for (auto &sc : ch.children) {
                 if (sc->tag == "bsdf") {
                     if (bsdf >= 0) throw SceneError("Shape: tried to register multiple BSDF instances");
-                    sd.bsdfs.push_back(make_bsdf(*sc));
+                    sd.bsdfs.push_back(make_bsdf(*sc, base_dir, sd));
                     bsdf = (int)sd.bsdfs.size() - 1;
                 } else if (sc->tag == "emitter") {
                     if (emitter >= 0) throw SceneError("Shape: tried to register multiple Emitter instances");
@@ -945,6 +1030,10 @@ void fill_desc(const SceneData &sd, nh_scene_desc *d) {
     d->F = sd.F.data();
     d->n_area_cdf = (uint32_t)sd.area_cdf.size();
     d->area_cdf = sd.area_cdf.data();
+    d->n_textures = (uint32_t)sd.textures.size();
+    d->textures = sd.textures.data();
+    d->n_texels = sd.texels.size() / 4;
+    d->texels = sd.texels.data();
     if (sd.envmap >= 0) {
         d->env = sd.env;
         d->env.rgba = sd.env_rgba.data();
@@ -1005,6 +1094,22 @@ int nh_scene_set_bsdf(nh_scene *scene, uint32_t shape, const nh_bsdf *bsdf) {
     scene->data->bsdfs.push_back(*bsdf);
     scene->data->shapes[shape].bsdf = (int32_t)scene->data->bsdfs.size() - 1;
     return NH_OK;
+}
+
+uint32_t nh_scene_add_texture(nh_scene *scene, const nh_texture *tex, const float *texels) {
+    if (!scene || !tex || tex->type < NH_TEXTURE_CONSTANT || tex->type > NH_TEXTURE_PNG) {
+        nh::set_host_error("invalid texture");
+        return 0;
+    }
+    nh_texture t = *tex;
+    if (t.type == NH_TEXTURE_PNG) {
+        if (!texels || t.width <= 0 || t.height <= 0) { nh::set_host_error("png texture without texels"); return 0; }
+        auto &v = scene->data->texels;
+        t.texel_offset = v.size() / 4;
+        v.insert(v.end(), texels, texels + (size_t)t.width * (size_t)t.height * 4);
+    }
+    scene->data->textures.push_back(t);
+    return (uint32_t)scene->data->textures.size();
 }
 
 int nh_scene_set_integrator(nh_scene *scene, int32_t integrator) {

@@ -23,17 +23,9 @@ LIB_PATH = os.environ.get("NH_LIB_PATH") or os.path.join(_HERE, "lib", "libnori_
 
 # The wavefront pipeline drives up to three path pools on their own streams; each needs its own hardware
 # queue, or one pool's long tail kernel blocks another's bounces (HIP's default is 4 queues per process, one
-# of which the context's own stream takes). Read once by the HIP runtime when it initialises.
-def _raise_hw_queues(n=8):
-    try:
-        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
-    except ValueError:
-        cur = 0
-    if cur < n:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(n)
-
-
-_raise_hw_queues()
+# of which the context's own stream takes). Read once by the HIP runtime when it initialises. Set only when
+# the user or operator has not set it: an explicit value is respected.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"nori_hip: HIP library not built ({LIB_PATH}); run `make` or __graft_entry__.build()")
@@ -65,7 +57,16 @@ class nh_shape(C.Structure):
 
 class nh_bsdf(C.Structure):
     _fields_ = [("type", _i32), ("albedo", _f * 3), ("alpha", _f), ("int_ior", _f), ("ext_ior", _f),
-                ("kd", _f * 3), ("ks", _f)]
+                ("kd", _f * 3), ("ks", _f), ("albedo_texture", _u32)]
+
+
+TEXTURE_CONSTANT, TEXTURE_CHECKERBOARD, TEXTURE_PNG = 0, 1, 2
+
+
+class nh_texture(C.Structure):
+    _fields_ = [("type", _i32), ("value1", _f * 3), ("value2", _f * 3), ("delta", _f * 2), ("scale", _f * 2),
+                ("width", _i32), ("height", _i32), ("texel_offset", C.c_uint64), ("scale_u", _f), ("scale_v", _f),
+                ("offset_u", _f), ("offset_v", _f), ("spherical", _i32), ("pad", _i32)]
 
 
 class nh_emitter(C.Structure):
@@ -116,7 +117,8 @@ class nh_scene_desc(C.Structure):
                 ("bsdfs", C.POINTER(nh_bsdf)), ("n_emitters", _u32), ("emitters", C.POINTER(nh_emitter)),
                 ("emitter_cdf", _fp), ("envmap", _i32), ("n_vertices", _u32), ("V", _fp), ("N", _fp),
                 ("UV", _fp), ("T", _fp), ("BT", _fp), ("n_faces", _u32), ("F", _u32p), ("n_area_cdf", _u32),
-                ("area_cdf", _fp), ("env", nh_envmap), ("denoiser", nh_denoiser)]
+                ("area_cdf", _fp), ("env", nh_envmap), ("denoiser", nh_denoiser), ("n_textures", _u32),
+                ("textures", C.POINTER(nh_texture)), ("n_texels", C.c_uint64), ("texels", _fp)]
 
 
 class nh_bvh_node(C.Structure):
@@ -159,7 +161,8 @@ class nh_render_stats(C.Structure):
         (n, C.c_uint64) for n in ("tail_queries", "tail_nodes_visited", "tail_boxes_tested", "tail_prims_tested",
                                   "tail_shadow_queries", "tail_shadow_nodes_visited", "tail_shadow_boxes_tested",
                                   "tail_shadow_prims_tested", "lds_scene", "fused_bounce", "comm_inits")] + [
-        ("kernel_ms_denoise", C.c_double), ("launches_denoise", C.c_uint64), ("tails_async", C.c_uint64)]
+        ("kernel_ms_denoise", C.c_double), ("launches_denoise", C.c_uint64), ("tails_async", C.c_uint64),
+        ("pools_active", C.c_uint64)]
 
 
 def _sig(name, res, *args):
@@ -177,6 +180,7 @@ _sig("nh_scene_set_resolution", _i32, _vp, _i32, _i32)
 _sig("nh_scene_set_sample_count", _i32, _vp, _i32)
 _sig("nh_scene_set_bsdf", _i32, _vp, _u32, C.POINTER(nh_bsdf))
 _sig("nh_scene_set_integrator", _i32, _vp, _i32)
+_sig("nh_scene_add_texture", _u32, _vp, C.POINTER(nh_texture), _fp)
 _sig("nh_scene_free", None, _vp)
 _sig("nh_host_last_error", C.c_char_p)
 _sig("nh_debug_transform", _i32, C.c_char_p, _fp, _i32)
@@ -266,7 +270,31 @@ class Scene:
         m = kdf[1] if not (kdf[1] < kdf[2]) else kdf[2]
         m = kdf[0] if not (kdf[0] < m) else m
         b.ks = float(np.float32(1) - np.float32(m))
+        b.albedo_texture = kw.get("albedo_texture", 0)
         _host_check(_lib.nh_scene_set_bsdf(self._h, shape, C.byref(b)), "set_bsdf")
+
+    def add_texture(self, type: int, value1=(0, 0, 0), value2=(1, 1, 1), delta=(0, 0), scale=(1, 1), texels=None,
+                    scale_uv=(1, 1), offset_uv=(0, 0), spherical=False) -> int:
+        """Append an albedo texture (nh_scene_add_texture); returns the nh_bsdf.albedo_texture value naming it.
+        texels: (H, W, 4) float32 RGBA for TEXTURE_PNG (already sRGB-decoded, row 0 first)."""
+        t = nh_texture()
+        t.type = type
+        for i in range(3):
+            t.value1[i], t.value2[i] = value1[i], value2[i]
+        t.delta[0], t.delta[1] = delta
+        t.scale[0], t.scale[1] = scale
+        t.scale_u, t.scale_v = scale_uv
+        t.offset_u, t.offset_v = offset_uv
+        t.spherical = int(spherical)
+        ptr = None
+        if texels is not None:
+            tx = np.ascontiguousarray(texels, dtype=np.float32)
+            t.height, t.width = tx.shape[0], tx.shape[1]
+            ptr = _fptr(tx)
+        idx = _lib.nh_scene_add_texture(self._h, C.byref(t), ptr)
+        if idx == 0:
+            raise NoriError(f"add_texture: {_lib.nh_host_last_error().decode()}")
+        return idx
 
     @property
     def width(self):

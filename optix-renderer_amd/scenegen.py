@@ -17,14 +17,20 @@ import numpy as np
 
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIXTURE = os.path.join(_REPO, "tests", "golden", "reference_scenes.json")
+TEXTURED_FIXTURE = os.path.join(_REPO, "tests", "golden", "textured_scenes.json.gz")
 
 C2_ALBEDO = "0.725 0.71 0.68"
 
 
 def materialize(out_dir: str) -> str:
-    """Write the reference scene fixtures under out_dir; returns out_dir."""
+    """Write the reference scene fixtures (reference_scenes.json and the textured scenes of
+    textured_scenes.json.gz) under out_dir; returns out_dir."""
     with open(FIXTURE) as f:
         files = json.load(f)
+    if os.path.exists(TEXTURED_FIXTURE):
+        import gzip
+        with gzip.open(TEXTURED_FIXTURE, "rt") as f:
+            files.update(json.load(f))
     for rel, text in files.items():
         p = os.path.join(out_dir, rel)
         os.makedirs(os.path.dirname(p), exist_ok=True)
@@ -34,16 +40,22 @@ def materialize(out_dir: str) -> str:
 
 
 def cbox_xml(out_dir: str, variant: str = "c1", width: int | None = None, height: int | None = None,
-             spp: int | None = None, extra_shapes: str = "", drop_spheres: bool = False, denoiser: str = "") -> str:
+             spp: int | None = None, extra_shapes: str = "", drop_spheres: bool = False, denoiser: str = "",
+             walls_bsdf: str = "") -> str:
     """Cornell box scene file. variant: c1/c4 = reference (mirror + dielectric spheres),
     c2 = both spheres diffuse (albedo of the walls), as SURVEY.md 8(d) defines. denoiser: a
-    <denoiser> element to add (scenes/project/denoiser/denoiser-test.xml:28-32 form)."""
+    <denoiser> element to add (scenes/project/denoiser/denoiser-test.xml:28-32 form). walls_bsdf: a <bsdf>
+    element replacing the one of walls.obj (floor, ceiling, back wall), e.g. a textured diffuse."""
     materialize(out_dir)
     src = os.path.join(out_dir, "scenes/pa4/cbox/cbox_path_mis.xml")
     text = open(src).read()
     if variant == "c2":
         text = text.replace('<bsdf type="mirror"/>', f'<bsdf type="diffuse"><color name="albedo" value="{C2_ALBEDO}"/></bsdf>')
         text = text.replace('<bsdf type="dielectric"/>', f'<bsdf type="diffuse"><color name="albedo" value="{C2_ALBEDO}"/></bsdf>')
+    if walls_bsdf:
+        old = '<bsdf type="diffuse">\n\t\t\t<color name="albedo" value="0.725 0.71 0.68"/>\n\t\t</bsdf>'
+        assert text.count(old) == 1
+        text = text.replace(old, walls_bsdf)
     if drop_spheres:
         import re
         text = re.sub(r'<shape type="sphere">.*?</shape>', "", text, flags=re.S)
@@ -57,7 +69,7 @@ def cbox_xml(out_dir: str, variant: str = "c1", width: int | None = None, height
         text = text.replace('<integer name="height" value="600"/>', f'<integer name="height" value="{height}"/>')
     if spp:
         text = text.replace('<integer name="sampleCount" value="512"/>', f'<integer name="sampleCount" value="{spp}"/>')
-    key = repr((width, height, spp, extra_shapes, drop_spheres, denoiser)).encode()
+    key = repr((width, height, spp, extra_shapes, drop_spheres, denoiser, walls_bsdf)).encode()
     name = f"cbox_{variant}_{hashlib.sha1(key).hexdigest()[:10]}.xml"
     dst = os.path.join(out_dir, "scenes/pa4/cbox", name)
     with open(dst, "w") as f:

@@ -259,7 +259,14 @@ struct BRec {
     V3 wi, wo = mk(0, 0, 0);  // Nori vectors zero-initialise (vector.h:49)
     float eta = 1.0f;
     Measure measure = EUnknown;
+    // BSDFQueryRecord::uv (bsdf.h:58), set to its.uv by every integrator (path_mis.cpp:92/:110, path_mats.cpp:64,
+    // direct*.cpp), and the scene whose texture table a textured albedo indexes
+    float u = 0.f, v = 0.f;
+    const ::no_scene *scene = nullptr;
 };
+
+// m_albedo->eval(bRec.uv) (diffuse.cpp:101, :139): the constant albedo or the BSDF's texture
+V3 diffuse_albedo(const nh_bsdf &b, const BRec &r);
 
 inline float tan_theta(V3 v) {  // frame.h:76-82
     float temp = 1 - v.z * v.z;
@@ -284,7 +291,7 @@ V3 bsdf_eval(const nh_bsdf &b, const BRec &r) {
     switch (b.type) {
         case NH_BSDF_DIFFUSE:  // diffuse.cpp:94-103
             if (r.measure != ESolidAngle || r.wi.z <= 0 || r.wo.z <= 0) return mk(0, 0, 0);
-            return mk(b.albedo[0], b.albedo[1], b.albedo[2]) * kInvPi;
+            return diffuse_albedo(b, r) * kInvPi;
         case NH_BSDF_MICROFACET: {  // microfacet.cpp:92-105
             if (r.wo.z < 0.f) return mk(0, 0, 0);
             V3 wh = normalized(r.wi + r.wo);
@@ -321,7 +328,7 @@ V3 bsdf_sample(const nh_bsdf &b, BRec &r, float sx, float sy) {
             r.measure = ESolidAngle;
             r.wo = square_to_cosine_hemisphere(sx, sy);
             r.eta = 1.0f;
-            return mk(b.albedo[0], b.albedo[1], b.albedo[2]);
+            return diffuse_albedo(b, r);
         case NH_BSDF_MIRROR:  // mirror.cpp:41-57
             if (r.wi.z <= 0) return mk(0, 0, 0);
             r.wo = mk(-r.wi.x, -r.wi.y, r.wi.z);
@@ -409,6 +416,8 @@ struct no_scene {
     nh_envmap env{};              // scalar parameters (pointers below)
     std::vector<float> env_rgba;  // PNGTexture::data
     std::vector<float> env_cdf;   // EnvMap::calculateProbs, recomputed here (no_env_cdf)
+    std::vector<nh_texture> textures;  // BSDF albedo textures (nh_bsdf.albedo_texture = index + 1)
+    std::vector<float> texels;         // RGBA texels of the png textures
     std::vector<uint32_t> shape_offset;
     std::vector<BNode> nodes;
     std::vector<uint32_t> indices;
@@ -621,6 +630,16 @@ void spherical_coordinates(V3 v, float &theta, float &phi) {  // common.cpp:283-
     phi = f_atan2(v.y, v.x);
     if (phi < 0) phi += 2 * kPi;
 }
+// the texel lookup of PNGTexture::eval (PNGTexture.cpp:147-155), written as the reference writes it: the float ->
+// unsigned casts are compiled by g++ for x86-64 (cvttss2si to 64 bits, low word: trunc(x) mod 2^32 for
+// |x| < 2^63, else 0), which is what the reference binary executes for negative or huge products
+V3 png_lookup(const float *d, unsigned width, unsigned height, float scale_u, float scale_v, float u, float v) {
+    unsigned int w = static_cast<unsigned int>((u) * scale_u * (float)width);
+    unsigned int h = height - static_cast<unsigned int>((v) * scale_v * (float)height);
+    unsigned int index = (h * width + w) % (width * height);
+    return mk(d[4 * (size_t)index], d[4 * (size_t)index + 1], d[4 * (size_t)index + 2]);
+}
+
 V3 env_tex_eval(const no_scene &s, float u, float v) {
     const float *d = s.env_rgba.data();
     if (s.env.constant) return mk(d[0], d[1], d[2]);  // ConstantTexture::eval
@@ -637,12 +656,7 @@ V3 env_tex_eval(const no_scene &s, float u, float v) {
         u += s.env.offset_u;
         v += s.env.offset_v;
     }
-    const unsigned W = (unsigned)s.env.width, H = (unsigned)s.env.height;
-    const float fu = u * s.env.scale_u * (float)W, fv = v * s.env.scale_v * (float)H;
-    const unsigned w = fu > 0.f ? (unsigned)fu : 0u, hh = fv > 0.f ? (unsigned)fv : 0u;
-    const unsigned h = H - hh;
-    const unsigned index = (h * W + w) % (W * H);
-    return mk(d[4 * (size_t)index], d[4 * (size_t)index + 1], d[4 * (size_t)index + 2]);
+    return png_lookup(d, (unsigned)s.env.width, (unsigned)s.env.height, s.env.scale_u, s.env.scale_v, u, v);
 }
 V3 env_eval(const no_scene &s, V3 wi) {  // EnvMap::eval
     float th, ph;
@@ -655,6 +669,49 @@ float env_pdf(const no_scene &s, V3 wi) {  // EnvMap::pdf
     if (s.env.width == 1 && s.env.height == 1) return sphere_pdf;
     return luminance(env_eval(s, wi)) * s.env.normalization / sphere_pdf * (float)(unsigned)s.env.height *
            (float)(unsigned)s.env.width;
+}
+
+// Texture<Color3f>::eval of a BSDF albedo (src/textures/consttexture.cpp, checkerboard.cpp:29-47,
+// PNGTexture.cpp:125-160)
+V3 texture_eval(const no_scene &s, const nh_texture &t, float u, float v) {
+    if (t.type == NH_TEXTURE_CHECKERBOARD) {
+        float ox = u / t.scale[0] - t.delta[0];
+        float oy = v / t.scale[1] - t.delta[1];
+        // int(float) as the x86-64 reference executes it (cvttss2si: NaN / out of range -> INT_MIN)
+        int x = int(ox) + (ox < 0.f);
+        int y = int(oy) + (oy < 0.f);
+        // (x + y) % 2 == 0 with the reference's wrap-around int addition
+        if ((int)((unsigned)x + (unsigned)y) % 2 == 0) return mk(t.value1[0], t.value1[1], t.value1[2]);
+        return mk(t.value2[0], t.value2[1], t.value2[2]);
+    }
+    if (t.type == NH_TEXTURE_PNG) {
+        if (t.spherical) {
+            V3 wi = spherical_direction(v * kPi, u * 2.f * kPi);
+            wi = mk(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
+                    0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+            float th, ph;
+            spherical_coordinates(wi, th, ph);
+            u = ph / (2.f * kPi);
+            v = th / kPi;
+        } else {
+            u += t.offset_u;
+            v += t.offset_v;
+        }
+        return png_lookup(s.texels.data() + 4 * (size_t)t.texel_offset, (unsigned)t.width, (unsigned)t.height,
+                          t.scale_u, t.scale_v, u, v);
+    }
+    return mk(t.value1[0], t.value1[1], t.value1[2]);
+}
+
+V3 diffuse_albedo(const nh_bsdf &b, const BRec &r) {
+    if (b.albedo_texture == 0 || !r.scene) return mk(b.albedo[0], b.albedo[1], b.albedo[2]);
+    return texture_eval(*r.scene, r.scene->textures[b.albedo_texture - 1], r.u, r.v);
+}
+// bRec.uv = its.uv
+inline void set_uv(BRec &r, const no_scene &s, const Its &its) {
+    r.u = its.u;
+    r.v = its.v;
+    r.scene = &s;
 }
 
 size_t dpdf_sample(const float *cdf, size_t n_cdf, float x) {  // dpdf.h:124-130
@@ -776,6 +833,7 @@ V3 li_path_mis(const no_scene &s, Sampler &smp, const Ray &ray) {  // path_mis.c
             Its dummy;
             if (!bvh_intersect(s, eqr_ems.shadow, dummy, true)) {
                 BRec bq;
+                set_uv(bq, s, its);
                 bq.wi = its.sh.to_local(-trace.d);
                 bq.wo = we;
                 bq.measure = ESolidAngle;
@@ -789,6 +847,7 @@ V3 li_path_mis(const no_scene &s, Sampler &smp, const Ray &ray) {  // path_mis.c
         if ((pdfems_mats + pdfems) > kEps) w_ems = pdfems / (pdfems_mats + pdfems);
 
         BRec br;
+        set_uv(br, s, its);
         br.wi = its.sh.to_local(-trace.d);
         float bx, by;
         smp.next2d(bx, by);
@@ -838,6 +897,7 @@ V3 li_path_mats(const no_scene &s, Sampler &smp, const Ray &ray) {  // path_mats
         else if (smp.next1d() > succ) break;
         else t = t / succ;
         BRec br;
+        set_uv(br, s, its);
         br.wi = its.sh.to_local(-trace.d);
         br.measure = ESolidAngle;
         float bx, by;
@@ -879,6 +939,7 @@ V3 li_direct_ems(const no_scene &s, Sampler &smp, const Ray &ray) {  // direct_e
         Its dummy;
         if (bvh_intersect(s, eqr.shadow, dummy, true)) continue;
         BRec bq;
+        set_uv(bq, s, its);
         bq.wi = wo;
         bq.wo = its.sh.to_local(eqr.wi);
         bq.measure = ESolidAngle;
@@ -894,6 +955,7 @@ V3 li_direct_mats(const no_scene &s, Sampler &smp, const Ray &ray) {  // direct_
     if (!direct_first_hit(s, ray, its, result)) return result;
     const nh_bsdf &bsdf = s.bsdfs[s.shapes[its.shape].bsdf];
     BRec br;
+    set_uv(br, s, its);
     br.wi = its.sh.to_local(-ray.d);
     br.measure = ESolidAngle;
     float bx, by;
@@ -930,6 +992,7 @@ V3 li_direct_mis(const no_scene &s, Sampler &smp, const Ray &ray) {  // direct_m
         Its dummy;
         if (!bvh_intersect(s, eqr.shadow, dummy, true)) {
             BRec bq;
+            set_uv(bq, s, its);
             bq.wi = its.sh.to_local(-ray.d);
             bq.wo = its.sh.to_local(eqr.wi);
             bq.measure = ESolidAngle;
@@ -944,6 +1007,7 @@ V3 li_direct_mis(const no_scene &s, Sampler &smp, const Ray &ray) {  // direct_m
         }
     }
     BRec bm;
+    set_uv(bm, s, its);
     bm.wi = its.sh.to_local(-ray.d);
     bm.measure = ESolidAngle;
     float bx, by;
@@ -985,6 +1049,7 @@ V3 li_direct(const no_scene &s, Sampler &smp, const Ray &ray) {
         Its dummy;
         if (bvh_intersect(s, rec.shadow, dummy, true)) continue;
         BRec bq;
+        set_uv(bq, s, its);
         bq.wi = wi;
         bq.wo = wo;
         bq.measure = ESolidAngle;
@@ -1116,6 +1181,10 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
     s->integrator = d->integrator;
     s->shapes.assign(d->shapes, d->shapes + d->n_shapes);
     s->bsdfs.assign(d->bsdfs, d->bsdfs + d->n_bsdfs);
+    if (d->n_textures) s->textures.assign(d->textures, d->textures + d->n_textures);
+    if (d->n_texels) s->texels.assign(d->texels, d->texels + 4 * (size_t)d->n_texels);
+    for (const nh_bsdf &b : s->bsdfs)
+        if (b.albedo_texture > s->textures.size()) return NH_ERR_INVALID;
     s->emitters.assign(d->emitters, d->emitters + d->n_emitters);
     s->emitter_cdf.assign(d->emitter_cdf, d->emitter_cdf + d->n_emitters + 1);
     for (uint32_t i = 0; i < d->n_vertices; ++i) {
@@ -1721,6 +1790,17 @@ int no_chi2_histogram(const nh_bsdf *b, const float *wi, uint64_t *state, uint64
     }
     *state = rng.state;
     *inc = rng.inc;
+    return NH_OK;
+}
+
+int no_texture_eval(const no_scene *s, uint32_t texture, int32_t n, const float *u, const float *v, float *rgb) {
+    if (!s || texture == 0 || texture > s->textures.size() || n < 0) return NH_ERR_INVALID;
+    for (int32_t i = 0; i < n; ++i) {
+        const V3 c = texture_eval(*s, s->textures[texture - 1], u[i], v[i]);
+        rgb[3 * i] = c.x;
+        rgb[3 * i + 1] = c.y;
+        rgb[3 * i + 2] = c.z;
+    }
     return NH_OK;
 }
 

@@ -79,6 +79,9 @@ int no_ttest_bsdf(const nh_bsdf *b, float angle_deg, uint64_t *state, uint64_t *
 int no_bsdf_sample(const nh_bsdf *b, const float *wi, const float *sample, float *wo, float *weight3,
                    float *pdf, int32_t *measure);
 float no_bsdf_pdf(const nh_bsdf *b, const float *wi, const float *wo);
+/* Texture<Color3f>::eval of the scene's albedo texture `texture` (1-based, nh_bsdf.albedo_texture) at n uv
+ * pairs: rgb = 3n floats */
+int no_texture_eval(const no_scene *s, uint32_t texture, int32_t n, const float *u, const float *v, float *rgb);
 int no_bsdf_pdf_batch(const nh_bsdf *b, const float *wi, int32_t n, const float *wo, float *out);
 /* ChiSquareTest histogram (src/utils/chi2test.cpp:150-170), rng state in/out */
 int no_chi2_histogram(const nh_bsdf *b, const float *wi, uint64_t *state, uint64_t *inc, int32_t n, int32_t res_theta,

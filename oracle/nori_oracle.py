@@ -49,6 +49,7 @@ _sig("no_ttest_bsdf", _i32, C.POINTER(nh.nh_bsdf), C.c_float, _u64p, _u64p, _i32
      C.POINTER(C.c_double))
 _sig("no_bsdf_sample", _i32, C.POINTER(nh.nh_bsdf), _fp, _fp, _fp, _fp, _fp, C.POINTER(_i32))
 _sig("no_bsdf_pdf", C.c_float, C.POINTER(nh.nh_bsdf), _fp, _fp)
+_sig("no_texture_eval", _i32, _vp, _u32, _i32, _fp, _fp, _fp)
 _sig("no_bsdf_pdf_batch", _i32, C.POINTER(nh.nh_bsdf), _fp, _i32, _fp, _fp)
 _sig("no_eigen_ops", _i32, _i32, _fp, _fp)
 _sig("no_denoise_simple", _i32, _fp, _i32, _i32, _i32, C.POINTER(nh.nh_denoiser))
@@ -111,6 +112,16 @@ class OracleScene:
         if _lib.no_env_cdf(self._h, C.byref(p), C.byref(n), C.byref(norm)) != 0:
             return None
         return np.ctypeslib.as_array(p, shape=(n.value,)).copy(), norm.value
+
+    def texture_eval(self, texture: int, u, v):
+        """Albedo texture `texture` (1-based, nh_bsdf.albedo_texture) at the uv pairs: (n, 3) float32."""
+        u = np.ascontiguousarray(u, dtype=np.float32)
+        v = np.ascontiguousarray(v, dtype=np.float32)
+        out = np.zeros((len(u), 3), np.float32)
+        if _lib.no_texture_eval(self._h, texture, len(u), u.ctypes.data_as(_fp), v.ctypes.data_as(_fp),
+                                out.ctypes.data_as(_fp)) != 0:
+            raise RuntimeError("no_texture_eval failed")
+        return out
 
     def trace(self, o, d, mint, maxt, any_hit=False):
         n = len(o)

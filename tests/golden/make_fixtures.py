@@ -11,7 +11,14 @@ Writes (all data, no reference source):
                           (scenes/pa4/tests), the microfacet BSDF tests (scenes/pa3/tests
                           ttest/chi2test XML) and the point-light tests (scenes/pa1/test-direct.xml). Stored as {relative path: file text}; tests write
                           them to a temporary directory and load them through nh_scene_load_xml.
+  textured_scenes.json.gz the reference's textured-albedo scenes with their meshes (gzip of the same
+                          {relative path: file text} form): scenes/project/denoiser/denoiser-test.xml (the
+                          scene of the reference's only published timing, checkerboard_color floor),
+                          scenes/pa1/mesh-texture.xml and sphere-texture.xml (checkerboard_color),
+                          scenes/project/textures/aircraft.xml (png_texture; its aircraft_base.png and .hdr
+                          envmap are absent from the reference checkout)
 """
+import gzip
 import json
 import os
 import subprocess
@@ -51,6 +58,19 @@ SCENE_FILES = [
     # point-light known-answer scenes of the `direct` integrator (PointLight, pointlight.cpp:47-78)
     "scenes/pa1/test-direct.xml",
     "scenes/pa1/disk.obj",
+]
+
+TEXTURED_FILES = [
+    "scenes/project/denoiser/denoiser-test.xml",
+    "scenes/project/meshes/table/plane.obj",
+    "scenes/project/meshes/table/curvy_bowl.obj",
+    "scenes/pa1/mesh-texture.xml",
+    "scenes/pa1/sphere-texture.xml",
+    "scenes/pa1/camelhead.obj",
+    "scenes/pa1/plane.obj",
+    "scenes/project/textures/aircraft.xml",
+    "scenes/project/meshes/aircraft/aircraft_base.obj",
+    "scenes/project/meshes/aircraft/aircraft_glass.obj",
 ]
 
 
@@ -97,7 +117,10 @@ def main():
     scenes = {p: open(os.path.join(ref, p)).read() for p in SCENE_FILES}
     with open(os.path.join(HERE, "reference_scenes.json"), "w") as f:
         json.dump(scenes, f, indent=0)
-    print("wrote pcg32_kat.json, reference_scenes.json")
+    textured = {p: open(os.path.join(ref, p)).read() for p in TEXTURED_FILES}
+    with open(os.path.join(HERE, "textured_scenes.json.gz"), "wb") as f:
+        f.write(gzip.compress(json.dumps(textured, indent=0).encode(), mtime=0))
+    print("wrote pcg32_kat.json, reference_scenes.json, textured_scenes.json.gz")
 
 
 if __name__ == "__main__":
