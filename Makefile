@@ -34,10 +34,11 @@ ORACLE   := oracle/_build/libnori_oracle.so
 CLI      := $(LIBDIR)/nori_hip
 
 RCPCHECK := tools/bin/rcp_exhaustive
+VALUBENCH := tools/bin/valu_issue
 
 MANUAL   := tests/c/bin/manual_scene
 
-all: $(LIB) $(HOSTLIB) $(ORACLE) $(CLI) $(RCPCHECK) $(MANUAL)
+all: $(LIB) $(HOSTLIB) $(ORACLE) $(CLI) $(RCPCHECK) $(VALUBENCH) $(MANUAL)
 
 # C test: a scene description filled field by field (no XML loader), rendered through the C-ABI and
 # compared with the oracle (run by tests/test_gpu_parity.py)
@@ -50,6 +51,11 @@ $(MANUAL): tests/c/manual_scene.c $(LIB) $(ORACLE) include/nori_hip.h oracle/nor
 $(RCPCHECK): tools/rcp_exhaustive.hip $(HIP_DEPS)
 	@mkdir -p tools/bin
 	$(HIPCC) $(HIP_FLAGS) -o $@ $<
+
+# VALU issue-rate microbenchmark (scripts/valu_issue.sh): the ceiling bench.py's limiter record divides by
+$(VALUBENCH): tools/valu_issue.hip
+	@mkdir -p tools/bin
+	$(HIPCC) -std=c++17 -O3 --offload-arch=$(ARCH) -o $@ $<
 
 $(OBJDIR)/host_%.o: $(PKG)/host/%.cpp $(wildcard $(PKG)/host/*.h) include/nori_hip.h
 	@mkdir -p $(OBJDIR)

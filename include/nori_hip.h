@@ -110,7 +110,9 @@ typedef struct nh_texture {
     uint64_t texel_offset;   /* png: first texel (4 floats) in nh_scene_desc.texels */
     float scale_u, scale_v;  /* png scaleU / scaleV */
     float offset_u, offset_v;/* png offsetU / offsetV (non-spherical lookups) */
-    int32_t spherical;       /* png sphericalTexture (eulerAngles = 0) */
+    int32_t spherical;       /* png sphericalTexture */
+    float rotation[9];       /* png spherical lookups: the eulerAngles rotation (PNGTexture.cpp:133-139), row-major;
+                                identity for eulerAngles = 0 */
     int32_t pad;
 } nh_texture;
 
@@ -155,6 +157,8 @@ typedef struct nh_envmap {
     int32_t constant;             /* ConstantTexture: eval ignores uv */
     const float *cdf;             /* EnvMap::calculateProbs DiscretePDF: width*height+1 CDF entries */
     float normalization;          /* DiscretePDF::getNormalization() */
+    float rotation[9];            /* spherical lookups: the png_texture's eulerAngles rotation (PNGTexture.cpp:133-139),
+                                     row-major; identity for eulerAngles = 0 */
 } nh_envmap;
 
 /* <denoiser> of the scene (Scene::m_denoiser, src/utils/scene.cpp:242-245): SimpleDenoiser's parameters after

@@ -354,6 +354,7 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         o.dx = t.delta[0]; o.dy = t.delta[1]; o.sx = t.scale[0]; o.sy = t.scale[1];
         o.su = t.scale_u; o.sv = t.scale_v; o.ou = t.offset_u; o.ov = t.offset_v;
         o.off = (long long)t.texel_offset;
+        std::memcpy(o.rot, t.rotation, sizeof(o.rot));
     }
     std::vector<DEmitter> de(d->n_emitters);
     for (uint32_t i = 0; i < d->n_emitters; ++i) {
@@ -399,6 +400,7 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         S.env_w = e.width;
         S.env_h = e.height;
         S.env_spherical = e.spherical;
+        std::memcpy(S.env_rot, e.rotation, sizeof(S.env_rot));
         S.env_constant = e.constant;
         S.env_norm = e.normalization;
         S.env_su = e.scale_u;

@@ -150,6 +150,8 @@ struct alignas(16) DTex {
     float sx, sy, su, sv;
     float ou, ov;
     long long off;  // png: first texel in DScene::texels
+    float rot[9];   // png spherical lookups: the eulerAngles rotation, row-major
+    float pad[3];
 };
 struct alignas(16) DEmitter {
     int type, shape;
@@ -188,6 +190,7 @@ struct DScene {
     int env_w, env_h, env_spherical, env_constant;
     float env_norm, env_su, env_sv, env_ou, env_ov;
     float env_r, env_g, env_b;
+    float env_rot[9];  // spherical lookups: the png_texture's eulerAngles rotation, row-major
     // BSDF albedo textures (DBsdf::tex) and the png texels they index
     const DTex *texs;
     const float4 *texels;

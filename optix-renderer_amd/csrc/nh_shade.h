@@ -77,6 +77,12 @@ __device__ __forceinline__ void spherical_coordinates(F3 v, float &theta, float 
     phi = f_atan2(v.y, v.x);
     if (phi < 0) phi += 2 * kPi;
 }
+// Matrix3f * Vector3f as Eigen 3.3.8 evaluates it (row . v as x0*y0 + (x1*y1 + x2*y2)), m row-major
+__device__ __forceinline__ F3 rot3(const float *m, F3 w) {
+    return f3(m[0] * w.x + (m[1] * w.y + m[2] * w.z), m[3] * w.x + (m[4] * w.y + m[5] * w.z),
+              m[6] * w.x + (m[7] * w.y + m[8] * w.z));
+}
+
 // static_cast<unsigned int>(float) / int(float) as the reference's x86-64 build executes them (cvttss2si: to 64
 // bits and the low word for unsigned, |x| >= 2^63 or NaN -> 0; to 32 bits for int, out of range or NaN -> INT_MIN)
 __device__ __forceinline__ unsigned x86_f2u(float x) { return fabsf(x) < 0x1p63f ? (unsigned)(long long)x : 0u; }
@@ -103,9 +109,7 @@ __device__ __noinline__ F3 tex_eval(const DScene &S, int ti, float u, float v) {
     }
     if (t.type == TEX_PNG) {
         if (t.spherical) {
-            F3 wi = spherical_direction(v * kPi, u * 2.f * kPi);
-            wi = f3(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
-                    0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+            const F3 wi = rot3(t.rot, spherical_direction(v * kPi, u * 2.f * kPi));
             float th, ph;
             spherical_coordinates(wi, th, ph);
             u = ph / (2.f * kPi);
@@ -130,10 +134,8 @@ __device__ __forceinline__ F3 env_tex(const DScene &S, float u, float v) {
         return f3(c.x, c.y, c.z);
     }
     if (S.env_spherical) {
-        F3 wi = spherical_direction(v * kPi, u * 2.f * kPi);
-        // Eigen rotation (identity for eulerAngles = 0) times wi, keeping the signed zeros it produces
-        wi = f3(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
-                0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+        // rot * wi, Eigen's Matrix3f * Vector3f (eulerAngles = 0: the identity, signed zeros as Eigen produces them)
+        const F3 wi = rot3(S.env_rot, spherical_direction(v * kPi, u * 2.f * kPi));
         float th, ph;
         spherical_coordinates(wi, th, ph);
         u = ph / (2.f * kPi);

@@ -109,6 +109,56 @@ inline void pre_affine(Mat4 &t, const Mat4 &a) {
 }
 
 // parser.cpp:343-359: columns left, newUp, dir, origin
+// PNGTexture's spherical-lookup rotation (PNGTexture.cpp:28, :133-139):
+//   eulerAngles = degrees * M_PI / 180.f;
+//   rot = Quaternionf(Identity * AngleAxisf(e.x, UnitZ) * AngleAxisf(e.y, UnitX)) * AngleAxisf(e.z, UnitZ).toRotationMatrix()
+// in Eigen 3.3.8's float arithmetic: AngleAxis -> Quaternion (Quaternion.h:523-531), the SSE quaternion product
+// (arch/Geometry_SSE.h quat_product), Quaternion::toRotationMatrix (Quaternion.h:554-586), AngleAxis::
+// toRotationMatrix (AngleAxis.h:218-242) and the 3x3 product in the order Eigen's lazy product gives. Pinned by
+// oracle/eigen_xform_probe.cpp ("prot"). Row-major out[9].
+struct Quat {
+    float x, y, z, w;
+};
+inline Quat quat_from_angle_axis(float angle, Vec3 axis) {
+    const float ha = 0.5f * angle;
+    const float s = std::sin(ha);
+    return {s * axis.x, s * axis.y, s * axis.z, std::cos(ha)};
+}
+inline Quat quat_mul(Quat a, Quat b) {  // _mm_add_ps(_mm_sub_ps(a * b.wwww, a.zxyx * b.yzxx), mask ^ (s1 + s2))
+    const float s1[4] = {a.y * b.z, a.z * b.x, a.x * b.y, a.z * b.z};
+    const float s2[4] = {a.w * b.x, a.w * b.y, a.w * b.z, a.y * b.y};
+    const float t1[4] = {a.x * b.w, a.y * b.w, a.z * b.w, a.w * b.w};
+    const float t2[4] = {a.z * b.y, a.x * b.z, a.y * b.x, a.x * b.x};
+    return {(t1[0] - t2[0]) + (s1[0] + s2[0]), (t1[1] - t2[1]) + (s1[1] + s2[1]), (t1[2] - t2[2]) + (s1[2] + s2[2]),
+            (t1[3] - t2[3]) + -(s1[3] + s2[3])};
+}
+inline void quat_matrix(Quat q, float r[3][3]) {
+    const float tx = 2.f * q.x, ty = 2.f * q.y, tz = 2.f * q.z;
+    const float twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const float txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const float tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    r[0][0] = 1.f - (tyy + tzz);
+    r[0][1] = txy - twz;
+    r[0][2] = txz + twy;
+    r[1][0] = txy + twz;
+    r[1][1] = 1.f - (txx + tzz);
+    r[1][2] = tyz - twx;
+    r[2][0] = txz - twy;
+    r[2][1] = tyz + twx;
+    r[2][2] = 1.f - (txx + tyy);
+}
+inline void png_rotation(Vec3 deg, float out[9]) {
+    const float pi = 3.14159265358979323846f;  // Nori's float M_PI (common.h:61)
+    const Vec3 e = {deg.x * pi / 180.f, deg.y * pi / 180.f, deg.z * pi / 180.f};
+    const Vec3 ux = {1.f, 0.f, 0.f}, uz = {0.f, 0.f, 1.f};
+    const Quat q = quat_mul(quat_mul(Quat{0.f, 0.f, 0.f, 1.f}, quat_from_angle_axis(e.x, uz)), quat_from_angle_axis(e.y, ux));
+    float a[3][3], b[3][3];
+    quat_matrix(q, a);
+    angle_axis_matrix(e.z, uz, b);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) out[3 * i + j] = dot3(a[i][0], a[i][1], a[i][2], b[0][j], b[1][j], b[2][j]);
+}
+
 inline Mat4 lookat_matrix(Vec3 origin, Vec3 target, Vec3 up) {
     const Vec3 dir = normalized({target.x - origin.x, target.y - origin.y, target.z - origin.z});
     const Vec3 left = normalized(cross(normalized(up), dir));

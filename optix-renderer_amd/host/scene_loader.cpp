@@ -620,10 +620,8 @@ nh_texture make_texture(const Obj &t, const std::string &base_dir, SceneData &sd
         x.type = NH_TEXTURE_PNG;
         if (!p.get_bool("sRGB", p.get_string("name", "") != "normal"))
             throw SceneError("png_texture: normal-map (sRGB=false) lookups are not supported as an albedo");
-        V3 eul = p.get_vector("eulerAngles", v3(0, 0, 0));
         x.spherical = p.get_bool("sphericalTexture", false) ? 1 : 0;
-        if (x.spherical && (eul.x != 0 || eul.y != 0 || eul.z != 0))
-            throw SceneError("png_texture: eulerAngles are not supported");
+        xf::png_rotation(to_xf(p.get_vector("eulerAngles", v3(0, 0, 0))), x.rotation);
         x.scale_u = p.get_float("scaleU", 1.f);
         x.scale_v = p.get_float("scaleV", 1.f);
         x.offset_u = p.get_float("offsetU", 0.f);
@@ -717,9 +715,10 @@ float inverse_gamma(float x) {  // PNGTexture.cpp:442-447
 void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w, unsigned &h) {
     const auto dot = fn.find_last_of('.');
     const std::string ext = dot == std::string::npos ? std::string() : fn.substr(dot);
+    // PNGTexture::loadFromFile's order (PNGTexture.cpp:63-72): existence first, then the extension
+    if (!std::ifstream(fn).good()) throw SceneError("PNGTexture: image file not found " + fn);
     if (ext == ".hdr") throw SceneError("PNGTexture: .hdr images (HDRLoader) are not supported by the HIP path");
     if (ext != ".png") throw SceneError("PNGTexture: file extension " + ext + " unknown.");
-    if (!std::ifstream(fn).good()) throw SceneError("PNGTexture: image file not found " + fn);
     std::vector<uint8_t> px;
     std::string err;
     if (!png_decode_rgba8(fn, px, w, h, err)) throw SceneError("PNGTexture: " + err);
@@ -736,9 +735,10 @@ V3 env_tex_eval(const nh_envmap &e, const float *rgba, float u, float v) {
     if (e.constant) return v3(rgba[0], rgba[1], rgba[2]);
     if (e.spherical) {
         V3 wi = spherical_direction(v * kPiF, u * 2.f * kPiF);
-        // rot * wi with rot = identity from the Euler-angle quaternions (fp32, signed zeros kept)
-        wi = v3(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
-                0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+        // rot * wi (Matrix3f * Vector3f: x0*y0 + (x1*y1 + x2*y2) per row, pinned by the probe's "pdir")
+        const float *m = e.rotation;
+        wi = v3(m[0] * wi.x + (m[1] * wi.y + m[2] * wi.z), m[3] * wi.x + (m[4] * wi.y + m[5] * wi.z),
+                m[6] * wi.x + (m[7] * wi.y + m[8] * wi.z));
         float th, ph;
         spherical_coordinates(wi, th, ph);
         u = ph / (2.f * kPiF);
@@ -762,6 +762,7 @@ void build_envmap(const Obj &o, const std::string &base_dir, SceneData &sd, nh_e
     e = nh_envmap{};
     e.radiance[0] = rad.x; e.radiance[1] = rad.y; e.radiance[2] = rad.z;
     e.scale_u = e.scale_v = 1.f;
+    xf::png_rotation(xf::Vec3{0.f, 0.f, 0.f}, e.rotation);
     const Obj *tex = nullptr;
     for (auto &ch : o.children) {
         if (ch->tag != "texture") throw SceneError("EnvMap::addChild(<" + ch->tag + ">) is not supported!");
@@ -779,9 +780,7 @@ void build_envmap(const Obj &o, const std::string &base_dir, SceneData &sd, nh_e
         const PropList &p = tex->props;
         const std::string fn = join_path(base_dir, p.get_string("filename"));
         if (!p.get_bool("sRGB", true)) throw SceneError("png_texture: normal-map (sRGB=false) lookups are not supported");
-        V3 eul = p.get_vector("eulerAngles", v3(0, 0, 0));
-        if (eul.x != 0 || eul.y != 0 || eul.z != 0) throw SceneError("png_texture: eulerAngles are not supported");
-        if (p.get_float("intensity", 1.f) != 1.f) { /* only used by normal maps */ }
+        xf::png_rotation(to_xf(p.get_vector("eulerAngles", v3(0, 0, 0))), e.rotation);
         e.scale_u = p.get_float("scaleU", 1.f);
         e.scale_v = p.get_float("scaleV", 1.f);
         e.offset_u = p.get_float("offsetU", 0.f);
@@ -1185,6 +1184,16 @@ int nh_debug_transform(const char *request, float *out, int32_t cap) {
             const xf::Mat4 p = xf::camera_projection((int)w, (int)h, fov, n, f);
             put_m4(xf::inverse(p));
             put_m4(p);
+        } else if (cmd == "prot") {
+            float rot[9];
+            xf::png_rotation(v3(), rot);
+            r.insert(r.end(), rot, rot + 9);
+        } else if (cmd == "pdir") {
+            float m[9];
+            for (float &x : m) x = next();
+            const xf::Vec3 v = v3();
+            r.insert(r.end(), {xf::dot3(m[0], m[1], m[2], v.x, v.y, v.z), xf::dot3(m[3], m[4], m[5], v.x, v.y, v.z),
+                               xf::dot3(m[6], m[7], m[8], v.x, v.y, v.z)});
         } else if (cmd == "pt" || cmd == "vec" || cmd == "nrm") {
             const xf::Mat4 m = m4();
             const xf::Vec3 v = v3();

@@ -66,7 +66,7 @@ TEXTURE_CONSTANT, TEXTURE_CHECKERBOARD, TEXTURE_PNG = 0, 1, 2
 class nh_texture(C.Structure):
     _fields_ = [("type", _i32), ("value1", _f * 3), ("value2", _f * 3), ("delta", _f * 2), ("scale", _f * 2),
                 ("width", _i32), ("height", _i32), ("texel_offset", C.c_uint64), ("scale_u", _f), ("scale_v", _f),
-                ("offset_u", _f), ("offset_v", _f), ("spherical", _i32), ("pad", _i32)]
+                ("offset_u", _f), ("offset_v", _f), ("spherical", _i32), ("rotation", _f * 9), ("pad", _i32)]
 
 
 class nh_emitter(C.Structure):
@@ -87,7 +87,7 @@ class nh_filter(C.Structure):
 class nh_envmap(C.Structure):
     _fields_ = [("width", _i32), ("height", _i32), ("rgba", _fp), ("radiance", _f * 3), ("scale_u", _f),
                 ("scale_v", _f), ("offset_u", _f), ("offset_v", _f), ("spherical", _i32), ("constant", _i32),
-                ("cdf", _fp), ("normalization", _f)]
+                ("cdf", _fp), ("normalization", _f), ("rotation", _f * 9)]
 
 
 class nh_denoiser(C.Structure):
@@ -286,6 +286,8 @@ class Scene:
         t.scale_u, t.scale_v = scale_uv
         t.offset_u, t.offset_v = offset_uv
         t.spherical = int(spherical)
+        for i in range(9):
+            t.rotation[i] = 1.0 if i % 4 == 0 else 0.0
         ptr = None
         if texels is not None:
             tx = np.ascontiguousarray(texels, dtype=np.float32)

@@ -215,10 +215,11 @@ def sky_image(width: int, height: int, seed: int = 7) -> np.ndarray:
 
 def envmap_xml(out_dir: str, width: int = 64, height: int = 48, spp: int = 16, texture: str = "png",
                tex_size=(96, 48), spherical: bool = True, area_light: bool = True, integrator: str = "path_mis",
-               mesh: str | None = None) -> str:
+               mesh: str | None = None, euler=None) -> str:
     """Open scene lit by an envmap (+ optionally a small area light): a ground quad, a diffuse
     and a microfacet sphere, a mirror sphere. texture: png | constant | none (EnvMap's 0.5
-    fallback). mesh: optional OBJ path added with a diffuse BSDF."""
+    fallback). mesh: optional OBJ path added with a diffuse BSDF. euler: the png_texture's eulerAngles
+    (degrees) of the spherical lookup."""
     os.makedirs(out_dir, exist_ok=True)
     tex_xml = ""
     if texture == "png":
@@ -228,6 +229,7 @@ def envmap_xml(out_dir: str, width: int = 64, height: int = 48, spp: int = 16, t
         tex_xml = f"""<texture type="png_texture" name="albedo">
       <string name="filename" value="{os.path.basename(png)}"/>
       <boolean name="sphericalTexture" value="{'true' if spherical else 'false'}"/>
+      {f'<vector name="eulerAngles" value="{euler[0]},{euler[1]},{euler[2]}"/>' if euler else ''}
     </texture>"""
     elif texture == "constant":
         tex_xml = '<texture type="constant_color" name="albedo"><color name="value" value="0.8 0.7 0.6"/></texture>'
@@ -270,7 +272,7 @@ def envmap_xml(out_dir: str, width: int = 64, height: int = 48, spp: int = 16, t
   {extra}
 </scene>
 """
-    key = repr((width, height, spp, texture, tex_size, spherical, area_light, integrator, mesh)).encode()
+    key = repr((width, height, spp, texture, tex_size, spherical, area_light, integrator, mesh, euler)).encode()
     dst = os.path.join(out_dir, f"envmap_{hashlib.sha1(key).hexdigest()[:10]}.xml")
     with open(dst, "w") as f:
         f.write(text)

@@ -21,6 +21,9 @@
 //   pt   m[16] x y z                    -> Transform(m) * Point3f                           (3)
 //   vec  m[16] x y z                    -> Transform(m) * Vector3f                          (3)
 //   nrm  m[16] x y z                    -> (Transform(m) * Normal3f).normalized()           (3)
+//   prot ex ey ez                       -> PNGTexture's spherical-lookup rotation for eulerAngles (degrees, as
+//                                          the XML gives them; PNGTexture.cpp:28, :133-139), row-major (9)
+//   pdir m[9] x y z                     -> Matrix3f(m) * Vector3f (the lookup's rot * wi)    (3)
 // Matrices are row-major in the protocol.
 #include <Eigen/Core>
 #include <Eigen/Geometry>
@@ -145,6 +148,24 @@ int main() {
             } else {
                 r = (inv.topLeftCorner<3, 3>().transpose() * v).normalized();
             }
+            put(r.x()); put(r.y()); put(r.z());
+        } else if (cmd == "prot") {
+            // eulerAngles = props.getVector3("eulerAngles", Vector3f(0.f)) * M_PI / 180.f (Nori's float M_PI)
+            const Eigen::Vector3f deg = read_v3(in);
+            const Eigen::Vector3f eulerAngles = deg * 3.14159265358979323846f / 180.f;
+            Eigen::Matrix3f rot = Eigen::Quaternionf(
+                                      Eigen::Quaternionf::Identity() *
+                                      Eigen::AngleAxisf(eulerAngles.x(), Eigen::Vector3f::UnitZ()) *
+                                      Eigen::AngleAxisf(eulerAngles.y(), Eigen::Vector3f::UnitX())) *
+                                  Eigen::AngleAxisf(eulerAngles.z(), Eigen::Vector3f::UnitZ()).toRotationMatrix();
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) put(rot(i, j));
+        } else if (cmd == "pdir") {
+            Eigen::Matrix3f m;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) m(i, j) = next(in);
+            const Eigen::Vector3f v = read_v3(in);
+            const Eigen::Vector3f r = m * v;
             put(r.x()); put(r.y()); put(r.z());
         } else if (cmd.empty()) {
             continue;

@@ -640,14 +640,18 @@ V3 png_lookup(const float *d, unsigned width, unsigned height, float scale_u, fl
     return mk(d[4 * (size_t)index], d[4 * (size_t)index + 1], d[4 * (size_t)index + 2]);
 }
 
+// Matrix3f * Vector3f in Eigen 3.3.8's order (x0*y0 + (x1*y1 + x2*y2) per row; m row-major)
+inline V3 rot3(const float *m, V3 w) {
+    return mk(m[0] * w.x + (m[1] * w.y + m[2] * w.z), m[3] * w.x + (m[4] * w.y + m[5] * w.z),
+              m[6] * w.x + (m[7] * w.y + m[8] * w.z));
+}
+
 V3 env_tex_eval(const no_scene &s, float u, float v) {
     const float *d = s.env_rgba.data();
     if (s.env.constant) return mk(d[0], d[1], d[2]);  // ConstantTexture::eval
     if (s.env.spherical) {
-        V3 wi = spherical_direction(v * kPi, u * 2.f * kPi);
-        // Eigen rotation (identity for eulerAngles = 0) times wi, signed zeros as Eigen produces them
-        wi = mk(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
-                0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+        // rot * wi: Eigen's Matrix3f * Vector3f (PNGTexture.cpp:133-140; identity for eulerAngles = 0)
+        const V3 wi = rot3(s.env.rotation, spherical_direction(v * kPi, u * 2.f * kPi));
         float th, ph;
         spherical_coordinates(wi, th, ph);
         u = ph / (2.f * kPi);
@@ -686,9 +690,7 @@ V3 texture_eval(const no_scene &s, const nh_texture &t, float u, float v) {
     }
     if (t.type == NH_TEXTURE_PNG) {
         if (t.spherical) {
-            V3 wi = spherical_direction(v * kPi, u * 2.f * kPi);
-            wi = mk(1.f * wi.x + (0.f * wi.y + 0.f * wi.z), 0.f * wi.x + (1.f * wi.y + 0.f * wi.z),
-                    0.f * wi.x + (0.f * wi.y + 1.f * wi.z));
+            const V3 wi = rot3(t.rotation, spherical_direction(v * kPi, u * 2.f * kPi));
             float th, ph;
             spherical_coordinates(wi, th, ph);
             u = ph / (2.f * kPi);

@@ -84,7 +84,8 @@ def test_bench_two_hip_ranks_reduce_to_one_rank_render(tmp_path, gpu):
     out = str(tmp_path / "reduced.npy")
     line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--config", "c2", "--width", "160", "--height", "96",
                    "--rounds", "2", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-denoise",
-                   "--traversal-1m-steps", "0", "--roofline-steps", "0", "--dump-framebuffer", out])
+                   "--traversal-1m-steps", "0", "--roofline-steps", "0", "--strong-spp", "0", "--no-extras",
+                   "--dump-framebuffer", out])
     assert line["n_gpus"] == 2 and line["value"] > 0
     reduced = np.load(out).astype(np.float64)
     xml = scenegen.cbox_xml(str(tmp_path), "c2", width=160, height=96)
@@ -93,6 +94,36 @@ def test_bench_two_hip_ranks_reduce_to_one_rank_render(tmp_path, gpu):
     ctx.upload(s, nh.Bvh(s))
     R = 2 * 2  # --rounds x world: each rank's weak-scaling step
     ctx.render(0, 2 * R, seed=1234, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT)
+    full = ctx.framebuffer().astype(np.float64)
+    ctx.close()
+    err = np.sqrt(((reduced - full) ** 2).sum() / (full ** 2).sum())
+    assert err < 1e-6, err
+
+
+@pytest.mark.gpu
+def test_bench_two_hip_ranks_strong_scaling_equals_one_rank_render(tmp_path, gpu):
+    """bench.py --gpus 2 --scaling strong: a fixed image (the mirror + dielectric Cornell box, C4's scene at test
+    size) whose --rounds x --steps spp are split over the ranks by blocks; the reduced framebuffer equals one HIP
+    render of the whole image over the same samples (render.cpp:281-347: the sample budget of a block does not
+    depend on the rank that renders it), up to fp32 summation order where block footprints overlap. Also runs the
+    strong_c4 sub-record's code path (a small --strong-spp) on both ranks."""
+    sys.path.insert(0, os.path.join(REPO, "optix-renderer_amd"))
+    import nori_hip as nh
+    import scenegen
+    out = str(tmp_path / "reduced.npy")
+    line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--scaling", "strong", "--config", "c1", "--width", "160",
+                   "--height", "96", "--rounds", "3", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-denoise",
+                   "--traversal-1m-steps", "0", "--roofline-steps", "0", "--strong-spp", "2", "--no-extras",
+                   "--dump-framebuffer", out])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["config"]["spp"] == 6
+    sc = line["strong_c4"]
+    assert sc["n_gpus"] == 2 and sc["spp"] == 2 and sc["msamples_s"] > 0
+    reduced = np.load(out).astype(np.float64)
+    xml = scenegen.cbox_xml(str(tmp_path), "c1", width=160, height=96)
+    s = nh.Scene(xml)
+    ctx = nh.Context(0)
+    ctx.upload(s, nh.Bvh(s))
+    ctx.render(0, 6, seed=1234, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT)
     full = ctx.framebuffer().astype(np.float64)
     ctx.close()
     err = np.sqrt(((reduced - full) ** 2).sum() / (full ** 2).sum())

@@ -80,8 +80,12 @@ def test_c4_full_path_id_range(gpu, tmp_path, monkeypatch):
     assert st["samples"] == 16 * 2048 * 2048
 
 
-def test_c3_full_mesh(gpu, tmp_path):
-    """C3's 498k-triangle Beckmann-microfacet mesh (the bench scene itself) at 128^2, 4 spp."""
+@pytest.mark.parametrize("sort_shade", ["0", "1"])
+def test_c3_full_mesh(gpu, tmp_path, monkeypatch, sort_shade):
+    """C3's 498k-triangle Beckmann-microfacet mesh (the bench scene itself) at 128^2, 4 spp; with NH_SORT_SHADE=1
+    the deep-BVH material-sorted shade (wf_shade<true>: the workgroup's entries shaded in BSDF-type order, the
+    north star's material-sorted queues on the split pipeline) against the oracle too."""
+    monkeypatch.setenv("NH_SORT_SHADE", sort_shade)
     xml, ntri = scenegen.bumpy_cbox_xml(str(tmp_path), 1000, 250, width=128, height=128)
     assert ntri == 498000
     _, _, st = bench_pipeline_vs_oracle(xml, 128, 128, 4)

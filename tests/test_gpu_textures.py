@@ -11,7 +11,7 @@ import pytest
 import nori_hip as nh
 import nori_oracle as no
 import scenegen
-from test_textures import png_scene
+from test_textures import aircraft_substituted, png_scene
 
 pytestmark = pytest.mark.gpu
 
@@ -83,3 +83,27 @@ def test_checkerboard_through_cabi(gpu, tmp_path):
         for mode in (nh.MODE_MEGAKERNEL, nh.MODE_WAVEFRONT):
             g, r = render_both(s, 8, None, mode)
             np.testing.assert_array_equal(g, r)
+
+
+@pytest.mark.parametrize("euler", [(0, 270, 0), (30, -45, 110)])
+def test_envmap_euler_rotation(gpu, tmp_path, euler):
+    """A spherical png envmap with eulerAngles (PNGTexture.cpp:133-139; the rotation is pinned against Eigen by
+    test_transforms.py): NEE by the rotated luminance CDF, escaped rays, both modes, GPU = oracle."""
+    xml = scenegen.envmap_xml(str(tmp_path), texture="png", tex_size=(96, 48), euler=euler)
+    s = nh.Scene(xml)
+    s.set_resolution(64, 48)
+    for mode in (nh.MODE_MEGAKERNEL, nh.MODE_WAVEFRONT):
+        g, r = render_both(s, 8, None, mode)
+        np.testing.assert_array_equal(g, r)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_aircraft_substituted_crop(gpu, tex_dir, mode):
+    """scenes/project/textures/aircraft.xml (png_texture albedo on the aircraft's own texture coordinates, glass,
+    envmap with eulerAngles 0,270,0) with synthetic stand-ins for its two absent images, a crop of its 800x600
+    camera at 2 spp."""
+    s = nh.Scene(aircraft_substituted(tex_dir))
+    blocks = blocks_of(800, 600, 256, 192, 544, 416)
+    g, r = render_both(s, 2, blocks, mode)
+    np.testing.assert_array_equal(g, r)
+    assert np.abs(r).sum() > 0

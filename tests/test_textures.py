@@ -145,8 +145,6 @@ def png_scene(tmp_path, tex_w=37, tex_h=23, scale=None, offset=None, spherical=F
     tex = (f'<bsdf type="diffuse"><texture type="png_texture" name="albedo"><string name="filename" '
            f'value="{png}"/>{props}</texture></bsdf>')
     xml = scenegen.cbox_xml(d, "c2", walls_bsdf=tex)
-    px = img.astype(np.float64) / 255.0
-    lin = np.where(px <= 0.04045, px / 12.92, ((px + 0.055) / 1.055) ** 2.4)
     return xml, img
 
 
@@ -207,13 +205,14 @@ def test_texture_loader_errors(tmp_path):
     d = str(tmp_path)
     png = os.path.join(d, "t.png")
     scenegen.write_png(png, np.full((4, 4, 4), 128, np.uint8))
+    open(png[:-4] + ".hdr", "wb").write(b"#?RADIANCE\n")  # an existing .hdr image: HDRLoader is not restated
     cases = {
         # an albedo colour already creates the albedo texture (diffuse.cpp:33-40, :75-79)
         '<bsdf type="diffuse"><color name="albedo" value="0.5,0.5,0.5"/><texture type="constant_color" name="albedo">'
         '<color name="value" value="1,1,1"/></texture></bsdf>': "There is already an albedo defined!",
         '<bsdf type="diffuse"><texture type="constant_color" name="kd"><color name="value" value="1,1,1"/></texture>'
         '</bsdf>': "does not match any field",
-        f'<bsdf type="diffuse"><texture type="png_texture" name="albedo"><string name="filename" value="{d}/x.hdr"/>'
+        f'<bsdf type="diffuse"><texture type="png_texture" name="albedo"><string name="filename" value="{png[:-4]}.hdr"/>'
         '</texture></bsdf>': ".hdr",
         '<bsdf type="diffuse"><texture type="png_texture" name="albedo"><string name="filename" value="nope.png"/>'
         '</texture></bsdf>': "image file not found",
@@ -231,3 +230,44 @@ def test_texture_loader_errors(tmp_path):
     assert s.desc.textures[0].type == nh.TEXTURE_CONSTANT
     np.testing.assert_array_equal(no.OracleScene(s).texture_eval(1, [0.3, -7.0], [0.1, 2.0]),
                                   np.array([[0.25, 0.5, 0.75]] * 2, F))
+
+
+def aircraft_substituted(tex_dir):
+    """aircraft.xml with synthetic stand-ins for its two absent images (a random 128x64 aircraft_base.png, the
+    envmap pointed at a png sky); returns the scene file's path."""
+    src = os.path.join(tex_dir, "scenes/project/textures/aircraft.xml")
+    res = os.path.join(tex_dir, "scenes/project/res")
+    os.makedirs(res, exist_ok=True)
+    rng = np.random.default_rng(2)
+    scenegen.write_png(os.path.join(res, "aircraft_base.png"), rng.integers(0, 256, (64, 128, 4), dtype=np.uint8))
+    scenegen.write_png(os.path.join(res, "sky_substitute.png"), scenegen.sky_image(96, 48))
+    text = open(src).read().replace("../res/dikhololo_night_4k.hdr", "../res/sky_substitute.png")
+    xml = os.path.join(os.path.dirname(src), "aircraft_substituted.xml")
+    open(xml, "w").write(text)
+    return xml
+
+
+def test_aircraft_scene(tex_dir, tmp_path):
+    """scenes/project/textures/aircraft.xml: png_texture albedo on the aircraft body, glass dielectric, spherical
+    envmap texture with eulerAngles (0, 270, 0). Its two images (res/aircraft_base.png, res/dikhololo_night_4k.hdr)
+    are absent from the reference checkout, so it fails to load as the reference would (PNGTexture: image file not
+    found); with a synthetic aircraft_base.png and the envmap pointed at a synthetic png sky it loads, with the
+    reference's rotation (Eigen-pinned, test_transforms.py) and the aircraft's texture coordinates."""
+    src = os.path.join(tex_dir, "scenes/project/textures/aircraft.xml")
+    if not os.path.exists(os.path.join(tex_dir, "scenes/project/res/aircraft_base.png")):
+        with pytest.raises(nh.NoriError, match="image file not found"):
+            nh.Scene(src)
+    s = nh.Scene(aircraft_substituted(tex_dir))
+    d = s.desc
+    assert d.n_textures == 1 and d.textures[0].type == nh.TEXTURE_PNG and d.textures[0].spherical == 0
+    assert (d.textures[0].width, d.textures[0].height) == (128, 64)
+    assert d.envmap >= 0 and d.env.spherical == 1
+    rot = np.array(list(d.env.rotation), np.float32).reshape(3, 3)
+    assert not np.array_equal(rot, np.eye(3, dtype=np.float32))  # eulerAngles (0, 270, 0): a rotation about x
+    assert abs(abs(rot[1, 2]) - 1) < 1e-6 and abs(rot[0, 0] - 1) < 1e-6
+    body = d.shapes[0]
+    assert body.has_uvs == 1 and d.bsdfs[body.bsdf].albedo_texture == 1
+    assert d.bsdfs[d.shapes[1].bsdf].type == nh.BSDF_DIELECTRIC
+    s.set_resolution(40, 30)
+    img = no.OracleScene(s).render(0, 1, seed=1)
+    assert np.isfinite(img).all() and img[..., :3].sum() > 0

@@ -150,6 +150,24 @@ def test_point_vector_normal_application_matches_eigen():
     assert_bits(probe(reqs), product(reqs), "Transform * Point3f / Vector3f / Normal3f")
 
 
+def test_png_texture_rotation_matches_eigen():
+    """PNGTexture's spherical-lookup rotation for eulerAngles (PNGTexture.cpp:28, :133-139: quaternion products of
+    AngleAxisf rotations in Eigen's SSE arithmetic, toRotationMatrix, a 3x3 product) and the lookup's rot * wi,
+    restated in host/nori_transform.h (png_rotation) and applied by the loader, the oracle and the kernels."""
+    rng = np.random.default_rng(17)
+    reqs = ["prot " + hx([0, 270, 0]), "prot " + hx([0, 0, 0])]
+    for k in range(3000):
+        e = rng.uniform(-720, 720, 3).astype(np.float32)
+        if k % 5 == 0:
+            e = np.round(e / 45) * 45  # the right angles scenes use
+        if k % 7 == 0:
+            e[rng.integers(0, 3)] = 0
+        reqs.append("prot " + hx(e))
+    for _ in range(3000):
+        reqs.append("pdir " + hx(rng.normal(size=9)) + " " + hx(rng.normal(size=3)))
+    assert_bits(probe(reqs), product(reqs), "PNGTexture rotation / rot * wi")
+
+
 # ------------------------------------------------------------------------------------------------
 # whole scenes through the product loader, checked against matrices recomputed from the XML by the probe
 
