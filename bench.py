@@ -199,6 +199,19 @@ def roofline(args, calib, st, W, H, R):
         q, n, p = w["tail"]
         trav = n * node_b + p * PRIM_BYTES
         stages["tail"] = {"work_bytes": trav, "hbm_bytes": 0 if lds else trav, "queries": q, "nodes": n, "prims": p}
+    elif args.mode == "wavefront" and calib.get("trace_fused"):
+        # deep BVHs: one persistent launch per bounce answers both queries (wf_trace_pt2); its time is in the
+        # extend slot, and its bytes are both queries' traversal work plus both queues
+        w = stage_work(calib)
+        (eq, en, ep), (sq, sn, sp) = w["extend"], w["shadow"]
+        trav = (en + sn) * node_b + (ep + sp) * PRIM_BYTES
+        queue = calib["extend_queue_bytes"] + calib["shadow_queue_bytes"]
+        stages["trace"] = {"work_bytes": trav + queue, "hbm_bytes": queue + (0 if lds else trav), "queries": eq + sq,
+                           "nodes": en + sn, "prims": ep + sp, "ms": "extend"}
+        q, n, p = w["tail"]
+        trav = n * node_b + p * PRIM_BYTES
+        stages["tail"] = {"work_bytes": trav, "hbm_bytes": 0 if lds else trav, "queries": q, "nodes": n, "prims": p}
+        stages["shade"] = {"work_bytes": calib["shade_state_bytes"], "hbm_bytes": calib["shade_state_bytes"]}
     elif args.mode == "wavefront":
         w = stage_work(calib)
         for k in ("extend", "shadow", "tail"):
@@ -244,6 +257,7 @@ def roofline(args, calib, st, W, H, R):
     wide = node_b == 128  # deep trees: the persistent 4-wide traversal kernel runs both queries
     rr = os.environ.get("NH_RR_AHEAD", "1") != "0"
     kernel = {"shade": "wf_shade",
+              "trace": "wf_trace_pt2 (persistent 4-wide closest hit + any hit, one launch per bounce)",
               "extend": "wf_trace_pt (persistent 4-wide closest hit)" if wide else "wf_extend",
               "shadow": "wf_trace_pt (persistent 4-wide any hit)" if wide else "wf_shadow",
               "tail": "wf_tail_rr" if fused and rr else "wf_tail", "path": "nh_path_kernel",
@@ -273,6 +287,15 @@ def roofline(args, calib, st, W, H, R):
         roof["traffic_frac"] = round(roof["traffic_gbs"] / HBM_PEAK_GBS, 4)
     if rec.get("valu_issue_frac") is not None:
         roof["limiter"] = limiter_record(rec, key)
+    if calib.get("tail_bounces"):
+        # the RR-ahead tail kernel's phases (clock64 in the calibration launch, summed over lanes): where one
+        # path-bounce of the specular chains that set the tail's length spends its cycles
+        nb = calib["tail_bounces"]
+        roof["tail_profile"] = {
+            "path_bounces": nb, "longest_chain_bounces": calib["tail_max_bounces"],
+            "cycles_per_bounce": {k: round(calib[f"tail_cycles_{k}"] / nb, 1)
+                                  for k in ("body", "shadow", "closest", "head")},
+            "source": "wf_tail_rr calibration launch (collect_stats), clock64 per phase"}
     return roof
 
 
@@ -306,11 +329,12 @@ def traversal_record(roof):
     """The metric's "traversal HBM GB/s": the closest-hit traversal kernel of the timed run (the fused
     bounce kernel when the BVH is traversed inside it): its algorithmic global-memory rate, and for an
     LDS-staged BVH the algorithmic traversal bytes it read from LDS; measured HBM bytes are roofline.traffic."""
-    name = next((k for k in ("extend", "bounce", "path") if k in roof["stages"]), None)
+    name = next((k for k in ("trace", "extend", "bounce", "path") if k in roof["stages"]), None)
     if name is None:
         return None
     e = roof["stages"][name]
-    out = {"kernel": {"extend": "wf_extend", "bounce": "wf_bounce", "path": "nh_path_kernel"}[name],
+    out = {"kernel": {"trace": "wf_trace_pt2", "extend": "wf_extend", "bounce": "wf_bounce",
+                      "path": "nh_path_kernel"}[name],
            "global_gbs": e["global_gbs"], "frac_of_hbm_peak": round(e["global_gbs"] / HBM_PEAK_GBS, 4),
            "avg_launch_ms": e["avg_launch_ms"]}
     if "lds_work_gbs" in e:
@@ -513,17 +537,21 @@ def traversal_1m(nh, args, local):
     a.dump_framebuffer = None
     r = run_workload(nh, a, "bumpy1m", args.traversal_1m_steps, 1, local)
     roof = r["roof"]
-    e = roof["stages"]["extend"]
-    key1m = f"bumpy1m_{r['W']}x{r['H']}_r{r['R']}_{args.traversal}_{args.mode}/extend"
+    stage = "trace" if "trace" in roof["stages"] else "extend"
+    e = roof["stages"][stage]
+    key1m = f"bumpy1m_{r['W']}x{r['H']}_r{r['R']}_{args.traversal}_{args.mode}/{stage}"
     traffic, source = pmc_traffic(key1m)
     rec1m = pmc_record(key1m)
     out = {"workload": r["desc"], "msamples_s": round(r["samples"] / r["elapsed"] / 1e6, 3),
-           "kernel": "wf_trace_pt (persistent 4-wide closest-hit traversal)" if roof["node_bytes"] == 128 else "wf_extend",
+           "kernel": ({"trace": "wf_trace_pt2 (persistent 4-wide closest-hit + any-hit traversal, one launch per bounce)",
+                       "extend": "wf_trace_pt (persistent 4-wide closest-hit traversal)"}[stage]
+                      if roof["node_bytes"] == 128 else "wf_extend"),
            "avg_launch_ms": e["avg_launch_ms"], "algorithmic_bytes_per_launch": e["global_bytes_per_launch"],
            "achieved_gbs": e["global_gbs"], "frac": round(e["global_gbs"] / HBM_PEAK_GBS, 4), "target_frac": 0.40,
            "nodes_per_query": e.get("nodes_per_query"), "prims_per_query": e.get("prims_per_query"),
            "node_bytes": roof["node_bytes"],
-           "bytes": "algorithmic: nodes x node_bytes + primitive tests x 48 B + 48 B ray/hit per query",
+           "bytes": "algorithmic: nodes x node_bytes + primitive tests x 48 B + the queue bytes (ray in, hit / occlusion "
+                    "out) per query",
            "traffic": traffic, "traffic_source": source or "not collected for this workload",
            "traffic_gbs": round(traffic / (e["avg_launch_ms"] * 1e-3) / 1e9, 1) if traffic else None,
            "l2_hit_rate": rec1m.get("l2_hit_rate"),

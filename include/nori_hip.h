@@ -308,6 +308,14 @@ typedef struct nh_render_stats {
     uint64_t tails_async;
     /* wavefront path pools the last render drove (NH_POOLS, else 2, or 3 for scenes with mirror / dielectric BSDFs) */
     uint64_t pools_active;
+    /* 1 when the last wavefront render traced each bounce's closest-hit and any-hit queries in one persistent
+       launch (deep BVHs, 4-wide tree): its time is in kernel_ms_extend, kernel_ms_shadow stays 0 */
+    uint64_t trace_fused;
+    /* RR-ahead tail kernel (wf_tail_rr), collect_stats only: cycles its lanes spent in the shade body, the light
+       sample's any-hit query, the next closest hit and the next vertex's head (clock64, summed over lanes), the
+       path-bounces it ran and its longest chain (bounces of one path) */
+    uint64_t tail_cycles_body, tail_cycles_shadow, tail_cycles_closest, tail_cycles_head;
+    uint64_t tail_bounces, tail_max_bounces;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;

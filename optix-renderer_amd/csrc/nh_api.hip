@@ -78,7 +78,7 @@ struct WfPool {
     enum State { IDLE, ENQUEUE, COUNTS, SPLAT, FINISH } state = IDLE;
     WfJob job{};
     WfLaunch L{};
-    bool persistent = false, wide = false, tail = false, draining = false;
+    bool persistent = false, wide = false, trace2 = false, tail = false, draining = false;
     bool fused = false, sorted = false;  // one wf_bounce kernel per bounce (LDS-staged BVH); material-sorted queue
     bool rr = false;                     // fused kernels with the next vertex's Russian roulette ahead (wf_bounce_rr)
     bool shade_sorted = false;           // wf_shade entries in BSDF-type order (deep BVHs, mixed materials)
@@ -988,6 +988,11 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     // unless the reference's own visit order was asked for
     p.wide = p.persistent && j.ordered && c->tv.wnodes != nullptr;
     if (const char *e = std::getenv("NH_WIDE")) p.wide = p.wide && e[0] != '0';
+    // both queries of a bounce in one persistent launch (one tail per bounce instead of two); NH_TRACE2=0: the
+    // closest-hit and any-hit launches of round 3
+    p.trace2 = p.wide;
+    if (const char *e = std::getenv("NH_TRACE2")) p.trace2 = p.trace2 && e[0] != '0';
+    c->stats.trace_fused = p.trace2 ? 1 : 0;
     // spill words per lane: binary entries are one word, wide entries two (8-B aligned)
     const int spill_words = p.wide ? 2 * c->depth_wide : (c->depth + 1) / 2 * 2;
     if (p.persistent && p.spill_words < spill_words) {
@@ -1055,6 +1060,7 @@ static void chunk_swap(WfPool &a, WfPool &b) {
     std::swap(a.L, b.L);
     std::swap(a.persistent, b.persistent);
     std::swap(a.wide, b.wide);
+    std::swap(a.trace2, b.trace2);
     std::swap(a.tail, b.tail);
     std::swap(a.draining, b.draining);
     std::swap(a.fused, b.fused);
@@ -1161,12 +1167,19 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
         else p.state = WfPool::COUNTS;
         return NH_OK;
     }
-    nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, p.persistent, p.wide, bound, c->depth, p.stream);
-    HIP_TRY(c, hipEventRecord(ev[1], p.stream));
-    // bounce 0 has no shadow rays (the launch still runs: the kernels read the count on the device)
-    nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, p.persistent, p.wide, it == 0 ? 0 : bound, c->depth,
-                        p.stream);
-    HIP_TRY(c, hipEventRecord(ev[2], p.stream));
+    if (p.trace2) {  // both queries in one launch: its time counts as the extend stage's, the shadow stage's is 0
+        nh::launch_wf_trace2(c->d_scene, c->tv, L, ordered, stats, it == 0 ? bound : 2 * bound, p.stream);
+        HIP_TRY(c, hipEventRecord(ev[1], p.stream));
+        HIP_TRY(c, hipEventRecord(ev[2], p.stream));
+    } else {
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, p.persistent, p.wide, bound, c->depth,
+                            p.stream);
+        HIP_TRY(c, hipEventRecord(ev[1], p.stream));
+        // bounce 0 has no shadow rays (the launch still runs: the kernels read the count on the device)
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, p.persistent, p.wide, it == 0 ? 0 : bound,
+                            c->depth, p.stream);
+        HIP_TRY(c, hipEventRecord(ev[2], p.stream));
+    }
     if (it > 0 && (int64_t)bound <= p.tail_at) {
         nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, p.wide, bound, c->depth, p.stream);
         HIP_TRY(c, hipGetLastError());
@@ -1484,6 +1497,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     rc = ensure_pixel_list(c, q);
     if (rc) return rc;
     c->stats.node_bytes = 64;  // binary tree unless a wavefront pool picks the 4-wide one
+    c->stats.trace_fused = 0;
     c->stats.lds_scene = 0;
     c->stats.fused_bounce = 0;
     if (q->clear) {
@@ -1609,6 +1623,15 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         HIP_TRY(c, hipMemcpy(hs, c->counters, sizeof(hs), hipMemcpyDeviceToHost));
         for (int sh = 0; sh < kStatShards; ++sh)
             for (int j = 0; j < kStatStride; ++j) h[j] += hs[sh * kStatStride + j];
+        h[kStatTailClk + 5] = 0;  // the longest tail chain: a max over the shards, not a sum
+        for (int sh = 0; sh < kStatShards; ++sh)
+            h[kStatTailClk + 5] = std::max(h[kStatTailClk + 5], hs[sh * kStatStride + kStatTailClk + 5]);
+        c->stats.tail_cycles_body += h[kStatTailClk];
+        c->stats.tail_cycles_shadow += h[kStatTailClk + 1];
+        c->stats.tail_cycles_closest += h[kStatTailClk + 2];
+        c->stats.tail_cycles_head += h[kStatTailClk + 3];
+        c->stats.tail_bounces += h[kStatTailClk + 4];
+        c->stats.tail_max_bounces = std::max<uint64_t>(c->stats.tail_max_bounces, h[kStatTailClk + 5]);
         const unsigned long long *cl = h, *an = h + kStatAny, *tc = h + kStatTail, *ta = h + kStatTailAny;
         c->stats.ray_queries += cl[0] + an[0] + tc[0] + ta[0];
         c->stats.nodes_visited += cl[1] + an[1] + tc[1] + ta[1];

@@ -67,6 +67,8 @@ struct DenoiseLaunch {
 // the tail kernel, one copy per XCD (workgroup b adds to copy b % 8) so the per-wave atomics of
 // concurrent workgroups do not serialise on one address.
 constexpr int kStatShards = 8, kStatStride = 32, kStatAny = 8, kStatTail = 16, kStatTailAny = 20;
+// wf_tail_rr calibration clocks: 4 phase cycle sums, path-bounces, longest chain (max over shards)
+constexpr int kStatTailClk = 24;
 __device__ __forceinline__ unsigned long long *stat_shard(unsigned long long *c) {
     return c + (blockIdx.x & (kStatShards - 1)) * kStatStride;
 }
@@ -153,6 +155,9 @@ namespace nh {
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                      bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st);
 // sort: entries shaded in the order of their hit's BSDF type within each workgroup (material-sorted shading)
+// closest-hit + any-hit queries of a bounce in one persistent launch (4-wide tree); bound = both queues' sum
+void launch_wf_trace2(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
+                      int bound, hipStream_t st);
 void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool sort, int bound,
                      hipStream_t st);
 // fused shade + any-hit + closest-hit bounce for LDS-staged BVHs; sort = material-sorted output queue

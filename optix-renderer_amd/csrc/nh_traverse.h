@@ -636,7 +636,9 @@ NHD int wide_first(bool va, float na, bool vb, float nb) {
 
 // Resumable 4-wide traversal (same step protocol as Tracer: one wide node, one primitive or one
 // stack pop per step). Answers: smallest t, ties to the largest leaf-order position k.
-template <bool ORDERED, bool ANY, bool STATS, class Stack>
+// RT: the query kind is a run-time property of the lane (any_q, set before begin()), so one persistent launch
+// serves closest-hit and any-hit rays together (wf_trace_pt2); otherwise ANY fixes it.
+template <bool ORDERED, bool ANY, bool STATS, class Stack, bool RT = false>
 struct Tracer4 {
     F3 o, d, r;
     float mint, maxt;
@@ -645,7 +647,10 @@ struct Tracer4 {
     int sp;
     bool found, done;
     bool finite_r;  // all 1/d components finite: branch-free box tests (box_test_finite)
+    bool any_q;     // RT: this lane's query is an any-hit query
     Hit best;
+
+    NHD bool is_any() const { return RT ? any_q : ANY; }
 
     NHD void begin(const DScene &S, const Traversal &tv, F3 o_, F3 d_, float mint_, float maxt_, TravStats &st) {
         o = o_;
@@ -802,7 +807,7 @@ struct Tracer4 {
             hit = sphere_test(a, o, d, mint, maxt, t);
         }
         if (hit) {
-            if (ANY) {
+            if (is_any()) {
                 found = true;
                 done = true;
                 return true;

@@ -413,6 +413,98 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
     if (STATS) flush_trav_stats(stat_shard(L.counters) + (ANY ? 8 : 0), queries, st);
 }
 
+// Both traversal queries of a bounce in one persistent launch (deep BVHs, 4-wide tree): the closest hit of every
+// live path's ray (wf_extend's queue) and the any hit of every queued light sample (wf_shadow's), each answered
+// exactly as wf_trace_pt answers it -- same Tracer4 visits, tests and order per ray; only which lane runs which
+// ray changes. A wave takes batches from the closest-hit segments first (the longer queries) and then from the
+// any-hit segments, so the launch has one tail (its slowest rays) where two launches had two, and an XCD whose
+// closest-hit work is done moves on to shadow rays while others finish.
+template <bool ORDERED, bool STATS>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES))) void wf_trace_pt2(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+    __shared__ uint32_t stk[kRingEntries * 128];
+    __shared__ float4 s_top[kTopNodes * kWideF4];  // the top of the 4-wide tree (nodes 0 .. n_top-1)
+    const DScene &S = *Sp;
+    const int n_top = min(tv.n_top, kTopNodes);
+    for (int i = threadIdx.x; i < n_top * kWideF4; i += 128) s_top[i] = tv.wnodes[i];
+    __syncthreads();
+    const QView qe = queue_view(L.cnt_in), qs = queue_view(L.cnt_in + kCountGroup);
+    unsigned *fetch_e = L.cnt_in + 2 * kCountGroup, *fetch_s = L.cnt_in + 3 * kCountGroup;
+    const WfBuf &B = L.st.buf[L.in_q];
+    const int lane = threadIdx.x & 63;
+    using Stk = typename PtStack<true>::type;
+    Stk my_stk = PtStack<true>::make(stk, L);
+    // segments 0-7: closest-hit queue, 8-15: any-hit queue; a wave starts on its XCD's segment of each
+    int seg = blockIdx.x & (kQueueShards - 1), tried = 0;
+    int batch_next = 0, batch_end = 0;  // wave-uniform
+    bool batch_any = false;             // wave-uniform: the queue of the current batch
+    int slot = -1;                      // this lane's ray (queue slot), -1 = idle
+    Tracer4<ORDERED, false, STATS, Stk, true> tr;
+    TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
+    unsigned long long q_e = 0, q_s = 0;
+    for (;;) {
+        const bool idle = slot < 0;
+        const unsigned long long im = __ballot(idle);
+        if (im && (__popcll(im) >= NH_REFILL_MIN || im == ~0ull)) {
+            while (batch_next >= batch_end && tried < 2 * kQueueShards) {  // wave-uniform refill
+                const bool any = tried >= kQueueShards;
+                const int n = any ? qs.n : qe.n;
+                const int lo = (int)((long long)seg * n / kQueueShards);
+                const int hi = (int)((long long)(seg + 1) * n / kQueueShards);
+                unsigned base = 0;
+                if (lane == 0) base = atomicAdd(&(any ? fetch_s : fetch_e)[seg * kCountStride], (unsigned)kFetchBatch);
+                base = __shfl(base, 0, 64);
+                if ((long long)lo + base < hi) {
+                    batch_next = lo + (int)base;
+                    batch_end = min(batch_next + kFetchBatch, hi);
+                    batch_any = any;
+                } else {
+                    seg = (seg + 1) & (kQueueShards - 1);
+                    ++tried;
+                }
+            }
+            const int rank = __popcll(im & ((1ull << lane) - 1ull));
+            if (idle && batch_next + rank < batch_end) {
+                const int q = batch_next + rank;
+                float4 ro, rd;
+                if (batch_any) {
+                    slot = queue_slot(qs.pre, L.seg_cap, q);
+                    ro = L.st.sh_o[slot];
+                    rd = L.st.sh_d[slot];
+                    if (STATS) ++q_s;
+                } else {
+                    slot = queue_slot(qe.pre, L.seg_cap, q);
+                    load_ray(S, L, B, q, slot, ro, rd);
+                    // a zero BSDF direction (maxt = -inf) misses every primitive without a traversal
+                    if (STATS && rd.w >= ro.w) ++q_e;
+                }
+                tr.any_q = batch_any;
+                tr.begin(S, tv, xyz(ro), xyz(rd), ro.w, rd.w, batch_any ? st_s : st_e);
+            }
+            batch_next = min(batch_next + __popcll(im), batch_end);
+        }
+        if (!__any(slot >= 0)) break;
+        if (slot >= 0) {
+            if (!tr.done) {
+                if (STATS) {
+                    if (tr.any_q) tr.step(tv, my_stk, st_s, s_top, n_top);
+                    else tr.step(tv, my_stk, st_e, s_top, n_top);
+                } else {
+                    tr.step(tv, my_stk, st_e, s_top, n_top);
+                }
+            }
+            if (tr.done) {
+                if (tr.any_q) B.occl[L.st.sh_slot[slot]] = tr.found ? 1 : 0;
+                else B.hit[slot] = make_float4(tr.best.t, tr.best.u, tr.best.v, __int_as_float(tr.found ? tr.best.k : -1));
+                slot = -1;
+            }
+        }
+    }
+    if (STATS) {
+        flush_trav_stats(stat_shard(L.counters), q_e, st_e);
+        flush_trav_stats(stat_shard(L.counters) + 8, q_s, st_s);
+    }
+}
+
 // Where shade_path reads a path's state from: slot s of a path buffer (MemState), or the registers
 // of the previous shade step of the same thread (RegState, the tail kernel: no store -> load round
 // trip through memory per bounce on its latency-bound chains). Both hand shade_path the same values.
@@ -953,16 +1045,30 @@ __device__ __forceinline__ bool first_vertex(const DScene &S, const Traversal &t
     return true;
 }
 
+// Cycle counters of the tail kernel's phases (calibration launches only, CLK): shade body, the light sample's
+// any-hit query, the next closest hit, the next vertex's head -- summed over lanes -- and the path-bounces run.
+struct TailClocks {
+    unsigned long long c[4] = {0, 0, 0, 0};
+    unsigned long long bounces = 0, max_bounces = 0;
+};
+
 // body of the current vertex, its light sample's any-hit query, the next ray's closest hit, and the next
 // vertex's head; false once the path has ended (its radiance written)
-template <bool ORDERED, bool STATS>
+template <bool ORDERED, bool STATS, bool CLK = false>
 __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, const WfLaunch &L, PathV &v, Its &its,
                                         Hit &h, uint32_t *stk, int stride, TravStats &st_e, TravStats &st_s,
-                                        unsigned long long &q_e, unsigned long long &q_s) {
+                                        unsigned long long &q_e, unsigned long long &q_s, TailClocks *clk = nullptr) {
     PState o;
     bool nee = false;
     float4 so, sd;
+    unsigned long long t0 = 0, t1 = 0;
+    if constexpr (CLK) t0 = clock64();
     shade_body(S, tv, v, its, o, nee, so, sd);
+    if constexpr (CLK) {
+        t1 = clock64();
+        clk->c[0] += t1 - t0;
+        t0 = t1;
+    }
     if (nee) {  // the light sample's any-hit query, its outcome applied as the next shade_path would
         Hit hs;
         ++q_s;
@@ -978,12 +1084,27 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
         }
         o.flags &= ~(F_NEE | F_ZNAN);
     }
+    if constexpr (CLK) {
+        t1 = clock64();
+        clk->c[1] += t1 - t0;
+        t0 = t1;
+    }
     const bool live = o.rd.w >= o.ro.w;
     q_e += live ? 1 : 0;
     const bool found = live && trace<16, ORDERED, false, STATS, true>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h,
                                                                     stk, stride, st_e);
+    if constexpr (CLK) {
+        t1 = clock64();
+        clk->c[2] += t1 - t0;
+        t0 = t1;
+    }
     v = path_of(L, o);
-    if (!shade_head(S, tv, v, h, found, o.pdfmat, its)) {
+    const bool alive = shade_head(S, tv, v, h, found, o.pdfmat, its);
+    if constexpr (CLK) {
+        clk->c[3] += clock64() - t0;
+        clk->bounces++;
+    }
+    if (!alive) {
         write_radiance(L, v);
         return false;
     }
@@ -1065,18 +1186,30 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
     const WfBuf &B = L.st.buf[L.in_q];
     TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
     unsigned long long q_e = 0, q_s = 0;
+    TailClocks clk;
     for (int q = blockIdx.x * TB + threadIdx.x; q < qv.n; q += gridDim.x * TB) {
         const int s = queue_slot(qv.pre, L.seg_cap, q);
         PathV v;
         Hit h;
         Its its;
         load_post_head(S, tv, L, B, s, v, h, its);
-        while (rr_step<ORDERED, STATS>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s, q_e, q_s)) {
+        const unsigned long long b0 = clk.bounces;
+        while (rr_step<ORDERED, STATS, STATS>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s, q_e, q_s, &clk)) {
         }
+        if (STATS) clk.max_bounces = max(clk.max_bounces, clk.bounces - b0);
     }
     if (STATS) {  // the tail's own counter slots (kStatTail*), so stage rates stay per kernel
         flush_trav_stats(stat_shard(L.counters) + kStatTail, q_e, st_e);
         flush_trav_stats(stat_shard(L.counters) + kStatTailAny, q_s, st_s);
+        unsigned long long *dst = stat_shard(L.counters) + kStatTailClk;
+        for (int j = 0; j < 5; ++j) {
+            unsigned long long x = j < 4 ? clk.c[j] : clk.bounces;
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            if ((threadIdx.x & 63) == 0) atomicAdd(&dst[j], x);
+        }
+        unsigned long long m = clk.max_bounces;
+        for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, off, 64));
+        if ((threadIdx.x & 63) == 0) atomicMax(&dst[5], m);
     }
 }
 
@@ -1228,6 +1361,15 @@ static void launch_wf_tail_d(const DScene *S, const Traversal &tv, const WfLaunc
     else { if (stats) NH_TL(false, true) else NH_TL(false, false) }
 #undef NH_TL2
 #undef NH_TL
+}
+
+void launch_wf_trace2(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
+                      hipStream_t st) {
+    // the 4-wide tree is walked near-first only (nh_api.hip uses it for ordered traversals)
+    (void)ordered;
+    const int want = std::max(1, (bound + 127) / 128);
+    if (stats) launch_persistent<wf_trace_pt2<true, true>>(want, st, S, tv, L);
+    else launch_persistent<wf_trace_pt2<true, false>>(want, st, S, tv, L);
 }
 
 void launch_wf_tail(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool wide,

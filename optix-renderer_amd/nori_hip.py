@@ -162,7 +162,9 @@ class nh_render_stats(C.Structure):
                                   "tail_shadow_queries", "tail_shadow_nodes_visited", "tail_shadow_boxes_tested",
                                   "tail_shadow_prims_tested", "lds_scene", "fused_bounce", "comm_inits")] + [
         ("kernel_ms_denoise", C.c_double), ("launches_denoise", C.c_uint64), ("tails_async", C.c_uint64),
-        ("pools_active", C.c_uint64)]
+        ("pools_active", C.c_uint64), ("trace_fused", C.c_uint64)] + [
+        (n, C.c_uint64) for n in ("tail_cycles_body", "tail_cycles_shadow", "tail_cycles_closest", "tail_cycles_head",
+                                  "tail_bounces", "tail_max_bounces")]
 
 
 def _sig(name, res, *args):
