@@ -286,7 +286,7 @@ def roofline(args, calib, st, W, H, R):
         roof["traffic_gbs"] = round(traffic / (d["avg_launch_ms"] * 1e-3) / 1e9, 1)
         roof["traffic_frac"] = round(roof["traffic_gbs"] / HBM_PEAK_GBS, 4)
     if rec.get("valu_issue_frac") is not None:
-        roof["limiter"] = limiter_record(rec, key)
+        roof["limiter"] = limiter_record(rec, key, d["avg_launch_ms"], 5 if dom in ("trace", "extend") and wide else 4)
     if calib.get("tail_bounces"):
         # the RR-ahead tail kernel's phases (clock64 in the calibration launch, summed over lanes): where one
         # path-bounce of the specular chains that set the tail's length spends its cycles
@@ -299,25 +299,56 @@ def roofline(args, calib, st, W, H, R):
     return roof
 
 
-def limiter_record(rec, key):
-    """What bounds the kernel, from the committed PMC passes of the same command: the share of the CUs'
-    VALU issue slots used (SQ_INSTS_VALU / (256 CUs x kernel cycles): a wave64 VALU instruction occupies its
-    SIMD for one quad-cycle -- SQ_ACTIVE_INST_VALU ~ SQ_INSTS_VALU in quad-cycles -- so the 4 SIMDs of a CU
-    issue at most one per cycle together), rocprofv3's VALUBusy and VALUUtilization (active lanes per VALU
+VALU_CEILING_FILE = os.path.join(REPO, "profiles", "round4_valu_issue_events.jsonl")
+NOMINAL_CLOCK_HZ = 2.4e9  # MI355X peak engine clock (hipDeviceProp_t::clockRate on the box)
+
+
+def valu_ceiling(waves_per_simd):
+    """Measured VALU issue ceiling (tools/valu_issue.hip, scripts/valu_issue.sh; committed events.jsonl): wave64
+    instructions per CU-cycle at the nominal clock for independent chains at the given waves/SIMD -- the
+    select / compare / integer mix (the path kernels' bookkeeping) and fp32 FMA."""
+    try:
+        rows = [json.loads(x) for x in open(VALU_CEILING_FILE) if x.startswith("{") and "kind" in x]
+    except OSError:
+        return None
+    # the sweep measures 1, 2, 4 and 8 waves/SIMD: the largest of those not above the kernel's occupancy
+    w = max((r["waves_per_simd"] for r in rows if r["waves_per_simd"] <= waves_per_simd), default=None)
+    pick = lambda k: next((r["insts_per_cu_cycle_at_peak_clock"] for r in rows  # noqa: E731
+                           if r["kind"].startswith(k) and r["waves_per_simd"] == w), None)
+    mix, fma = pick("cmp+cndmask"), pick("v_fma_f32")
+    return {"mix": mix, "fma32": fma} if mix and fma else None
+
+
+def limiter_record(rec, key, avg_launch_ms=None, waves_per_simd=4):
+    """What bounds the kernel, from the committed PMC passes of the same command: VALU instructions per CU-cycle
+    (SQ_INSTS_VALU per launch over this run's launch time at the nominal clock) against the MEASURED issue ceiling
+    of the same occupancy (valu_ceiling: round 3 assumed one wave64 instruction per CU-cycle from the quad-cycle
+    counter; the microbenchmark shows 1.1-1.4), rocprofv3's VALUBusy and VALUUtilization (active lanes per VALU
     instruction: divergence), and the share of wave-cycles spent waiting (SQ_WAIT_ANY / SQ_WAVE_CYCLES)."""
-    out = {"valu_issue_frac": rec["valu_issue_frac"], "valu_busy_pct": rec.get("valu_busy_pct"),
-           "valu_utilization_pct": rec.get("valu_utilization_pct"), "wait_frac": rec.get("wait_frac"),
-           "valu_insts_per_launch": rec.get("valu_insts_per_launch"),
-           "quad_cycles_per_valu_inst": rec.get("quad_cycles_per_valu_inst"), "source": traffic_source_of(key)}
+    out = {"valu_busy_pct": rec.get("valu_busy_pct"), "valu_utilization_pct": rec.get("valu_utilization_pct"),
+           "wait_frac": rec.get("wait_frac"), "valu_insts_per_launch": rec.get("valu_insts_per_launch"),
+           "source": traffic_source_of(key)}
+    ceil = valu_ceiling(waves_per_simd)
+    frac = rec.get("valu_issue_frac")
+    if ceil and avg_launch_ms and rec.get("valu_insts_per_launch"):
+        rate = rec["valu_insts_per_launch"] / (avg_launch_ms * 1e-3 * NOMINAL_CLOCK_HZ * 256)
+        frac = rate / ceil["mix"]
+        out.update(valu_insts_per_cu_cycle=round(rate, 3), valu_issue_frac=round(frac, 3),
+                   valu_ceiling_insts_per_cu_cycle=ceil, valu_ceiling_waves_per_simd=waves_per_simd,
+                   valu_ceiling_source="profiles/round4_valu_issue_events.jsonl (tools/valu_issue.hip, the "
+                                       "select/compare/integer mix; fp32 FMA quoted beside it)")
+    else:
+        out["valu_issue_frac"] = frac
     util = rec.get("valu_utilization_pct")
     if util is not None and util < 60:
         out["note"] = (f"divergence-bound: only {util:.0f} % of the lanes are active per VALU instruction, with "
-                       f"{rec['valu_issue_frac']:.2f} of the issue slots used and waves waiting "
+                       f"{frac:.2f} of the measured issue ceiling used and waves waiting "
                        f"{rec.get('wait_frac', 0):.2f} of their cycles -- neither HBM- nor issue-bound")
-    elif rec["valu_issue_frac"] > 0.6:
+    elif frac is not None and frac > 0.8:
         out["note"] = "VALU-issue bound: its HBM bytes are the path state only"
     else:
-        out["note"] = "latency bound (waves waiting on dependent loads)"
+        out["note"] = (f"issue and latency: {frac:.2f} of the measured VALU issue ceiling, waves waiting "
+                       f"{rec.get('wait_frac', 0):.2f} of their cycles")
     return out
 
 
@@ -555,7 +586,8 @@ def traversal_1m(nh, args, local):
            "traffic": traffic, "traffic_source": source or "not collected for this workload",
            "traffic_gbs": round(traffic / (e["avg_launch_ms"] * 1e-3) / 1e9, 1) if traffic else None,
            "l2_hit_rate": rec1m.get("l2_hit_rate"),
-           "limiter": limiter_record(rec1m, key1m) if rec1m.get("valu_issue_frac") is not None else None,
+           "limiter": (limiter_record(rec1m, key1m, e["avg_launch_ms"], 5) if rec1m.get("valu_issue_frac") is not None
+                       else None),
            "note": "the ~176 MB tree is resident in the 256 MB MALL: measured HBM traffic (traffic) is well below "
                    "the algorithmic bytes; this kernel is bound by dependent-load latency",
            "steps": args.traversal_1m_steps, "spp": r["R"] * args.traversal_1m_steps, "timed": roof["timed"]}

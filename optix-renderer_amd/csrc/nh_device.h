@@ -194,6 +194,8 @@ struct DScene {
     // BSDF albedo textures (DBsdf::tex) and the png texels they index
     const DTex *texs;
     const float4 *texels;
+    // element counts of the record arrays above (LDS staging of small scenes, nh_wavefront.hip stage_records)
+    int n_shapes, n_bsdfs, n_faces, n_vertices, n_area_cdf;
 };
 
 NHD F3 ldv(const float *a, uint32_t i) { return f3(a[3 * i], a[3 * i + 1], a[3 * i + 2]); }

@@ -99,8 +99,8 @@ __device__ __forceinline__ F3 png_lookup(const float4 *texels, unsigned W, unsig
 
 // the albedo texture of a diffuse BSDF at the hit's uv (diffuse.cpp:101/:139, m_albedo->eval(bRec.uv)):
 // ConstantTexture, Checkerboard<Color3f> (checkerboard.cpp:29-47) or PNGTexture (PNGTexture.cpp:125-160)
-__device__ __noinline__ F3 tex_eval(const DScene &S, int ti, float u, float v) {
-    const DTex t = S.texs[ti];
+__device__ __noinline__ F3 tex_eval(const DTex *texs, const float4 *texels, int ti, float u, float v) {
+    const DTex t = texs[ti];
     if (t.type == TEX_CHECKERBOARD) {
         const float ox = u / t.sx - t.dx, oy = v / t.sy - t.dy;
         const int x = x86_f2i(ox) + (ox < 0.f), y = x86_f2i(oy) + (oy < 0.f);
@@ -118,13 +118,13 @@ __device__ __noinline__ F3 tex_eval(const DScene &S, int ti, float u, float v) {
             u += t.ou;
             v += t.ov;
         }
-        return png_lookup(S.texels + t.off, (unsigned)t.w, (unsigned)t.h, t.su, t.sv, u, v);
+        return png_lookup(texels + t.off, (unsigned)t.w, (unsigned)t.h, t.su, t.sv, u, v);
     }
     return f3(t.v1r, t.v1g, t.v1b);
 }
 // the diffuse albedo of BSDF b at uv: its constant colour unless it has a texture
 __device__ __forceinline__ F3 bsdf_albedo(const DScene &S, const DBsdf &b, float u, float v) {
-    if (__builtin_expect(b.tex != 0, 0)) return tex_eval(S, b.tex - 1, u, v);
+    if (__builtin_expect(b.tex != 0, 0)) return tex_eval(S.texs, S.texels, b.tex - 1, u, v);
     return f3(b.ar, b.ag, b.ab);
 }
 

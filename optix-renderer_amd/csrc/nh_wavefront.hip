@@ -205,6 +205,45 @@ __device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, cons
     return t;
 }
 
+// float4 count of the dynamic LDS of the RR-ahead fused kernels: BVH + pair records + the scene's record arrays
+__host__ __device__ __forceinline__ int rr_lds_f4(const WfLaunch &L) {
+    int n = small_pairs_offset_f4(L) + kPairF4 * (L.small_prims / 3);
+    for (int a = 0; a < kRecArrays; ++a) n += L.rec_n16[a];
+    return n;
+}
+
+// The scene's record arrays copied into LDS after the BVH (WfLaunch::rec_off / rec_n16, float4 units) and a view of
+// the scene whose record pointers address the copies. The RR-ahead kernels of LDS-sized scenes read every shading
+// record -- hit_info's shape, the BSDF and emitter records, the emitter CDF, the light's area CDF, faces and
+// vertices -- from LDS instead of an L2 / MALL round trip (each bounce of a specular tail chain makes ~10 such
+// dependent reads). The same values, so the same arithmetic. Called by the whole workgroup before
+// stage_small_scene's barrier.
+__device__ __forceinline__ DScene stage_records(const DScene &S, const WfLaunch &L, float4 *lds) {
+    const float4 *src[kRecArrays] = {
+        reinterpret_cast<const float4 *>(S.shapes), reinterpret_cast<const float4 *>(S.bsdfs),
+        reinterpret_cast<const float4 *>(S.emitters), reinterpret_cast<const float4 *>(S.emitter_cdf),
+        reinterpret_cast<const float4 *>(S.area_cdf), reinterpret_cast<const float4 *>(S.F),
+        reinterpret_cast<const float4 *>(S.V), reinterpret_cast<const float4 *>(S.N),
+        reinterpret_cast<const float4 *>(S.UV), reinterpret_cast<const float4 *>(S.T),
+        reinterpret_cast<const float4 *>(S.BT)};
+#pragma unroll
+    for (int a = 0; a < kRecArrays; ++a)
+        for (int i = threadIdx.x; i < L.rec_n16[a]; i += blockDim.x) lds[L.rec_off[a] + i] = src[a][i];
+    DScene R = S;
+    R.shapes = reinterpret_cast<const DShape *>(lds + L.rec_off[0]);
+    R.bsdfs = reinterpret_cast<const DBsdf *>(lds + L.rec_off[1]);
+    R.emitters = reinterpret_cast<const DEmitter *>(lds + L.rec_off[2]);
+    R.emitter_cdf = reinterpret_cast<const float *>(lds + L.rec_off[3]);
+    R.area_cdf = reinterpret_cast<const float *>(lds + L.rec_off[4]);
+    R.F = reinterpret_cast<const uint32_t *>(lds + L.rec_off[5]);
+    R.V = reinterpret_cast<const float *>(lds + L.rec_off[6]);
+    R.N = reinterpret_cast<const float *>(lds + L.rec_off[7]);
+    R.UV = reinterpret_cast<const float *>(lds + L.rec_off[8]);
+    R.T = reinterpret_cast<const float *>(lds + L.rec_off[9]);
+    R.BT = reinterpret_cast<const float *>(lds + L.rec_off[10]);
+    return R;
+}
+
 template <bool SMALL>
 __device__ __forceinline__ Traversal traversal_view(const Traversal &tv, const WfLaunch &L, float4 *lds) {
     if constexpr (SMALL) return stage_small_scene(tv, L, lds);
@@ -1117,11 +1156,11 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScen
     __shared__ uint32_t stk[16 * 256];
     __shared__ unsigned s_n[kMatClasses], s_off[kMatClasses], s_base;
     extern __shared__ float4 lds_scene[];
-    const DScene &S = *Sp;
     const QView qv = queue_view(L.cnt_in);
     const int base = blockIdx.x * 256;
     if (base >= qv.n) return;  // whole workgroup
     if (threadIdx.x < kMatClasses) s_n[threadIdx.x] = 0u;  // visible after the staging barrier
+    const DScene S = stage_records(*Sp, L, lds_scene);
     const Traversal tv = stage_small_scene<true>(tv_g, L, lds_scene);
     const int shard = blockIdx.x & (kQueueShards - 1);
     const int q = base + (int)threadIdx.x;
@@ -1180,7 +1219,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
     const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[16 * TB];
     extern __shared__ float4 lds_scene[];
-    const DScene &S = *Sp;
+    const DScene S = stage_records(*Sp, L, lds_scene);
     const Traversal tv = stage_small_scene<true>(tv_g, L, lds_scene);
     const QView qv = queue_view(L.cnt_in);
     const WfBuf &B = L.st.buf[L.in_q];
@@ -1281,6 +1320,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAV
 namespace nh {
 
 int tree_top_nodes() { return kTopNodes; }
+int rr_records_base_f4(const WfLaunch &L) { return small_pairs_offset_f4(L) + kPairF4 * (L.small_prims / 3); }
 
 // Persistent grids hold exactly the workgroups that are resident at once (occupancy of this
 // instantiation x CUs, at most kPersistentBlocks -- the spill area's size): a workgroup that
@@ -1401,7 +1441,7 @@ void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L
                          int bound, hipStream_t st) {
     int blocks = std::max(1, (bound + 255) / 256);
     blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
-    const size_t lds = 16 * ((size_t)small_pairs_offset_f4(L) + (size_t)kPairF4 * (L.small_prims / 3));
+    const size_t lds = 16 * (size_t)rr_lds_f4(L);
 #define NH_FB(O, T, SO) hipLaunchKernelGGL((wf_bounce_rr<O, T, SO>), dim3(blocks), dim3(256), lds, st, S, tv, L)
     if (ordered) {
         if (stats) { if (sort) NH_FB(true, true, true); else NH_FB(true, true, false); }
@@ -1420,7 +1460,7 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
     const char *w = std::getenv("NH_TAIL_RR_WAVES");  // register budget: 4 waves/SIMD (default) or 1
     const bool w1 = w && std::atoi(w) == 1;
     const dim3 grid(std::min(std::max(1, (bound + tb - 1) / tb), kTraceBlocksMax));
-    const size_t lds = 16 * ((size_t)small_pairs_offset_f4(L) + (size_t)kPairF4 * (L.small_prims / 3));
+    const size_t lds = 16 * (size_t)rr_lds_f4(L);
 #define NH_TR(O, T)                                                                                         \
     do {                                                                                                    \
         if (tb == 256) hipLaunchKernelGGL((wf_tail_rr<O, T, 256, 1>), grid, dim3(256), lds, st, S, tv, L);      \
