@@ -127,7 +127,6 @@ struct nh_ctx {
     int width = 0, height = 0, border = 0, n_emitters = 0, integrator = 0;
     nh_filter filter{};
     nhd::DScene S{};
-    size_t rec_bytes[kRecArrays] = {};  // record array bytes the RR-ahead kernels stage in LDS
     nhd::DScene *d_scene = nullptr;  // device copy of S read by the kernels
     nhd::Traversal tv{};
     std::vector<void *> scene_bufs, bvh_bufs;
@@ -325,6 +324,7 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         o.radius = s.radius;
         o.pdf_off = (int)s.pdf_offset;
         o.pdf_norm = s.pdf_normalization;
+        o.tex_uv = d->bsdfs[s.bsdf].type == NH_BSDF_DIFFUSE && d->bsdfs[s.bsdf].albedo_texture != 0;
     }
     std::vector<DBsdf> db(d->n_bsdfs);
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
@@ -419,14 +419,6 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     S.n_faces = (int)d->n_faces;
     S.n_vertices = (int)d->n_vertices;
     S.n_area_cdf = (int)d->n_area_cdf;
-    {  // bytes of the record arrays the RR-ahead kernels stage in LDS (stage_records' order)
-        const size_t nv3 = 3 * nv * sizeof(float);
-        const size_t b[kRecArrays] = {d->n_shapes * sizeof(nhd::DShape), d->n_bsdfs * sizeof(nhd::DBsdf),
-                                      d->n_emitters * sizeof(nhd::DEmitter), (d->n_emitters + 1) * sizeof(float),
-                                      d->n_area_cdf * sizeof(float), 3 * (size_t)d->n_faces * sizeof(uint32_t), nv3,
-                                      nv3, 2 * nv * sizeof(float), nv3, nv3};
-        for (int a = 0; a < kRecArrays; ++a) c->rec_bytes[a] = b[a];
-    }
     if (d->integrator < NH_INTEGRATOR_PATH_MIS || d->integrator > NH_INTEGRATOR_DIRECT)
         return fail(c, "unknown integrator"), NH_ERR_INVALID;
     S.integrator = d->integrator;
@@ -1023,24 +1015,8 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     p.fused = small && !p.persistent && c->depth <= 16;
     if (const char *e = std::getenv("NH_FUSED")) p.fused = p.fused && e[0] != '0';
     p.sorted = p.fused && c->n_bsdf_types > 1;
-    // the RR-ahead kernels also read the scene's records from LDS (stage_records): they need them to fit
-    std::memset(L.rec_off, 0, sizeof(L.rec_off));
-    std::memset(L.rec_n16, 0, sizeof(L.rec_n16));
-    bool recs_fit = false;
-    if (small) {
-        int off = nh::rr_records_base_f4(L);
-        size_t total = 0;
-        for (int a = 0; a < kRecArrays; ++a) {
-            L.rec_off[a] = off;
-            L.rec_n16[a] = (int)((c->rec_bytes[a] + 15) / 16);
-            off += L.rec_n16[a];
-            total += c->rec_bytes[a];
-        }
-        recs_fit = total <= kSmallRecBytes;
-        if (!recs_fit) std::memset(L.rec_n16, 0, sizeof(L.rec_n16));
-    }
-    p.rr = p.fused && recs_fit;
-    if (const char *e = std::getenv("NH_RR_AHEAD")) p.rr = p.rr && e[0] != '0';
+    p.rr = p.fused;
+    if (const char *e = std::getenv("NH_RR_AHEAD")) p.rr = p.fused && e[0] != '0';
     // material-sorted shading on deep BVHs is measured slower (C3 1640 -> 1590, C5 1542 -> 1526 Msamples/s:
     // the extra hit read and barriers cost more than the divergence saved): off unless NH_SORT_SHADE=1
     p.shade_sorted = false;

@@ -132,7 +132,8 @@ struct alignas(16) DShape {
     float cx, cy, cz, radius;
     int pdf_off;
     float pdf_norm;
-    int pad0, pad1;
+    int tex_uv;  // its BSDF reads Intersection::uv (a textured diffuse albedo): hit_info computes uv only then
+    int pad1;
 };
 struct alignas(16) DBsdf {
     int type;

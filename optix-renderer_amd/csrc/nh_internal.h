@@ -127,7 +127,6 @@ struct WfState {
 constexpr int kCountGroup = kQueueShards * kCountStride;
 constexpr int kCountSlot = 4 * kCountGroup;
 
-constexpr int kRecArrays = 11;
 struct WfLaunch {
     WfState st;
     int n_paths, n_list, s0;
@@ -143,10 +142,6 @@ struct WfLaunch {
     // small scenes: float4 / int2 counts of the BVH arrays staged into LDS by the traversal
     // kernels (0 = traverse from HBM)
     int small_nodes, small_leaves, small_prims;
-    // small scenes, fused bounce kernels: the scene's record arrays (shapes, BSDFs, emitters, emitter CDF, area
-    // CDFs, faces, V, N, UV, T, BT) copied into LDS after the BVH too, at these float4 offsets / float4 counts of
-    // the dynamic LDS (all counts 0: records read from global memory)
-    int rec_off[kRecArrays], rec_n16[kRecArrays];
     // persistent traversal: per-lane stack spill area (kPersistentBlocks * 128 lanes x spill_depth
     // 32-bit words; the 4-wide traversal spills (ref, distance) pairs)
     uint32_t *trav_spill;
@@ -156,11 +151,7 @@ struct WfLaunch {
 // persistent traversal grid: 16 workgroups of 128 lanes per CU (the 8 waves/SIMD its registers allow)
 constexpr int kPersistentBlocks = 256 * 16;
 constexpr size_t kSmallSceneBytes = 16384;
-// scene records (shapes, BSDFs, emitters, CDFs, faces, vertex attributes) the RR-ahead kernels stage in LDS
-constexpr size_t kSmallRecBytes = 16384;
 namespace nh {
-// float4 offset of the scene-record region in the RR-ahead kernels' dynamic LDS (after BVH + pair records)
-int rr_records_base_f4(const WfLaunch &L);
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                      bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st);
 // sort: entries shaded in the order of their hit's BSDF type within each workgroup (material-sorted shading)

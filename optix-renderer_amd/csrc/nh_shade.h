@@ -21,11 +21,16 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
     if (sh.type == SHAPE_SPHERE) {
         its.p = add(o, scl(h.t, d));
         F3 n = normalized(sub(its.p, f3(sh.cx, sh.cy, sh.cz)));
-        F3 mn = neg(n);
-        float theta = f_acos(mn.z), phi = f_atan2(mn.y, mn.x);
-        if (phi < 0) phi += 2 * kPi;
-        its.u = phi / (2.f * kPi);
-        its.v = theta / kPi;
+        // uv (two fp64-evaluated transcendentals) only matters to a textured albedo (bsdf_albedo is its only
+        // reader): the specular chains that set the tail's length skip it
+        its.u = its.v = 0.f;
+        if (sh.tex_uv) {
+            F3 mn = neg(n);
+            float theta = f_acos(mn.z), phi = f_atan2(mn.y, mn.x);
+            if (phi < 0) phi += 2 * kPi;
+            its.u = phi / (2.f * kPi);
+            its.v = theta / kPi;
+        }
         F3 t = normalized(cross(f3(0, 0, 1), n));
         its.sh.s = t;
         its.sh.t = cross(n, t);
@@ -45,7 +50,7 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
     const int local = __float_as_int(a.w);
     const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + local);
     const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
-    if (sh.has_uv) {
+    if (sh.has_uv && sh.tex_uv) {  // texture coordinates, read only by a textured albedo
         its.u = bx * S.UV[2 * i0] + by * S.UV[2 * i1] + bz * S.UV[2 * i2];
         its.v = bx * S.UV[2 * i0 + 1] + by * S.UV[2 * i1 + 1] + bz * S.UV[2 * i2 + 1];
     }

@@ -312,6 +312,70 @@ NHD bool leaf_test(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float 
     return false;
 }
 
+// The primitives of one leaf tested by a G-lane group that carries one ray (every lane the same ray, the same
+// traversal): lane j of the group tests primitive start + j (+ G, + 2G for longer leaves), each against the maxt at
+// the leaf's entry, and the group reduces the accepted hits to the smallest t, ties to the largest leaf position k.
+// That is the sequential loop's answer: it accepts each primitive whose t <= the running maxt, so its last accepted
+// primitive is the latest one of the leaf's minimum t; a candidate above that minimum never wins either way (a
+// sphere's candidate t does not depend on maxt: tmin if it is past mint, else tmax). The update across leaves is the
+// sequential one (t < maxt, or a later primitive on a tie). Any hit: the group's OR. Counters match the sequential
+// loop's (every primitive of the leaf; an any-hit query up to its first hit).
+template <bool ANY, bool STATS, int G>
+NHD bool leaf_test_coop(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float &maxt, Hit &best, bool &found,
+                        TravStats &st) {
+    const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane & ~(G - 1);
+    const int2 lf = tv.leaves[leaf];
+    for (int base = lf.x, e = lf.x + lf.y; base < e; base += G) {
+        const int k = base + gl;
+        bool acc = false;
+        float t = INFINITY, u = 0.f, v = 0.f;
+        if (k < e) {
+            const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
+            if (prim_is_tri(c)) acc = tri_test_nb(a, b, c, o, d, mint, maxt, t, u, v);
+            else acc = sphere_test(a, o, d, mint, maxt, t);
+        }
+        const unsigned long long grp = (__ballot(acc) >> gbase) & ((1ull << G) - 1ull);
+        if (ANY) {
+            if (grp) {
+                if (STATS && gl == 0) st.prims += (uint32_t)(__ffsll((long long)grp));  // up to the first hit
+                return true;
+            }
+            if (STATS && gl == 0) st.prims += (uint32_t)min(G, e - base);
+            continue;
+        }
+        if (STATS && gl == 0) st.prims += (uint32_t)min(G, e - base);
+        if (!grp) continue;
+        float rt = acc ? t : INFINITY;
+        int rk = acc ? k : -1;
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) {
+            const float ot = __shfl_xor(rt, off, G);
+            const int ok = __shfl_xor(rk, off, G);
+            if (ok >= 0 && (rk < 0 || ot < rt || (ot == rt && ok > rk))) {
+                rt = ot;
+                rk = ok;
+            }
+        }
+        const float wu = __shfl(u, rk - base, G), wv = __shfl(v, rk - base, G);
+        if (rt < maxt || rk > best.k) {
+            found = true;
+            maxt = rt;
+            best.t = rt;
+            best.u = wu;
+            best.v = wv;
+            best.k = rk;
+        }
+    }
+    return false;
+}
+
+template <bool ANY, bool STATS, bool PAIRS, int G>
+NHD bool leaf_any(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float &maxt, Hit &best, bool &found,
+                  TravStats &st) {
+    if constexpr (G > 1) return leaf_test_coop<ANY, STATS, G>(tv, leaf, o, d, mint, maxt, best, found, st);
+    else return leaf_test<ANY, STATS, PAIRS>(tv, leaf, o, d, mint, maxt, best, found, st);
+}
+
 // Child box of an inner node: side 0 = left, 1 = right.
 NHD bool child_box_test(const float4 &n0, const float4 &n1, const float4 &n2, int side, F3 o, F3 d, F3 r, float mint,
                         float maxt, float &near_t) {
@@ -323,23 +387,26 @@ NHD bool child_box_test(const float4 &n0, const float4 &n1, const float4 &n2, in
 // entries are `stride` words apart (lane-interleaved, bank-conflict free). An entry is
 // (parent inner node << 1) | side: the deferred child's box is tested again when it is
 // popped, with the maxt of that moment -- the reference's visit-time test verbatim.
-template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool PAIRS = false>
+// G > 1: the ray is carried by a G-lane group (leaf primitives tested cooperatively, leaf_test_coop).
+template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool PAIRS = false, int G = 1>
 NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, float maxt, Hit &best, uint32_t *stk,
                int stride, TravStats &st) {
     // adaptive ray epsilon (bvh.cpp:407-410)
     if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));
+    // counters: one lane of a group carrying the ray counts for it
+    const bool lead = G == 1 || (threadIdx.x & (G - 1)) == 0;
     best.k = -1;
     best.t = INFINITY;
     if (S.root_kind == 0 || maxt < mint) return false;
     const F3 r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     bool found = false;
     float near_t;
-    if (STATS) st.boxes++;
+    if (STATS && lead) st.boxes++;
     if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d, r,
                   mint, maxt, near_t))
         return false;
     if (S.root_kind == 2) {
-        bool any = leaf_test<ANY, STATS, PAIRS>(tv, 0, o, d, mint, maxt, best, found, st);
+        bool any = leaf_any<ANY, STATS, PAIRS, G>(tv, 0, o, d, mint, maxt, best, found, st);
         return ANY ? any : found;
     }
     int sp = 0;
@@ -348,7 +415,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
         while (cur >= 0) {
             const float4 n0 = tv.nodes[4 * cur], n1 = tv.nodes[4 * cur + 1], n2 = tv.nodes[4 * cur + 2];
             const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * cur + 3]);
-            if (STATS) { st.nodes++; st.boxes += 2; }
+            if (STATS && lead) { st.nodes++; st.boxes += 2; }
             float nl, nr;
             const bool hl = box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, nl);
             const bool hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
@@ -369,7 +436,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
                 cur = next;
                 continue;
             }
-            if (leaf_test<ANY, STATS, PAIRS>(tv, ~next, o, d, mint, maxt, best, found, st)) return true;
+            if (leaf_any<ANY, STATS, PAIRS, G>(tv, ~next, o, d, mint, maxt, best, found, st)) return true;
             break;
         }
         // pop: re-test the deferred child against the current maxt
@@ -379,7 +446,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
             const uint32_t e = stk[sp * stride];
             const int parent = (int)(e >> 1), side = (int)(e & 1u);
             const float4 n0 = tv.nodes[4 * parent], n1 = tv.nodes[4 * parent + 1], n2 = tv.nodes[4 * parent + 2];
-            if (STATS) st.boxes++;
+            if (STATS && lead) st.boxes++;
             if (!child_box_test(n0, n1, n2, side, o, d, r, mint, maxt, near_t)) continue;
             const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * parent + 3]);
             const int ref = side ? n3.y : n3.x;
@@ -387,7 +454,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
                 cur = ref;
                 break;
             }
-            if (leaf_test<ANY, STATS, PAIRS>(tv, ~ref, o, d, mint, maxt, best, found, st)) return true;
+            if (leaf_any<ANY, STATS, PAIRS, G>(tv, ~ref, o, d, mint, maxt, best, found, st)) return true;
         }
         if (cur < 0) break;
     }

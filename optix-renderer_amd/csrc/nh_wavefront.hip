@@ -205,43 +205,9 @@ __device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, cons
     return t;
 }
 
-// float4 count of the dynamic LDS of the RR-ahead fused kernels: BVH + pair records + the scene's record arrays
+// float4 count of the dynamic LDS of the fused kernels: BVH + pair records
 __host__ __device__ __forceinline__ int rr_lds_f4(const WfLaunch &L) {
-    int n = small_pairs_offset_f4(L) + kPairF4 * (L.small_prims / 3);
-    for (int a = 0; a < kRecArrays; ++a) n += L.rec_n16[a];
-    return n;
-}
-
-// The scene's record arrays copied into LDS after the BVH (WfLaunch::rec_off / rec_n16, float4 units) and a view of
-// the scene whose record pointers address the copies. The RR-ahead kernels of LDS-sized scenes read every shading
-// record -- hit_info's shape, the BSDF and emitter records, the emitter CDF, the light's area CDF, faces and
-// vertices -- from LDS instead of an L2 / MALL round trip (each bounce of a specular tail chain makes ~10 such
-// dependent reads). The same values, so the same arithmetic. Called by the whole workgroup before
-// stage_small_scene's barrier.
-__device__ __forceinline__ DScene stage_records(const DScene &S, const WfLaunch &L, float4 *lds) {
-    const float4 *src[kRecArrays] = {
-        reinterpret_cast<const float4 *>(S.shapes), reinterpret_cast<const float4 *>(S.bsdfs),
-        reinterpret_cast<const float4 *>(S.emitters), reinterpret_cast<const float4 *>(S.emitter_cdf),
-        reinterpret_cast<const float4 *>(S.area_cdf), reinterpret_cast<const float4 *>(S.F),
-        reinterpret_cast<const float4 *>(S.V), reinterpret_cast<const float4 *>(S.N),
-        reinterpret_cast<const float4 *>(S.UV), reinterpret_cast<const float4 *>(S.T),
-        reinterpret_cast<const float4 *>(S.BT)};
-#pragma unroll
-    for (int a = 0; a < kRecArrays; ++a)
-        for (int i = threadIdx.x; i < L.rec_n16[a]; i += blockDim.x) lds[L.rec_off[a] + i] = src[a][i];
-    DScene R = S;
-    R.shapes = reinterpret_cast<const DShape *>(lds + L.rec_off[0]);
-    R.bsdfs = reinterpret_cast<const DBsdf *>(lds + L.rec_off[1]);
-    R.emitters = reinterpret_cast<const DEmitter *>(lds + L.rec_off[2]);
-    R.emitter_cdf = reinterpret_cast<const float *>(lds + L.rec_off[3]);
-    R.area_cdf = reinterpret_cast<const float *>(lds + L.rec_off[4]);
-    R.F = reinterpret_cast<const uint32_t *>(lds + L.rec_off[5]);
-    R.V = reinterpret_cast<const float *>(lds + L.rec_off[6]);
-    R.N = reinterpret_cast<const float *>(lds + L.rec_off[7]);
-    R.UV = reinterpret_cast<const float *>(lds + L.rec_off[8]);
-    R.T = reinterpret_cast<const float *>(lds + L.rec_off[9]);
-    R.BT = reinterpret_cast<const float *>(lds + L.rec_off[10]);
-    return R;
+    return small_pairs_offset_f4(L) + kPairF4 * (L.small_prims / 3);
 }
 
 template <bool SMALL>
@@ -1092,11 +1058,13 @@ struct TailClocks {
 };
 
 // body of the current vertex, its light sample's any-hit query, the next ray's closest hit, and the next
-// vertex's head; false once the path has ended (its radiance written)
-template <bool ORDERED, bool STATS, bool CLK = false>
+// vertex's head; false once the path has ended (its radiance written). G > 1: the path is carried by a G-lane
+// group (every lane the same state and arithmetic; leaf primitives tested cooperatively; one lane writes and counts).
+template <bool ORDERED, bool STATS, bool CLK = false, int G = 1>
 __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, const WfLaunch &L, PathV &v, Its &its,
                                         Hit &h, uint32_t *stk, int stride, TravStats &st_e, TravStats &st_s,
                                         unsigned long long &q_e, unsigned long long &q_s, TailClocks *clk = nullptr) {
+    const bool lead = G == 1 || (threadIdx.x & (G - 1)) == 0;
     PState o;
     bool nee = false;
     float4 so, sd;
@@ -1105,13 +1073,13 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     shade_body(S, tv, v, its, o, nee, so, sd);
     if constexpr (CLK) {
         t1 = clock64();
-        clk->c[0] += t1 - t0;
+        if (lead) clk->c[0] += t1 - t0;
         t0 = t1;
     }
     if (nee) {  // the light sample's any-hit query, its outcome applied as the next shade_path would
         Hit hs;
-        ++q_s;
-        if (!trace<16, ORDERED, true, STATS, true>(tv, S, xyz(so), xyz(sd), so.w, sd.w, hs, stk, stride, st_s)) {
+        if (lead) ++q_s;
+        if (!trace<16, ORDERED, true, STATS, true, G>(tv, S, xyz(so), xyz(sd), so.w, sd.w, hs, stk, stride, st_s)) {
             o.li.x = o.li.x + o.pe.x;
             o.li.y = o.li.y + o.pe.y;
             o.li.z = o.li.z + o.pe.z;
@@ -1125,26 +1093,26 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     }
     if constexpr (CLK) {
         t1 = clock64();
-        clk->c[1] += t1 - t0;
+        if (lead) clk->c[1] += t1 - t0;
         t0 = t1;
     }
     const bool live = o.rd.w >= o.ro.w;
-    q_e += live ? 1 : 0;
-    const bool found = live && trace<16, ORDERED, false, STATS, true>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h,
-                                                                    stk, stride, st_e);
+    if (lead) q_e += live ? 1 : 0;
+    const bool found = live && trace<16, ORDERED, false, STATS, true, G>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w,
+                                                                       h, stk, stride, st_e);
     if constexpr (CLK) {
         t1 = clock64();
-        clk->c[2] += t1 - t0;
+        if (lead) clk->c[2] += t1 - t0;
         t0 = t1;
     }
     v = path_of(L, o);
     const bool alive = shade_head(S, tv, v, h, found, o.pdfmat, its);
     if constexpr (CLK) {
-        clk->c[3] += clock64() - t0;
-        clk->bounces++;
+        if (lead) clk->c[3] += clock64() - t0;
+        if (lead) clk->bounces++;
     }
     if (!alive) {
-        write_radiance(L, v);
+        if (lead) write_radiance(L, v);
         return false;
     }
     return true;
@@ -1160,7 +1128,7 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScen
     const int base = blockIdx.x * 256;
     if (base >= qv.n) return;  // whole workgroup
     if (threadIdx.x < kMatClasses) s_n[threadIdx.x] = 0u;  // visible after the staging barrier
-    const DScene S = stage_records(*Sp, L, lds_scene);
+    const DScene &S = *Sp;
     const Traversal tv = stage_small_scene<true>(tv_g, L, lds_scene);
     const int shard = blockIdx.x & (kQueueShards - 1);
     const int q = base + (int)threadIdx.x;
@@ -1214,28 +1182,77 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScen
 // W: waves per SIMD the registers must allow. W = 1 (240-255 VGPRs) holds half a SIMD's register file per tail
 // wave for the tail's whole length, which halves the occupancy of the next chunks' bounce kernels (128 VGPRs)
 // beside it; W = 4 (the bounce kernel's budget) leaves them their 4 waves.
+// Cooperative finish (NH_TAIL_COOP, default 16): once a tail wave carries few enough paths, each remaining path is
+// handed through LDS to a group of lanes that carries it from then on (rr_step<.., G>): the chain of specular
+// bounces that sets the tail's length then tests each leaf's primitives in one parallel step instead of one after
+// the other. Only which lanes run which operation changes; every path's operations and draws are the same.
+constexpr int kTailCoopWords = 48;  // 32-bit words of one handed-over path (PathV, Hit, Its, bounce count)
 template <bool ORDERED, bool STATS, int TB, int W>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf_tail_rr(
-    const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
+    const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L, int coop) {
     __shared__ uint32_t stk[16 * TB];
+    __shared__ uint32_t xfer[TB == 64 ? 4 * kTailCoopWords : 1];
     extern __shared__ float4 lds_scene[];
-    const DScene S = stage_records(*Sp, L, lds_scene);
+    const DScene &S = *Sp;
     const Traversal tv = stage_small_scene<true>(tv_g, L, lds_scene);
     const QView qv = queue_view(L.cnt_in);
     const WfBuf &B = L.st.buf[L.in_q];
     TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
     unsigned long long q_e = 0, q_s = 0;
     TailClocks clk;
-    for (int q = blockIdx.x * TB + threadIdx.x; q < qv.n; q += gridDim.x * TB) {
-        const int s = queue_slot(qv.pre, L.seg_cap, q);
-        PathV v;
-        Hit h;
-        Its its;
-        load_post_head(S, tv, L, B, s, v, h, its);
-        const unsigned long long b0 = clk.bounces;
-        while (rr_step<ORDERED, STATS, STATS>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s, q_e, q_s, &clk)) {
+    // one path per lane (the host sizes the grid to the live count, at most kTailCap)
+    const int q = blockIdx.x * TB + threadIdx.x;
+    bool alive = q < qv.n;
+    PathV v;
+    Hit h;
+    Its its;
+    unsigned long long nb = 0;  // bounces of this lane's path
+    if (alive) load_post_head(S, tv, L, B, queue_slot(qv.pre, L.seg_cap, q), v, h, its);
+    const bool can_coop = TB == 64 && coop == 16;
+    for (;;) {
+        const unsigned long long m = __ballot(alive);
+        if (m == 0ull || (can_coop && __popcll(m) <= 4)) break;
+        if (alive) {
+            alive = rr_step<ORDERED, STATS, STATS>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s, q_e, q_s,
+                                                   &clk);
+            ++nb;
         }
-        if (STATS) clk.max_bounces = max(clk.max_bounces, clk.bounces - b0);
+    }
+    if (STATS && !can_coop) clk.max_bounces = max(clk.max_bounces, nb);
+    if constexpr (TB == 64) {
+        const unsigned long long m = __ballot(alive);
+        if (can_coop && m) {
+            // hand the (at most 4) remaining paths to 16-lane groups: path of rank r -> lanes 16r .. 16r+15
+            const int lane = threadIdx.x & 63;
+            if (alive) {
+                uint32_t *w = xfer + __popcll(m & ((1ull << lane) - 1ull)) * kTailCoopWords;
+                static_assert(sizeof(PathV) + sizeof(Hit) + sizeof(Its) + 8 <= kTailCoopWords * 4, "xfer slot");
+                __builtin_memcpy(w, &v, sizeof(PathV));
+                __builtin_memcpy(w + sizeof(PathV) / 4, &h, sizeof(Hit));
+                __builtin_memcpy(w + (sizeof(PathV) + sizeof(Hit)) / 4, &its, sizeof(Its));
+                __builtin_memcpy(w + (sizeof(PathV) + sizeof(Hit) + sizeof(Its)) / 4, &nb, 8);
+            }
+            __syncthreads();  // TB == 64: the workgroup is this one wave
+            const int g = lane >> 4;
+            bool carry = g < __popcll(m);
+            if (carry) {
+                const uint32_t *w = xfer + g * kTailCoopWords;
+                __builtin_memcpy(&v, w, sizeof(PathV));
+                __builtin_memcpy(&h, w + sizeof(PathV) / 4, sizeof(Hit));
+                __builtin_memcpy(&its, w + (sizeof(PathV) + sizeof(Hit)) / 4, sizeof(Its));
+                __builtin_memcpy(&nb, w + (sizeof(PathV) + sizeof(Hit) + sizeof(Its)) / 4, 8);
+            }
+            while (__ballot(carry)) {
+                if (carry) {
+                    carry = rr_step<ORDERED, STATS, STATS, 16>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s, q_e,
+                                                              q_s, &clk);
+                    ++nb;
+                }
+            }
+            if (STATS && (lane & 15) == 0 && g < __popcll(m)) clk.max_bounces = max(clk.max_bounces, nb);
+        } else if (STATS && can_coop) {
+            clk.max_bounces = max(clk.max_bounces, nb);
+        }
     }
     if (STATS) {  // the tail's own counter slots (kStatTail*), so stage rates stay per kernel
         flush_trav_stats(stat_shard(L.counters) + kStatTail, q_e, st_e);
@@ -1246,9 +1263,9 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
             if ((threadIdx.x & 63) == 0) atomicAdd(&dst[j], x);
         }
-        unsigned long long m = clk.max_bounces;
-        for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, off, 64));
-        if ((threadIdx.x & 63) == 0) atomicMax(&dst[5], m);
+        unsigned long long mx = clk.max_bounces;
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned long long)__shfl_xor(mx, off, 64));
+        if ((threadIdx.x & 63) == 0) atomicMax(&dst[5], mx);
     }
 }
 
@@ -1320,7 +1337,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAV
 namespace nh {
 
 int tree_top_nodes() { return kTopNodes; }
-int rr_records_base_f4(const WfLaunch &L) { return small_pairs_offset_f4(L) + kPairF4 * (L.small_prims / 3); }
 
 // Persistent grids hold exactly the workgroups that are resident at once (occupancy of this
 // instantiation x CUs, at most kPersistentBlocks -- the spill area's size): a workgroup that
@@ -1459,13 +1475,16 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
     const int tb = e && std::atoi(e) == 256 ? 256 : 64;
     const char *w = std::getenv("NH_TAIL_RR_WAVES");  // register budget: 4 waves/SIMD (default) or 1
     const bool w1 = w && std::atoi(w) == 1;
-    const dim3 grid(std::min(std::max(1, (bound + tb - 1) / tb), kTraceBlocksMax));
+    const char *cp = std::getenv("NH_TAIL_COOP");  // lanes per path once <= 4 remain in a wave: 16 (default) or 1
+    const int coop = cp && std::atoi(cp) == 1 ? 1 : 16;
+    // one path per lane: the grid covers the bound (tail bounds are <= kTailCap paths)
+    const dim3 grid(std::max(1, (bound + tb - 1) / tb));
     const size_t lds = 16 * (size_t)rr_lds_f4(L);
 #define NH_TR(O, T)                                                                                         \
     do {                                                                                                    \
-        if (tb == 256) hipLaunchKernelGGL((wf_tail_rr<O, T, 256, 1>), grid, dim3(256), lds, st, S, tv, L);      \
-        else if (w1) hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 1>), grid, dim3(64), lds, st, S, tv, L);         \
-        else hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 4>), grid, dim3(64), lds, st, S, tv, L);                 \
+        if (tb == 256) hipLaunchKernelGGL((wf_tail_rr<O, T, 256, 1>), grid, dim3(256), lds, st, S, tv, L, coop); \
+        else if (w1) hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 1>), grid, dim3(64), lds, st, S, tv, L, coop);   \
+        else hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 4>), grid, dim3(64), lds, st, S, tv, L, coop);           \
     } while (0)
     if (ordered) { if (stats) NH_TR(true, true); else NH_TR(true, false); }
     else { if (stats) NH_TR(false, true); else NH_TR(false, false); }

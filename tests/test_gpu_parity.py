@@ -327,6 +327,34 @@ def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
             assert ref.stats()[k] == ctx.stats()[k], (xml, k)
 
 
+@pytest.mark.parametrize("tail,coop,waves", [("4096", "16", "4"), ("4096", "1", "4"), ("200000", "16", "1"),
+                                             ("64", "16", "4")])
+def test_cooperative_tail_matches_oracle(gpu, tmp_path, monkeypatch, tail, coop, waves):
+    """The RR-ahead tail kernel's cooperative finish (NH_TAIL_COOP=16: once a tail wave carries <= 4 paths, each is
+    carried by a 16-lane group that tests a leaf's primitives in one parallel step and reduces to the smallest t,
+    ties to the later primitive) on the mirror + dielectric Cornell box (long specular chains), forced early by a
+    small tail threshold, and the per-lane tail (NH_TAIL_COOP=1), at both register budgets: framebuffer and traversal
+    counters equal the megakernel's, the framebuffer equals the oracle's."""
+    xml = scenegen.cbox_xml(str(tmp_path), "c1")
+    s = nh.Scene(xml)
+    s.set_resolution(64, 48)
+    b = nh.Bvh(s)
+    ref = nh.Context(0)
+    ref.upload(s, b)
+    ref.render(0, 8, seed=17, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_MEGAKERNEL, stats=True)
+    for name, val in (("NH_TAIL", tail), ("NH_TAIL_COOP", coop), ("NH_TAIL_RR_WAVES", waves)):
+        monkeypatch.setenv(name, val)
+    ctx = nh.Context(0)
+    ctx.upload(s, b)
+    ctx.render(0, 8, seed=17, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT, stats=True)
+    st = ctx.stats()
+    assert st["fused_bounce"] == 1 and st["launches_tail"] >= 1 and st["tail_bounces"] > 0
+    np.testing.assert_array_equal(ref.framebuffer(), ctx.framebuffer())
+    for k in ("ray_queries", "nodes_visited", "prims_tested", "shadow_queries", "shadow_prims_tested"):
+        assert ref.stats()[k] == st[k], k
+    np.testing.assert_array_equal(ctx.framebuffer(), no.OracleScene(s).render(0, 8, seed=17))
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_render_parity_c5_small(gpu, tmp_path, mode):
     """C5-shaped scene at test size: flattened transformed bumpy meshes (microfacet + diffuse),
