@@ -728,9 +728,12 @@ def launcher_selftest(args):
 
 def main():
     args = parse()
-    # one hardware queue per path-pool stream (nori_hip.py sets the same default; done here too, before torch may
-    # initialise the HIP runtime in a multi-rank run). An explicit setting is respected; the line records it.
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # one hardware queue per path-pool stream: the benchmark's own configuration (the GPU box exports HIP's default
+    # of 4, with which two pool streams share a queue and one pool's tail blocks another's bounces: C1 -15 %,
+    # profiles/round4_hw_queues_ab.txt). Raised before torch may initialise the HIP runtime in a multi-rank run;
+    # the line records the value. (Importing nori_hip only sets it when unset.)
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -287,6 +287,57 @@ void nh_destroy(nh_ctx *c) {
     delete c;
 }
 
+// Can a light sample ever be non-finite, or land on a discrete-BSDF (mirror / dielectric) shading point? No, when:
+// every emitter is an area light or the envmap, with finite radiance (and a finite constant env colour); every
+// shape's box is finite and well inside float range (no overflow in the sample's squared distance); and the box of
+// every area light's shape, widened by a relative margin for rounding, is disjoint from the widened box of every
+// shape with a discrete BSDF (so the sampled point p and the shading point ref always differ: a zero distance is the
+// only way the area light's pdf becomes 0/0, emitter_pdf). Then the wavefront shade may skip the light sample of a
+// discrete BSDF sample, which is zeroed by the reference anyway (path_mis.cpp:136-140).
+static bool nee_finite(const nh_scene_desc *d) {
+    auto fin = [](float x) { return std::fabs(x) < 1e15f; };
+    for (uint32_t i = 0; i < d->n_emitters; ++i) {
+        const nh_emitter &e = d->emitters[i];
+        if (e.type == NH_EMITTER_POINT) return false;
+        for (int k = 0; k < 3; ++k)
+            if (!std::isfinite(e.radiance[k])) return false;
+    }
+    if (d->envmap >= 0 && d->env.constant && d->env.rgba)
+        for (int k = 0; k < 3; ++k)
+            if (!std::isfinite(d->env.rgba[k])) return false;
+    struct Box { float lo[3], hi[3]; };
+    auto widened = [&](const nh_shape &s, Box &b) {
+        float ext = 0.f;
+        for (int k = 0; k < 3; ++k) {
+            if (!fin(s.bbox_min[k]) || !fin(s.bbox_max[k])) return false;
+            ext = std::max(ext, std::max(std::fabs(s.bbox_min[k]), std::fabs(s.bbox_max[k])));
+        }
+        const float m = 1e-3f * ext + 1e-6f;
+        for (int k = 0; k < 3; ++k) {
+            b.lo[k] = s.bbox_min[k] - m;
+            b.hi[k] = s.bbox_max[k] + m;
+        }
+        return true;
+    };
+    for (uint32_t i = 0; i < d->n_shapes; ++i) {
+        const nh_shape &si = d->shapes[i];
+        Box bi;
+        if (!widened(si, bi)) return false;
+        if (si.emitter < 0) continue;
+        for (uint32_t j = 0; j < d->n_shapes; ++j) {
+            const nh_shape &sj = d->shapes[j];
+            const int t = d->bsdfs[sj.bsdf].type;
+            if (t != NH_BSDF_MIRROR && t != NH_BSDF_DIELECTRIC) continue;
+            Box bj;
+            if (!widened(sj, bj)) return false;
+            bool apart = false;
+            for (int k = 0; k < 3; ++k) apart = apart || bi.hi[k] < bj.lo[k] || bj.hi[k] < bi.lo[k];
+            if (!apart) return false;
+        }
+    }
+    return true;
+}
+
 int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     if (!c || !d) return NH_ERR_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
@@ -414,11 +465,7 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         S.env_b = e.radiance[2];
     }
     S.n_emitters = (int)d->n_emitters;
-    S.n_shapes = (int)d->n_shapes;
-    S.n_bsdfs = (int)d->n_bsdfs;
-    S.n_faces = (int)d->n_faces;
-    S.n_vertices = (int)d->n_vertices;
-    S.n_area_cdf = (int)d->n_area_cdf;
+    S.nee_finite = nee_finite(d) ? 1 : 0;
     if (d->integrator < NH_INTEGRATOR_PATH_MIS || d->integrator > NH_INTEGRATOR_DIRECT)
         return fail(c, "unknown integrator"), NH_ERR_INVALID;
     S.integrator = d->integrator;

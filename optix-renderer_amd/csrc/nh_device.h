@@ -195,8 +195,9 @@ struct DScene {
     // BSDF albedo textures (DBsdf::tex) and the png texels they index
     const DTex *texs;
     const float4 *texels;
-    // element counts of the record arrays above (LDS staging of small scenes, nh_wavefront.hip stage_records)
-    int n_shapes, n_bsdfs, n_faces, n_vertices, n_area_cdf;
+    // 1: a light sample is always finite and never at a discrete-BSDF shading point (nh_api.hip, upload), so the
+    // wavefront shade skips the light sample of a discrete BSDF sample (it provably adds +-0)
+    int nee_finite;
 };
 
 NHD F3 ldv(const float *a, uint32_t i) { return f3(a[3 * i], a[3 * i + 1], a[3 * i + 2]); }

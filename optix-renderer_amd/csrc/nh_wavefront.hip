@@ -631,34 +631,44 @@ __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv,
         o.flags = v.flags & 0x30;
     } else {
         const float n_lights = (float)S.n_emitters;
-        const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, v.rng.next1d());
-        const DEmitter em = S.emitters[ei];
-        const float ex = v.rng.next1d(), ey = v.rng.next1d();
-        ESample es;
-        const F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
-        const F3 wi_l = to_local(its.sh, neg(v.d));
-        nee = !is_zero(ems_col);
-        F3 li_ems = f3(0, 0, 0);
-        float pdfems = 0.f, pdfems_mats = 0.f;
-        if (nee) {
-            const F3 we = to_local(its.sh, es.wi);
-            const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE, alb);
-            const float cs = we.z;
-            li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights, ems_col.z * cs * f.z * n_lights);
-            pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
-            pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
-            so = make_float4(es.so.x, es.so.y, es.so.z, es.smint);
-            sd = make_float4(es.sd.x, es.sd.y, es.sd.z, es.smaxt);
-        }
+        // the draws in the reference's order: emitter pick, light sample, BSDF sample
+        const float e0 = v.rng.next1d(), ex = v.rng.next1d(), ey = v.rng.next1d();
         const float bx = v.rng.next1d(), by = v.rng.next1d();
+        const F3 wi_l = to_local(its.sh, neg(v.d));
         F3 wo;
         int measure;
         const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure, alb);
         const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
+        const bool discrete = measure == M_DISCRETE;
+        // The light sample (path_mis.cpp:80-106). After a discrete BSDF sample its weight is zeroed (:136-140) and
+        // f = 0 (discrete BSDFs evaluate to 0), so it adds (0 * t) * (Le/pdf * cos * 0 * n) = +-0 and leaves every
+        // other state as it was -- unless a factor is non-finite. S.nee_finite (upload: area / envmap lights only,
+        // finite radiance, every light's box apart from every discrete-BSDF shape's, so the sampled point is never
+        // the shading point) rules out a non-finite light sample, and t is checked here: then it is not computed.
+        const bool skip_nee = discrete && S.nee_finite && isfinite(v.t.x) && isfinite(v.t.y) && isfinite(v.t.z);
+        F3 li_ems = f3(0, 0, 0);
+        float pdfems = 0.f, pdfems_mats = 0.f;
+        if (!skip_nee) {
+            const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, e0);
+            const DEmitter em = S.emitters[ei];
+            ESample es;
+            const F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
+            nee = !is_zero(ems_col);
+            if (nee) {
+                const F3 we = to_local(its.sh, es.wi);
+                const F3 f = bsdf_eval(bsdf, wi_l, we, M_SOLID_ANGLE, alb);
+                const float cs = we.z;
+                li_ems = f3(ems_col.x * cs * f.x * n_lights, ems_col.y * cs * f.y * n_lights,
+                            ems_col.z * cs * f.z * n_lights);
+                pdfems_mats = bsdf_pdf(bsdf, wi_l, we, M_SOLID_ANGLE);
+                pdfems = emitter_pdf(S, em, its.p, es.p, es.n, es.wi) / n_lights;
+                so = make_float4(es.so.x, es.so.y, es.so.z, es.smint);
+                sd = make_float4(es.sd.x, es.sd.y, es.sd.z, es.smaxt);
+            }
+        }
         const F3 nd = to_world(its.sh, wo);
         // w_ems of this bounce (:103-106): the occluded shadow ray leaves both pdfs 0 (w_ems keeps its
         // value), the unoccluded one sets it from them; a discrete sample zeroes it either way (:136-140)
-        const bool discrete = measure == M_DISCRETE;
         float w_occ = v.w_ems, w_un = v.w_ems;
         if (nee && (pdfems_mats + pdfems) > kEps) w_un = pdfems / (pdfems_mats + pdfems);
         if (discrete) w_occ = w_un = 0.f;
