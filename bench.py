@@ -296,6 +296,12 @@ def roofline(args, calib, st, W, H, R):
             "cycles_per_bounce": {k: round(calib[f"tail_cycles_{k}"] / nb, 1)
                                   for k in ("body", "shadow", "closest", "head")},
             "source": "wf_tail_rr calibration launch (collect_stats), clock64 per phase"}
+        nc = calib.get("tail_coop_bounces", 0)
+        if nc:
+            # bounces the cooperative finish ran (one path per 16-lane group): one bounce's latency on the last chains
+            roof["tail_profile"]["coop_bounces"] = nc
+            roof["tail_profile"]["coop_cycles_per_bounce"] = {
+                k: round(calib[f"tail_coop_cycles_{k}"] / nc, 1) for k in ("body", "shadow", "closest", "head")}
     return roof
 
 

@@ -316,6 +316,10 @@ typedef struct nh_render_stats {
        path-bounces it ran and its longest chain (bounces of one path) */
     uint64_t tail_cycles_body, tail_cycles_shadow, tail_cycles_closest, tail_cycles_head;
     uint64_t tail_bounces, tail_max_bounces;
+    /* the same four phase sums and the path-bounce count for the bounces the tail's cooperative finish ran (a path
+       carried by a 16-lane group once <= 4 remain in its wave): the latency of one bounce of the last chains */
+    uint64_t tail_coop_cycles_body, tail_coop_cycles_shadow, tail_coop_cycles_closest, tail_coop_cycles_head;
+    uint64_t tail_coop_bounces;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;

@@ -517,6 +517,71 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     return NH_OK;
 }
 
+// Isolated spheres (nhd::kPrimIsolated, nh_traverse.h trace_next): a sphere record whose box grown by 2m lies apart
+// from every other primitive's box gets the bit, and m in its record 1 .x (only read by the sphere shortcut). m is
+// 1e-4 of the scene's largest extent -- far above the float rounding of any hit point, far below the gaps of
+// real scenes (the Cornell box's spheres clear its floor by 6e-3). Boxes are compared in double, closed: a box
+// that touches or holds a NaN is not apart. NH_ISO_SPHERE=0 leaves every sphere unmarked (every ray walks the
+// tree). Spheres x primitives box tests, skipped (no marks) past 2e8.
+static void mark_isolated_spheres(std::vector<float4> &prims) {
+    const char *e = std::getenv("NH_ISO_SPHERE");
+    if (e && e[0] == '0') return;
+    const size_t n = prims.size() / 3;
+    std::vector<size_t> sph;
+    for (size_t k = 0; k < n; ++k) {
+        int bits;
+        std::memcpy(&bits, &prims[3 * k + 2].w, 4);
+        if (bits & nhd::kPrimSphere) sph.push_back(k);
+    }
+    if (sph.empty() || (double)sph.size() * (double)n > 2e8) return;
+    std::vector<double> lo(3 * n), hi(3 * n);
+    double slo[3] = {INFINITY, INFINITY, INFINITY}, shi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t k = 0; k < n; ++k) {
+        const float4 *p = &prims[3 * k];
+        int bits;
+        std::memcpy(&bits, &p[2].w, 4);
+        for (int a = 0; a < 3; ++a) {
+            const double v0 = a == 0 ? p[0].x : a == 1 ? p[0].y : p[0].z;
+            if (bits & nhd::kPrimSphere) {
+                lo[3 * k + a] = v0 - (double)p[0].w;
+                hi[3 * k + a] = v0 + (double)p[0].w;
+            } else {
+                const double v1 = a == 0 ? p[1].x : a == 1 ? p[1].y : p[1].z;
+                const double v2 = a == 0 ? p[2].x : a == 1 ? p[2].y : p[2].z;
+                lo[3 * k + a] = std::min(v0, std::min(v1, v2));
+                hi[3 * k + a] = std::max(v0, std::max(v1, v2));
+            }
+            slo[a] = std::min(slo[a], lo[3 * k + a]);
+            shi[a] = std::max(shi[a], hi[3 * k + a]);
+        }
+    }
+    const double ext = std::max(shi[0] - slo[0], std::max(shi[1] - slo[1], shi[2] - slo[2]));
+    if (!(ext > 0.0) || !std::isfinite(ext)) return;
+    const float m = (float)(1e-4 * ext);
+    for (size_t s : sph) {
+        const float4 a = prims[3 * s];
+        if (!(a.w > 0.f) || !std::isfinite(a.w) || !std::isfinite(a.x) || !std::isfinite(a.y) || !std::isfinite(a.z))
+            continue;
+        const double g = (double)a.w + 2.0 * (double)m;
+        const double glo[3] = {(double)a.x - g, (double)a.y - g, (double)a.z - g};
+        const double ghi[3] = {(double)a.x + g, (double)a.y + g, (double)a.z + g};
+        bool apart = true;
+        for (size_t k = 0; k < n && apart; ++k) {
+            if (k == s) continue;
+            bool sep = false;
+            for (int ax = 0; ax < 3; ++ax)
+                sep = sep || hi[3 * k + ax] < glo[ax] || lo[3 * k + ax] > ghi[ax];
+            apart = sep;
+        }
+        if (!apart) continue;
+        int bits;
+        std::memcpy(&bits, &prims[3 * s + 2].w, 4);
+        bits |= nhd::kPrimIsolated;
+        std::memcpy(&prims[3 * s + 2].w, &bits, 4);
+        prims[3 * s + 1].x = m;
+    }
+}
+
 // 4-wide collapse of the GPU binary tree (nh_traverse.h Tracer4): every wide node takes the two
 // children of a binary node and, while it has fewer than 4, replaces its largest-area inner child
 // by that child's two children in place (left-first DFS order of the slots is kept). Wide nodes
@@ -732,6 +797,7 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
             p[2] = make_float4(p2[0], p2[1], p2[2], f0);
         }
     }
+    mark_isolated_spheres(prims);
     // leaf-end bits: the 4-wide traversal walks a leaf's records until this bit
     for (const int2 &lf : leaves)
         if (lf.y > 0) {
@@ -1686,6 +1752,11 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         c->stats.tail_cycles_head += h[kStatTailClk + 3];
         c->stats.tail_bounces += h[kStatTailClk + 4];
         c->stats.tail_max_bounces = std::max<uint64_t>(c->stats.tail_max_bounces, h[kStatTailClk + 5]);
+        c->stats.tail_coop_cycles_body += h[kStatTailCoopClk];
+        c->stats.tail_coop_cycles_shadow += h[kStatTailCoopClk + 1];
+        c->stats.tail_coop_cycles_closest += h[kStatTailCoopClk + 2];
+        c->stats.tail_coop_cycles_head += h[kStatTailCoopClk + 3];
+        c->stats.tail_coop_bounces += h[kStatTailCoopClk + 4];
         const unsigned long long *cl = h, *an = h + kStatAny, *tc = h + kStatTail, *ta = h + kStatTailAny;
         c->stats.ray_queries += cl[0] + an[0] + tc[0] + ta[0];
         c->stats.nodes_visited += cl[1] + an[1] + tc[1] + ta[1];

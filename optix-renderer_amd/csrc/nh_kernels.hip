@@ -20,12 +20,6 @@ using namespace nhd;
 
 namespace {
 
-template <int DEPTH, bool ORDERED, bool STATS>
-__device__ __forceinline__ bool closest(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, float maxt,
-                                        Hit &h, uint32_t *stk, int stride, TravStats &st) {
-    return trace<DEPTH, ORDERED, false, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st);
-}
-
 // PathMISIntegrator::Li (src/integrators/path_mis.cpp:16-150). Lanes of a wave stay in
 // lockstep: shade, then one shadow traversal (any hit, :89) for the lanes that sample a
 // light, then one closest-hit traversal of the BSDF-sampled ray for every lane -- that ray
@@ -116,7 +110,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
             found = false;
         } else {
             if (STATS) queries++;
-            found = trace<DEPTH, ORDERED, false, STATS>(tv, S, no, nd, kEps, INFINITY, h, stk, stride, st);
+            found = trace_next<DEPTH, ORDERED, STATS>(tv, S, h.k, no, nd, kEps, INFINITY, h, stk, stride, st);
         }
         if (!is_zero(bsdf_col) && found) {
             const int hs_shape = __float_as_int(tv.prims[3 * h.k + 1].w);
@@ -149,13 +143,14 @@ __device__ F3 li_path_mats(const DScene &S, const Traversal &tv, Rng &rng, F3 o,
     F3 li = f3(0, 0, 0), t = f3(1, 1, 1);
     int counter = 0;
     Hit h;
+    h.k = -1;  // the camera ray leaves no surface
     for (;;) {
         bool found;
         if (d.x == 0 && d.y == 0 && d.z == 0) {
             found = false;
         } else {
             if (STATS) queries++;
-            found = closest<DEPTH, ORDERED, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st);
+            found = trace_next<DEPTH, ORDERED, STATS>(tv, S, h.k, o, d, mint, maxt, h, stk, stride, st);
         }
         if (!found) {  // path_mats.cpp:26-35
             if (S.envmap >= 0) li = add(li, mulc(t, env_eval(S, d)));

@@ -229,6 +229,8 @@ constexpr int kPairF4 = 6;
 // primitive record type / leaf-end bits (word 2 .w of the record), and the BSDF type of the owning
 // shape in bits 2-3 (the material key of the sorted shade queues)
 constexpr int kPrimSphere = 1, kPrimLeafEnd = 2, kPrimMatShift = 2;
+// an isolated sphere (record 2 .w bit; record 1 .x holds the host's margin m): see trace_next
+constexpr int kPrimIsolated = 16;
 NHD bool prim_is_tri(float4 c) { return (__float_as_int(c.w) & kPrimSphere) == 0; }
 NHD int prim_material(float4 c) { return (__float_as_int(c.w) >> kPrimMatShift) & 3; }
 
@@ -460,6 +462,45 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
     }
     (void)DEPTH;
     return ANY ? false : found;
+}
+
+// The closest hit of a path's next ray, which leaves the surface of primitive k_prev (-1: none). When k_prev is an
+// isolated sphere -- the host found its box, grown by 2m, apart from every other primitive's box -- and the ray
+// starts within m of that box and meets the sphere at t >= 2 mint, the traversal's answer is that sphere at that t,
+// so the tree is not walked. Why: every primitive a traversal accepts at t lies (up to rounding far below m) at
+// o + t d inside its own box; on [mint, t] the ray stays inside the sphere's box grown by m (both ends are in that
+// convex box), which no other primitive's box reaches, so no other primitive is accepted at or before t and the
+// answer -- the smallest accepted t, ties to the later record -- is the sphere's, found with the maxt any order of
+// visits tests it with (>= t). No box on the way culls it: each holds the sphere's box, the ray's exit from it is
+// past t (up to rounding) >= 2 mint, and the entry before the exit. The sphere test is sphere_test, with the
+// traversal's adaptive mint. Counted as one primitive test (no node or box).
+template <bool STATS, int G = 1>
+NHD bool iso_sphere_hit(const Traversal &tv, int k_prev, F3 o, F3 d, float mint, float maxt, Hit &best,
+                        TravStats &st) {
+    if (k_prev < 0) return false;
+    const float4 c = tv.prims[3 * k_prev + 2];
+    if (!(__float_as_int(c.w) & kPrimIsolated)) return false;
+    if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));  // as trace
+    if (maxt < mint) return false;
+    const float4 a = tv.prims[3 * k_prev];
+    const float lim = a.w + tv.prims[3 * k_prev + 1].x;
+    if (!(fabsf(o.x - a.x) <= lim && fabsf(o.y - a.y) <= lim && fabsf(o.z - a.z) <= lim)) return false;
+    float t;
+    if (!sphere_test(a, o, d, mint, maxt, t) || !(t >= 2.f * mint)) return false;
+    best.t = t;
+    best.u = 0.f;
+    best.v = 0.f;
+    best.k = k_prev;
+    if (STATS && (G == 1 || (threadIdx.x & (G - 1)) == 0)) st.prims++;
+    return true;
+}
+
+// trace (closest hit) of a path's next ray from the surface of primitive k_prev, with the isolated-sphere answer
+template <int DEPTH, bool ORDERED, bool STATS, bool PAIRS = false, int G = 1>
+NHD bool trace_next(const Traversal &tv, const DScene &S, int k_prev, F3 o, F3 d, float mint, float maxt, Hit &best,
+                    uint32_t *stk, int stride, TravStats &st) {
+    if (S.root_kind != 0 && iso_sphere_hit<STATS, G>(tv, k_prev, o, d, mint, maxt, best, st)) return true;
+    return trace<DEPTH, ORDERED, false, STATS, PAIRS, G>(tv, S, o, d, mint, maxt, best, stk, stride, st);
 }
 
 

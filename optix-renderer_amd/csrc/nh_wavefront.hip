@@ -633,13 +633,10 @@ __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv,
         const float n_lights = (float)S.n_emitters;
         // the draws in the reference's order: emitter pick, light sample, BSDF sample
         const float e0 = v.rng.next1d(), ex = v.rng.next1d(), ey = v.rng.next1d();
-        const float bx = v.rng.next1d(), by = v.rng.next1d();
         const F3 wi_l = to_local(its.sh, neg(v.d));
-        F3 wo;
-        int measure;
-        const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure, alb);
-        const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
-        const bool discrete = measure == M_DISCRETE;
+        // whether the BSDF sample will be discrete, known before it is drawn (bsdf_sample: a dielectric always, a
+        // mirror unless wi.z <= 0), so the light sample below runs in the reference's order
+        const bool discrete = bsdf.type == BSDF_DIELECTRIC || (bsdf.type == BSDF_MIRROR && !(wi_l.z <= 0));
         // The light sample (path_mis.cpp:80-106). After a discrete BSDF sample its weight is zeroed (:136-140) and
         // f = 0 (discrete BSDFs evaluate to 0), so it adds (0 * t) * (Le/pdf * cos * 0 * n) = +-0 and leaves every
         // other state as it was -- unless a factor is non-finite. S.nee_finite (upload: area / envmap lights only,
@@ -666,6 +663,11 @@ __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv,
                 sd = make_float4(es.sd.x, es.sd.y, es.sd.z, es.smaxt);
             }
         }
+        const float bx = v.rng.next1d(), by = v.rng.next1d();
+        F3 wo;
+        int measure;
+        const F3 bsdf_col = bsdf_sample(bsdf, wi_l, bx, by, wo, measure, alb);
+        const float pdfmat = bsdf_pdf(bsdf, wi_l, wo, measure);
         const F3 nd = to_world(its.sh, wo);
         // w_ems of this bounce (:103-106): the occluded shadow ray leaves both pdfs 0 (w_ems keeps its
         // value), the unoccluded one sets it from them; a discrete sample zeroes it either way (:136-140)
@@ -949,8 +951,8 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce(const DScene *
                     o.rng ^= (uint64_t)(h2.k == -7);
             }
 #endif
-            const bool found = live && trace<16, ORDERED, false, STATS, true>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h,
-                                                                        my_stk, 256, st_e);
+            const bool found = live && trace_next<16, ORDERED, STATS, true>(tv, S, __float_as_int(hv.w), xyz(o.ro),
+                                                                      xyz(o.rd), o.ro.w, o.rd.w, h, my_stk, 256, st_e);
             hit_out = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
             if (found) cls = prim_material(tv.prims[3 * h.k + 2]);
         }
@@ -1065,6 +1067,7 @@ __device__ __forceinline__ bool first_vertex(const DScene &S, const Traversal &t
 struct TailClocks {
     unsigned long long c[4] = {0, 0, 0, 0};
     unsigned long long bounces = 0, max_bounces = 0;
+    unsigned long long cc[4] = {0, 0, 0, 0}, coop_bounces = 0;  // the same, for bounces carried by lane groups
 };
 
 // body of the current vertex, its light sample's any-hit query, the next ray's closest hit, and the next
@@ -1079,11 +1082,12 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     bool nee = false;
     float4 so, sd;
     unsigned long long t0 = 0, t1 = 0;
+    unsigned long long *cs = CLK ? (G > 1 ? clk->cc : clk->c) : nullptr;
     if constexpr (CLK) t0 = clock64();
     shade_body(S, tv, v, its, o, nee, so, sd);
     if constexpr (CLK) {
         t1 = clock64();
-        if (lead) clk->c[0] += t1 - t0;
+        if (lead) cs[0] += t1 - t0;
         t0 = t1;
     }
     if (nee) {  // the light sample's any-hit query, its outcome applied as the next shade_path would
@@ -1103,23 +1107,23 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     }
     if constexpr (CLK) {
         t1 = clock64();
-        if (lead) clk->c[1] += t1 - t0;
+        if (lead) cs[1] += t1 - t0;
         t0 = t1;
     }
     const bool live = o.rd.w >= o.ro.w;
     if (lead) q_e += live ? 1 : 0;
-    const bool found = live && trace<16, ORDERED, false, STATS, true, G>(tv, S, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w,
-                                                                       h, stk, stride, st_e);
+    const bool found = live && trace_next<16, ORDERED, STATS, true, G>(tv, S, h.k, xyz(o.ro), xyz(o.rd), o.ro.w,
+                                                                      o.rd.w, h, stk, stride, st_e);
     if constexpr (CLK) {
         t1 = clock64();
-        if (lead) clk->c[2] += t1 - t0;
+        if (lead) cs[2] += t1 - t0;
         t0 = t1;
     }
     v = path_of(L, o);
     const bool alive = shade_head(S, tv, v, h, found, o.pdfmat, its);
     if constexpr (CLK) {
-        if (lead) clk->c[3] += clock64() - t0;
-        if (lead) clk->bounces++;
+        if (lead) cs[3] += clock64() - t0;
+        if (lead) ++(G > 1 ? clk->coop_bounces : clk->bounces);
     }
     if (!alive) {
         if (lead) write_radiance(L, v);
@@ -1270,8 +1274,15 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
         unsigned long long *dst = stat_shard(L.counters) + kStatTailClk;
         for (int j = 0; j < 5; ++j) {
             unsigned long long x = j < 4 ? clk.c[j] : clk.bounces;
-            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-            if ((threadIdx.x & 63) == 0) atomicAdd(&dst[j], x);
+            unsigned long long y = j < 4 ? clk.cc[j] : clk.coop_bounces;
+            for (int off = 32; off > 0; off >>= 1) {
+                x += __shfl_xor(x, off, 64);
+                y += __shfl_xor(y, off, 64);
+            }
+            if ((threadIdx.x & 63) == 0) {
+                atomicAdd(&dst[j], x);
+                atomicAdd(&dst[kStatTailCoopClk - kStatTailClk + j], y);
+            }
         }
         unsigned long long mx = clk.max_bounces;
         for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned long long)__shfl_xor(mx, off, 64));
@@ -1319,13 +1330,18 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAV
         PState o;
         bool nee = false, occ = false;
         float4 so, sd;
-        if (!shade_path(S, tv, L, MemState{B, s}, s, B.hit[s], o, nee, so, sd)) continue;
+        const float4 hv0 = B.hit[s];
+        if (!shade_path(S, tv, L, MemState{B, s}, s, hv0, o, nee, so, sd)) continue;
+        int kp = __float_as_int(hv0.w);  // the primitive the next ray leaves (trace_next)
         for (;;) {
             Hit h;
             const bool live = o.rd.w >= o.ro.w;
             q_e += live ? 1 : 0;
-            const bool found = live && trace_lane<WIDE, DEPTH, ORDERED, false, STATS>(tv, S, L, xyz(o.ro), xyz(o.rd),
-                                                                                      o.ro.w, o.rd.w, h, stk, st_e);
+            const bool found =
+                live && ((S.root_kind != 0 && iso_sphere_hit<STATS>(tv, kp, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h, st_e)) ||
+                         trace_lane<WIDE, DEPTH, ORDERED, false, STATS>(tv, S, L, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h,
+                                                                        stk, st_e));
+            kp = found ? h.k : -1;
             const float4 hv = make_float4(h.t, h.u, h.v, __int_as_float(found ? h.k : -1));
             occ = false;
             if (nee) {
@@ -1483,8 +1499,9 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
                        hipStream_t st) {
     const char *e = std::getenv("NH_TAIL_WG");  // threads per tail workgroup: 64 (default) or 256
     const int tb = e && std::atoi(e) == 256 ? 256 : 64;
-    const char *w = std::getenv("NH_TAIL_RR_WAVES");  // register budget: 4 waves/SIMD (default) or 1
-    const bool w1 = w && std::atoi(w) == 1;
+    // register budget: 1 wave/SIMD (default; profiles/round4_session4_ab.txt: shorter tails on C1 and C4) or 4
+    const char *w = std::getenv("NH_TAIL_RR_WAVES");
+    const bool w1 = !(w && std::atoi(w) == 4);
     const char *cp = std::getenv("NH_TAIL_COOP");  // lanes per path once <= 4 remain in a wave: 16 (default) or 1
     const int coop = cp && std::atoi(cp) == 1 ? 1 : 16;
     // one path per lane: the grid covers the bound (tail bounds are <= kTailCap paths)

@@ -164,7 +164,9 @@ class nh_render_stats(C.Structure):
         ("kernel_ms_denoise", C.c_double), ("launches_denoise", C.c_uint64), ("tails_async", C.c_uint64),
         ("pools_active", C.c_uint64), ("trace_fused", C.c_uint64)] + [
         (n, C.c_uint64) for n in ("tail_cycles_body", "tail_cycles_shadow", "tail_cycles_closest", "tail_cycles_head",
-                                  "tail_bounces", "tail_max_bounces")]
+                                  "tail_bounces", "tail_max_bounces", "tail_coop_cycles_body",
+                                  "tail_coop_cycles_shadow", "tail_coop_cycles_closest", "tail_coop_cycles_head",
+                                  "tail_coop_bounces")]
 
 
 def _sig(name, res, *args):

@@ -25,7 +25,8 @@ tms = sum(v["ms"] for k, v in st.items() if k in ("trace", "extend", "shadow"))
 tp = r.get("tail_profile")
 print(sys.argv[1], "Msamples/s", d["value"], "ms/step", d["ms_per_step"], "|", "; ".join(parts),
       f"| traversal (both queries) frac {tb / (tms * 1e-3) / 8e12:.4f}" if tms else "",
-      f"| tail chain {tp['longest_chain_bounces']} cyc/bounce {tp['cycles_per_bounce']}" if tp else "")
+      f"| tail chain {tp['longest_chain_bounces']} cyc/bounce {tp['cycles_per_bounce']}" if tp else "",
+      f"| coop bounces {tp['coop_bounces']} cyc/bounce {tp['coop_cycles_per_bounce']}" if tp and "coop_bounces" in tp else "")
 PY
   done
 done

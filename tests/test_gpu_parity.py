@@ -300,6 +300,9 @@ def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
     the megakernel's framebuffer bit for bit, on a microfacet mesh (deep BVH) and on the Cornell box
     (LDS-sized BVH). Binary-tree variants also visit exactly the megakernel's nodes and primitives."""
     knobs = [k.split("=") for k in knob.split(",")]
+    # the fused kernels answer rays inside an isolated sphere without walking the tree and the ray-queue kernels do
+    # not (test_isolated_sphere_shortcut): traversal work is compared with the shortcut off in both contexts
+    monkeypatch.setenv("NH_ISO_SPHERE", "0")
     for xml in (scenegen.bumpy_cbox_xml(str(tmp_path), 160, 80)[0], scenegen.cbox_xml(str(tmp_path), "c1")):
         s = nh.Scene(xml)
         s.set_resolution(48, 40)
@@ -349,10 +352,66 @@ def test_cooperative_tail_matches_oracle(gpu, tmp_path, monkeypatch, tail, coop,
     ctx.render(0, 8, seed=17, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT, stats=True)
     st = ctx.stats()
     assert st["fused_bounce"] == 1 and st["launches_tail"] >= 1 and st["tail_bounces"] > 0
+    assert (st["tail_coop_bounces"] > 0) == (coop == "16")  # the cooperative finish ran (its own clock slots)
     np.testing.assert_array_equal(ref.framebuffer(), ctx.framebuffer())
     for k in ("ray_queries", "nodes_visited", "prims_tested"):  # (the megakernel does not split off any-hit counts)
         assert ref.stats()[k] == st[k], k
     np.testing.assert_array_equal(ctx.framebuffer(), no.OracleScene(s).render(0, 8, seed=17))
+
+
+def _render_stats(s, b, mode, integrator=None, **env):
+    import os as _os
+    old = {k: _os.environ.get(k) for k in env}
+    _os.environ.update(env)
+    try:
+        ctx = nh.Context(0)
+        ctx.upload(s, b)
+        ctx.render(0, 8, seed=17, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=mode, stats=True)
+        return ctx.framebuffer(), ctx.stats()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                _os.environ.pop(k, None)
+            else:
+                _os.environ[k] = v
+
+
+@pytest.mark.parametrize("integrator", [nh.INTEGRATOR_PATH_MIS, nh.INTEGRATOR_PATH_MATS])
+def test_isolated_sphere_shortcut(gpu, tmp_path, integrator):
+    """Rays leaving the surface of an isolated sphere (its box, grown by the host's margin, apart from every other
+    primitive's: both Cornell-box spheres) that meet it again are answered by the sphere test alone
+    (nh_traverse.h trace_next) in the megakernel and the fused wavefront kernels (RR-ahead bounce, its tail with and
+    without the cooperative finish, the round-2 bounce, the per-lane tail). Every image equals the oracle's and the
+    one rendered with the shortcut off (NH_ISO_SPHERE=0); the megakernel and the RR-ahead wavefront still do the
+    same traversal work, and less of it than without the shortcut. A glass sphere sunk into the floor (boxes
+    overlap) is not marked: the same work with the shortcut on or off."""
+    xml = scenegen.cbox_xml(str(tmp_path), "c1")
+    sunk = open(xml).read().replace('"0.445800 0.332100 0.376700"', '"0.445800 0.200000 0.376700"')
+    assert sunk != open(xml).read()
+    sunk_xml = os.path.join(os.path.dirname(xml), "cbox_sunk.xml")
+    open(sunk_xml, "w").write(sunk)
+    for path, isolated in ((xml, True), (sunk_xml, False)):
+        s = nh.Scene(path)
+        s.set_resolution(64, 48)
+        s.set_integrator(integrator)
+        b = nh.Bvh(s)
+        ref = no.OracleScene(s).render(0, 8, seed=17)
+        off, st_off = _render_stats(s, b, nh.MODE_MEGAKERNEL, NH_ISO_SPHERE="0")
+        np.testing.assert_array_equal(off, ref)
+        mk, st_mk = _render_stats(s, b, nh.MODE_MEGAKERNEL)
+        np.testing.assert_array_equal(mk, ref)
+        assert st_mk["ray_queries"] == st_off["ray_queries"]
+        if isolated:
+            assert st_mk["prims_tested"] < st_off["prims_tested"] and st_mk["nodes_visited"] < st_off["nodes_visited"]
+        else:
+            assert st_mk["prims_tested"] == st_off["prims_tested"] and st_mk["nodes_visited"] == st_off["nodes_visited"]
+        for env in ({}, {"NH_TAIL": "1000000"}, {"NH_TAIL": "1000000", "NH_TAIL_COOP": "1"}, {"NH_RR_AHEAD": "0"},
+                    {"NH_RR_AHEAD": "0", "NH_TAIL": "1000000"}, {"NH_FUSED": "0"}):
+            wf, st_wf = _render_stats(s, b, nh.MODE_WAVEFRONT, **env)
+            np.testing.assert_array_equal(wf, ref, err_msg=f"{path} {env}")
+            if "NH_FUSED" not in env:  # every closest-hit query in a fused kernel: the megakernel's work
+                for k in ("ray_queries", "nodes_visited", "prims_tested"):
+                    assert st_wf[k] == st_mk[k], (path, env, k)
 
 
 @pytest.mark.parametrize("mode", MODES)
