@@ -517,23 +517,24 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     return NH_OK;
 }
 
-// Isolated spheres (nhd::kPrimIsolated, nh_traverse.h trace_next): a sphere record whose box grown by 2m lies apart
-// from every other primitive's box gets the bit, and m in its record 1 .x (only read by the sphere shortcut). m is
+// Isolated spheres (nhd::kPrimIsolated, nh_traverse.h trace_next): a dielectric sphere's record whose box grown by 2m
+// lies apart from every other primitive's box gets the bit (only a dielectric sends its rays inside: for the others
+// the sphere test would almost always be a wasted one), and m in its record 1 .x (only read by the sphere shortcut). m is
 // 1e-4 of the scene's largest extent -- far above the float rounding of any hit point, far below the gaps of
 // real scenes (the Cornell box's spheres clear its floor by 6e-3). Boxes are compared in double, closed: a box
 // that touches or holds a NaN is not apart. NH_ISO_SPHERE=0 leaves every sphere unmarked (every ray walks the
-// tree). Spheres x primitives box tests, skipped (no marks) past 2e8.
-static void mark_isolated_spheres(std::vector<float4> &prims) {
+// tree). Spheres x primitives box tests, skipped (no marks) past 2e8. Returns the number marked.
+static int mark_isolated_spheres(std::vector<float4> &prims) {
     const char *e = std::getenv("NH_ISO_SPHERE");
-    if (e && e[0] == '0') return;
+    if (e && e[0] == '0') return 0;
     const size_t n = prims.size() / 3;
     std::vector<size_t> sph;
     for (size_t k = 0; k < n; ++k) {
         int bits;
         std::memcpy(&bits, &prims[3 * k + 2].w, 4);
-        if (bits & nhd::kPrimSphere) sph.push_back(k);
+        if ((bits & nhd::kPrimSphere) && ((bits >> nhd::kPrimMatShift) & 3) == nhd::BSDF_DIELECTRIC) sph.push_back(k);
     }
-    if (sph.empty() || (double)sph.size() * (double)n > 2e8) return;
+    if (sph.empty() || (double)sph.size() * (double)n > 2e8) return 0;
     std::vector<double> lo(3 * n), hi(3 * n);
     double slo[3] = {INFINITY, INFINITY, INFINITY}, shi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (size_t k = 0; k < n; ++k) {
@@ -556,8 +557,9 @@ static void mark_isolated_spheres(std::vector<float4> &prims) {
         }
     }
     const double ext = std::max(shi[0] - slo[0], std::max(shi[1] - slo[1], shi[2] - slo[2]));
-    if (!(ext > 0.0) || !std::isfinite(ext)) return;
+    if (!(ext > 0.0) || !std::isfinite(ext)) return 0;
     const float m = (float)(1e-4 * ext);
+    int marked = 0;
     for (size_t s : sph) {
         const float4 a = prims[3 * s];
         if (!(a.w > 0.f) || !std::isfinite(a.w) || !std::isfinite(a.x) || !std::isfinite(a.y) || !std::isfinite(a.z))
@@ -579,7 +581,9 @@ static void mark_isolated_spheres(std::vector<float4> &prims) {
         bits |= nhd::kPrimIsolated;
         std::memcpy(&prims[3 * s + 2].w, &bits, 4);
         prims[3 * s + 1].x = m;
+        ++marked;
     }
+    return marked;
 }
 
 // 4-wide collapse of the GPU binary tree (nh_traverse.h Tracer4): every wide node takes the two
@@ -797,7 +801,7 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
             p[2] = make_float4(p2[0], p2[1], p2[2], f0);
         }
     }
-    mark_isolated_spheres(prims);
+    S.iso_spheres = mark_isolated_spheres(prims);
     // leaf-end bits: the 4-wide traversal walks a leaf's records until this bit
     for (const int2 &lf : leaves)
         if (lf.y > 0) {
@@ -1030,7 +1034,7 @@ static bool splat_staged(const nh_ctx *c) {
 // float4 entries of one (round, block) ImageBlock in the splat's staging buffer (0: the fused splat stages nothing)
 static size_t block_px(const nh_ctx *c, bool staged) {
     if (!staged) return 0;
-    return (size_t)(32 + 2 * c->border) * (32 + 2 * c->border);
+    return (size_t)(32 + 2 * c->border) * (size_t)stage_pitch(32 + 2 * c->border);
 }
 
 // path pools driven by pipeline_run (NH_POOLS: 1 = no overlap, for A/B and tests). Scenes with mirror or

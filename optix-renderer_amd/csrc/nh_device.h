@@ -198,6 +198,8 @@ struct DScene {
     // 1: a light sample is always finite and never at a discrete-BSDF shading point (nh_api.hip, upload), so the
     // wavefront shade skips the light sample of a discrete BSDF sample (it provably adds +-0)
     int nee_finite;
+    // isolated dielectric spheres the BVH upload marked (nh_traverse.h trace_next; 0: no ray tries the shortcut)
+    int iso_spheres;
 };
 
 NHD F3 ldv(const float *a, uint32_t i) { return f3(a[3 * i], a[3 * i + 1], a[3 * i + 2]); }

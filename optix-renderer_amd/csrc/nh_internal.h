@@ -24,6 +24,11 @@ struct PathLaunch {
     float *rec_jy;          // jitter.y
     unsigned long long *counters;
 };
+// Row pitch (float4) of one (round, block) ImageBlock of (32+2b)^2 pixels in the splat's staging buffer: rows start
+// on 128-B lines, so the merge's 16-pixel row segments (master columns 16a..16a+15 = block columns 0..15 / 16..31)
+// read whole lines instead of straddling three (the unpadded 36-float4 rows start 64 B off a line every other row)
+__host__ __device__ __forceinline__ int stage_pitch(int cols) { return (cols + 7) & ~7; }
+
 struct SplatLaunch {
     float *fb;              // master RGBW (W+2b)x(H+2b)
     int width, height, border, reach, nbx, n_rounds, n_list;
@@ -41,7 +46,7 @@ struct SplatLaunch {
     int staged;             // 1: staged pair (splat into staging, then merge); 0: the fused tile splat (no staging).
                             // Fixed when the chunk's staging was sized, so a knob change mid-pipeline cannot
                             // mismatch the two
-    int direct;             // the tab splat added the rounds of pixels with one covering block to fb (merge skips them)
+    int direct;             // rounds the tab splat added to fb for pixels one block covers (the merge starts them there)
     int debug;              // timing experiments only (NH_SPLAT_DEBUG, images wrong): bits skip the fused splat's
                             // phase 1 (1), phase 2 (2), record fetch (4), master-border strips (8)
 };

@@ -77,7 +77,8 @@ __global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
     const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
     const int cols = 32 + 2 * P.border;
     splat_stage(P, L, ox, oy, sxb, syb, k, cols);
-    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+    const int pitch = stage_pitch(cols);
+    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * pitch);
     const int R = P.reach, bd = P.border;
     for (int q = threadIdx.x; q < cols * cols; q += 256) {
         const int yt = q / cols, xt = q - yt * cols;
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
                 ab += L.val[2][i] * wx * wy;
                 aw += 1.0f * wx * wy;
             }
-        out[q] = make_float4(ar, ag, ab, aw);
+        out[yt * pitch + xt] = make_float4(ar, ag, ab, aw);
     }
 }
 
@@ -116,7 +117,8 @@ __global__ __launch_bounds__(256) void nh_block_splat_strip_kernel(SplatLaunch P
     const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
     const int cols = 32 + 2 * P.border;
     splat_stage(P, L, ox, oy, sxb, syb, k, cols);
-    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * cols);
+    const int pitch = stage_pitch(cols);
+    float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(cols * pitch);
     const int R = P.reach, bd = P.border;
     const int n_strips = (cols + kStripRows - 1) / kStripRows;
     for (int t = threadIdx.x; t < cols * n_strips; t += 256) {
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(256) void nh_block_splat_strip_kernel(SplatLaunch P
             }
 #pragma unroll
         for (int j = 0; j < kStripRows; ++j)
-            if (yt0 + j < cols) out[(yt0 + j) * cols + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
+            if (yt0 + j < cols) out[(yt0 + j) * pitch + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
     }
 }
 
@@ -249,15 +251,19 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
     bool own[kStripRows];
     float4 m[kStripRows];
     float4 *const fb4 = reinterpret_cast<float4 *>(P.fb);
+    // LEAD: the first workgroup of the block's rounds (rounds 0 .. ROUNDS-1) adds them straight into the master
+    // for the pixels only this block covers, in round order, read-modify-write (they come first in the merge's
+    // order: the merge starts those pixels at round P.direct), and stages only the shared pixels
+    const bool lead = !DIRECT && P.direct > 0 && blockIdx.y == 0;
 #pragma unroll
     for (int j = 0; j < kStripRows; ++j) {
         own[j] = false;
         m[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (DIRECT && threadIdx.x < 36 * 6) {
+        if ((DIRECT || lead) && threadIdx.x < 36 * 6) {
             const int mx = ox + xt, my = oy + yt0 + j;  // block-array position -> master pixel
             int sl[4];
             own[j] = mx < mcols && my < mrows && covering_blocks(P, mx, my, sl) == 1 && sl[0] == slot;
-            if (own[j]) m[j] = fb4[(size_t)my * mcols + mx];
+            if (DIRECT && own[j]) m[j] = fb4[(size_t)my * mcols + mx];
         }
     }
     for (int k = k0; k < k1; ++k) {
@@ -318,7 +324,7 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
                     }
                 }
             }
-            float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(36 * 36);
+            float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(36 * stage_pitch(36));
 #pragma unroll
             for (int j = 0; j < kStripRows; ++j) {
                 if (DIRECT && own[j]) {  // round k of a pixel only this block covers: the master, in round order
@@ -326,8 +332,16 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
                     m[j].y += rg[j].y;
                     m[j].z += bw[j].x;
                     m[j].w += bw[j].y;
+                } else if (!DIRECT && lead && own[j]) {  // the same, through the framebuffer (no registers held)
+                    float4 *mp = fb4 + (size_t)(oy + yt0 + j) * mcols + ox + xt;
+                    float4 mv = *mp;
+                    mv.x += rg[j].x;
+                    mv.y += rg[j].y;
+                    mv.z += bw[j].x;
+                    mv.w += bw[j].y;
+                    *mp = mv;
                 } else {
-                    out[(yt0 + j) * 36 + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
+                    out[(yt0 + j) * stage_pitch(36) + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
                 }
             }
         }
@@ -646,37 +660,41 @@ __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
     const int mcols = P.width + 2 * P.border, mrows = P.height + 2 * P.border;
     const int mx = blockIdx.x * 16 + (threadIdx.x & 15), my = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (mx >= mcols || my >= mrows) return;
-    const int cols = 32 + 2 * P.border;
+    const int cols = 32 + 2 * P.border, pitch = stage_pitch(cols);
     int slot[4];
     const int nb = covering_blocks(P, mx, my, slot);
-    if (nb == 0 || (P.direct && nb == 1)) return;  // direct: the tab splat already added this pixel's rounds
+    // P.direct: rounds the tab splat already added to the pixels one block covers (all of them, or its first
+    // workgroup's)
+    if (nb == 0 || (nb == 1 && P.direct >= P.n_rounds)) return;
     int off[4];
     for (int q = 0; q < nb; ++q) {
         const int bid = P.blocks[slot[q]];
         const int by = bid / P.nbx, bx = bid - by * P.nbx;
-        off[q] = (my - by * 32) * cols + (mx - bx * 32);
+        off[q] = (my - by * 32) * pitch + (mx - bx * 32);
     }
     float4 *mp = reinterpret_cast<float4 *>(P.fb) + (size_t)my * mcols + mx;
     float4 m = *mp;
-    const size_t per_round = (size_t)P.n_blocks * (size_t)(cols * cols);
-    int k = 0;
-    if (nb == 1) {  // one covering block (most pixels): four rounds' loads in flight, added in round order
-        const float4 *src = P.staging + (size_t)slot[0] * (cols * cols) + off[0];
-        for (; k + 4 <= P.n_rounds; k += 4) {
-            const float4 v0 = src[(size_t)k * per_round], v1 = src[(size_t)(k + 1) * per_round],
-                         v2 = src[(size_t)(k + 2) * per_round], v3 = src[(size_t)(k + 3) * per_round];
-            for (const float4 &v : {v0, v1, v2, v3}) {
-                m.x += v.x;
-                m.y += v.y;
-                m.z += v.z;
-                m.w += v.w;
+    const size_t blk = (size_t)cols * pitch, per_round = (size_t)P.n_blocks * blk;
+    int k = nb == 1 ? P.direct : 0;
+    if (nb == 1) {  // one covering block (most pixels): eight rounds' loads in flight, added in round order
+        const float4 *src = P.staging + (size_t)slot[0] * blk + off[0];
+        for (; k + 8 <= P.n_rounds; k += 8) {
+            float4 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = src[(size_t)(k + j) * per_round];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                m.x += v[j].x;
+                m.y += v[j].y;
+                m.z += v[j].z;
+                m.w += v[j].w;
             }
         }
     }
     for (; k < P.n_rounds; ++k) {
         const float4 *base = P.staging + (size_t)k * per_round;
         for (int q = 0; q < nb; ++q) {
-            const float4 v = base[(size_t)slot[q] * (cols * cols) + off[q]];
+            const float4 v = base[(size_t)slot[q] * blk + off[q]];
             m.x += v.x;
             m.y += v.y;
             m.z += v.z;
@@ -738,17 +756,19 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
     Q.direct = 0;
     if (tabulated && P.border == 2 && P.reach == 2) {
         const char *d = std::getenv("NH_SPLAT_DIRECT");  // opt-in until measured
-        Q.direct = d && d[0] == '1' ? 1 : 0;
+        const bool all_direct = d && d[0] == '1';
         const char *rv = std::getenv("NH_SPLAT_ROUNDS");  // rounds per workgroup: 1, 2, 4 (default) or 8
         int tr = rv ? std::atoi(rv) : kTabRounds;
         if (tr != 1 && tr != 2 && tr != 4 && tr != 8) tr = kTabRounds;  // 0 / garbage: the default (no 0 divisor)
+        const char *ld = std::getenv("NH_SPLAT_LEAD");  // the first workgroup's rounds straight into the master
+        const bool lead = !(ld && ld[0] == '0');
+        Q.direct = all_direct ? P.n_rounds : lead ? std::min(tr, P.n_rounds) : 0;
         const dim3 g(P.n_blocks, (P.n_rounds + tr - 1) / tr);
-        if (Q.direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
+        if (all_direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
         else if (tr == 1) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 1>), g, dim3(256), 0, st, Q);
         else if (tr == 2) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 2>), g, dim3(256), 0, st, Q);
         else if (tr == 8) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8>), g, dim3(256), 0, st, Q);
-        else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, kTabRounds>), dim3(P.n_blocks, (P.n_rounds + kTabRounds - 1) / kTabRounds),
-                                dim3(256), 0, st, Q);
+        else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, kTabRounds>), g, dim3(256), 0, st, Q);
     }
     else if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     else hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);

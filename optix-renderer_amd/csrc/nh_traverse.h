@@ -499,7 +499,8 @@ NHD bool iso_sphere_hit(const Traversal &tv, int k_prev, F3 o, F3 d, float mint,
 template <int DEPTH, bool ORDERED, bool STATS, bool PAIRS = false, int G = 1>
 NHD bool trace_next(const Traversal &tv, const DScene &S, int k_prev, F3 o, F3 d, float mint, float maxt, Hit &best,
                     uint32_t *stk, int stride, TravStats &st) {
-    if (S.root_kind != 0 && iso_sphere_hit<STATS, G>(tv, k_prev, o, d, mint, maxt, best, st)) return true;
+    if (S.iso_spheres && S.root_kind != 0 && iso_sphere_hit<STATS, G>(tv, k_prev, o, d, mint, maxt, best, st))
+        return true;
     return trace<DEPTH, ORDERED, false, STATS, PAIRS, G>(tv, S, o, d, mint, maxt, best, stk, stride, st);
 }
 

@@ -1338,7 +1338,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAV
             const bool live = o.rd.w >= o.ro.w;
             q_e += live ? 1 : 0;
             const bool found =
-                live && ((S.root_kind != 0 && iso_sphere_hit<STATS>(tv, kp, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h, st_e)) ||
+                live && ((S.iso_spheres && S.root_kind != 0 && iso_sphere_hit<STATS>(tv, kp, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h, st_e)) ||
                          trace_lane<WIDE, DEPTH, ORDERED, false, STATS>(tv, S, L, xyz(o.ro), xyz(o.rd), o.ro.w, o.rd.w, h,
                                                                         stk, st_e));
             kp = found ? h.k : -1;

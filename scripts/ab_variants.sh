@@ -23,7 +23,7 @@ parts = [f"{k} {v['ms']}ms/{v['launches']} {round(v['global_gbs'] / 8000, 4)}" f
 tb = sum(v["global_bytes_per_launch"] * v["launches"] for k, v in st.items() if k in ("trace", "extend", "shadow"))
 tms = sum(v["ms"] for k, v in st.items() if k in ("trace", "extend", "shadow"))
 tp = r.get("tail_profile")
-print(sys.argv[1], "Msamples/s", d["value"], "ms/step", d["ms_per_step"], "|", "; ".join(parts),
+print(sys.argv[1], "Msamples/s", d["value"], "ms/step", d["ms_per_step"], "| splat", r.get("splat_ms_per_launch"), "ms/chunk |", "; ".join(parts),
       f"| traversal (both queries) frac {tb / (tms * 1e-3) / 8e12:.4f}" if tms else "",
       f"| tail chain {tp['longest_chain_bounces']} cyc/bounce {tp['cycles_per_bounce']}" if tp else "",
       f"| coop bounces {tp['coop_bounces']} cyc/bounce {tp['coop_cycles_per_bounce']}" if tp and "coop_bounces" in tp else "")

@@ -218,18 +218,25 @@ def test_render_deterministic_and_sharded(gpu, tmp_path):
                                             ((64, 64), 3, [1, 2]), ((96, 96), 2, [4])])
 def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, spp, blocks):
     """The fused splat + merge (NH_SPLAT_FUSED=1: one workgroup per master tile, rounds in order, blocks in spiral
-    order, no staging) and the staged pair with and without direct interior pixels (NH_SPLAT_DIRECT: pixels one
-    block covers go straight to the master) give the same framebuffer bit for bit, and the oracle's: partial blocks and the master
-    border of the last block column / row (100x70, 33x31), block subsets whose neighbours are absent (every tile
-    quadrant case), several chunks (1 MiB path budget) and both render modes."""
+    order, no staging) and the staged pair -- its first workgroup per block adding its rounds of the pixels only that
+    block covers straight into the master (default, at 1 / 4 / 8 rounds per workgroup), every workgroup staging
+    (NH_SPLAT_LEAD=0), one workgroup per block taking all rounds of those pixels (NH_SPLAT_DIRECT=1) -- give the same
+    framebuffer bit for bit, and the oracle's: partial blocks and the master border of the last block column / row
+    (100x70, 33x31), block subsets whose neighbours are absent (every tile quadrant case), several chunks (1 MiB path
+    budget) and both render modes."""
     xml = scenegen.cbox_xml(str(tmp_path), "c2")
     s = nh.Scene(xml)
     s.set_resolution(*res)
     b = nh.Bvh(s)
     out = {}
-    for fused, direct in (("0", "1"), ("0", "0"), ("1", "1")):  # staged (direct interior / all staged), fused
-        monkeypatch.setenv("NH_SPLAT_FUSED", fused)
-        monkeypatch.setenv("NH_SPLAT_DIRECT", direct)
+    variants = ({"NH_SPLAT_DIRECT": "1"}, {"NH_SPLAT_LEAD": "0"}, {}, {"NH_SPLAT_ROUNDS": "8"},
+                {"NH_SPLAT_ROUNDS": "1"}, {"NH_SPLAT_FUSED": "1"})
+    for env in variants:
+        for name in ("NH_SPLAT_DIRECT", "NH_SPLAT_LEAD", "NH_SPLAT_ROUNDS", "NH_SPLAT_FUSED"):
+            monkeypatch.delenv(name, raising=False)
+        for name, val in env.items():
+            monkeypatch.setenv(name, val)
+        fused, direct = env.get("NH_SPLAT_FUSED", "0"), repr(sorted(env.items()))
         for mode in (nh.MODE_MEGAKERNEL, nh.MODE_WAVEFRONT):
             for budget in (None, "1"):
                 if budget:
@@ -383,10 +390,10 @@ def test_isolated_sphere_shortcut(gpu, tmp_path, integrator):
     (nh_traverse.h trace_next) in the megakernel and the fused wavefront kernels (RR-ahead bounce, its tail with and
     without the cooperative finish, the round-2 bounce, the per-lane tail). Every image equals the oracle's and the
     one rendered with the shortcut off (NH_ISO_SPHERE=0); the megakernel and the RR-ahead wavefront still do the
-    same traversal work, and less of it than without the shortcut. A glass sphere sunk into the floor (boxes
-    overlap) is not marked: the same work with the shortcut on or off."""
+    same traversal work, and less of it than without the shortcut. Spheres sunk into the floor (boxes overlap) are
+    not marked: the same work with the shortcut on or off."""
     xml = scenegen.cbox_xml(str(tmp_path), "c1")
-    sunk = open(xml).read().replace('"0.445800 0.332100 0.376700"', '"0.445800 0.200000 0.376700"')
+    sunk = open(xml).read().replace(' 0.332100 ', ' 0.200000 ')  # both spheres into the floor
     assert sunk != open(xml).read()
     sunk_xml = os.path.join(os.path.dirname(xml), "cbox_sunk.xml")
     open(sunk_xml, "w").write(sunk)
