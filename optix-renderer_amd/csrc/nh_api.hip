@@ -63,8 +63,7 @@ struct WfPool {
     WfState wf{};
     std::vector<void *> bufs;
     size_t cap = 0;  // paths
-    float4 *rec = nullptr;
-    float *rec_jy = nullptr;
+    float *rec = nullptr;  // (r, g, b) per sample
     size_t rec_cap = 0;
     float4 *staging = nullptr;
     size_t staging_cap = 0;
@@ -140,8 +139,7 @@ struct nh_ctx {
     bool specular = false;             // a mirror or dielectric BSDF: long discrete chains, long chunk tails
     float *fb = nullptr;
     size_t fb_floats = 0;
-    float4 *rec = nullptr;
-    float *rec_jy = nullptr;
+    float *rec = nullptr;  // (r, g, b) per sample
     size_t rec_cap = 0;  // entries
     int *pixel_list = nullptr, *pixel_map = nullptr, *block_rank = nullptr;
     int *block_ids = nullptr, *block_slot = nullptr;
@@ -271,7 +269,6 @@ void nh_destroy(nh_ctx *c) {
     free_all(c->bvh_bufs);
     (void)hipFree(c->fb);
     (void)hipFree(c->rec);
-    (void)hipFree(c->rec_jy);
     (void)hipFree(c->pixel_list);
     (void)hipFree(c->pixel_map);
     (void)hipFree(c->block_rank);
@@ -967,12 +964,9 @@ static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t rec_n, size_t stagi
     // the chunk's sample records: owned by whichever pool or tail slot holds the chunk (they move with it)
     if (p.rec_cap < rec_n) {
         (void)hipFree(p.rec);
-        (void)hipFree(p.rec_jy);
         p.rec = nullptr;
-        p.rec_jy = nullptr;
         p.rec_cap = 0;
-        HIP_TRY(c, hipMalloc(&p.rec, rec_n * sizeof(float4)));
-        HIP_TRY(c, hipMalloc(&p.rec_jy, rec_n * sizeof(float)));
+        HIP_TRY(c, hipMalloc(&p.rec, rec_n * 3 * sizeof(float)));
         p.rec_cap = rec_n;
     }
     if (p.staging_cap < staging_f4) {
@@ -988,7 +982,6 @@ static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t rec_n, size_t stagi
 static void pool_free(WfPool &p) {
     free_all(p.bufs);
     (void)hipFree(p.rec);
-    (void)hipFree(p.rec_jy);
     (void)hipFree(p.staging);
     (void)hipFree(p.spill);
     if (p.h_counts) (void)hipHostFree(p.h_counts);
@@ -1001,7 +994,7 @@ static void pool_free(WfPool &p) {
     p = WfPool{};
 }
 
-static SplatLaunch make_splat(const nh_ctx *c, const float4 *rec, const float *rec_jy, float4 *staging, int rounds,
+static SplatLaunch make_splat(const nh_ctx *c, const float *rec, uint64_t seed, int s0, float4 *staging, int rounds,
                               bool staged) {
     SplatLaunch P{};
     P.staged = staged ? 1 : 0;
@@ -1015,8 +1008,9 @@ static SplatLaunch make_splat(const nh_ctx *c, const float4 *rec, const float *r
     P.n_list = c->n_list;
     P.pixel_map = c->pixel_map;
     P.block_rank = c->block_rank;
-    P.rec_rgbx = rec;
-    P.rec_jy = rec_jy;
+    P.rec = rec;
+    P.seed = seed;
+    P.s0 = s0;
     P.radius = c->filter.radius;
     P.lookup = c->filter.lookup_factor;
     std::memcpy(P.table, c->filter.table, sizeof(P.table));
@@ -1089,8 +1083,7 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     L.s0 = j.s0;
     L.seed = j.seed;
     L.pixel_list = c->pixel_list;
-    L.rec_rgbx = p.rec;
-    L.rec_jy = p.rec_jy;
+    L.rec = p.rec;
     L.counters = c->counters;
     // scenes whose BVH fits in a few KB (the Cornell box: < 1 KB) are traversed from an LDS copy
     const size_t scene_bytes = 16 * (size_t)(c->n_node_f4 + c->n_prim_f4) + 8 * (size_t)c->n_leaves;
@@ -1197,7 +1190,6 @@ static void chunk_swap(WfPool &a, WfPool &b) {
     std::swap(a.in_e, b.in_e);
     std::swap(a.in_s, b.in_s);
     std::swap(a.rec, b.rec);
-    std::swap(a.rec_jy, b.rec_jy);
     std::swap(a.rec_cap, b.rec_cap);
     std::swap(a.staging, b.staging);
     std::swap(a.staging_cap, b.staging_cap);
@@ -1365,7 +1357,7 @@ static int pool_splat(nh_ctx *c, WfPool &p) {
     if (p.job.stats) nh::launch_count_invalid(p.rec, (size_t)p.L.n_paths, c->counters, p.stream);
     if (c->fb_ev_set) HIP_TRY(c, hipStreamWaitEvent(p.stream, c->fb_ev, 0));
     HIP_TRY(c, hipEventRecord(p.ev_splat0, p.stream));
-    nh::launch_splat(make_splat(c, p.rec, p.rec_jy, p.staging, p.job.rounds, p.job.staged), p.stream);
+    nh::launch_splat(make_splat(c, p.rec, p.L.seed, p.L.s0, p.staging, p.job.rounds, p.job.staged), p.stream);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(p.ev_splat, p.stream));
     HIP_TRY(c, hipEventRecord(c->fb_ev, p.stream));
@@ -1634,7 +1626,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     if (q->collect_stats)
         HIP_TRY(c, hipMemsetAsync(c->counters, 0, kStatShards * kStatStride * sizeof(unsigned long long), c->stream));
     const size_t per_round = (size_t)c->n_list;
-    const size_t per_round_bytes = per_round * 20 + (size_t)c->n_blocks * block_px(c, splat_staged(c)) * 16 +
+    const size_t per_round_bytes = per_round * 12 + (size_t)c->n_blocks * block_px(c, splat_staged(c)) * 16 +
                                    (wavefront ? per_round * kWfBytesPerPath : 0);
     // device memory per chunk: sample records + block ImageBlocks (+ path state, per pool). Every
     // wavefront chunk ends in a tail whose length is set by its longest path (C4: ~5-7 ms of
@@ -1679,13 +1671,10 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     } else {
         if (c->rec_cap < (size_t)chunk * per_round) {
             (void)hipFree(c->rec);
-            (void)hipFree(c->rec_jy);
             c->rec = nullptr;
-            c->rec_jy = nullptr;
             c->rec_cap = 0;
             const size_t cap = (size_t)chunk * per_round;
-            HIP_TRY(c, hipMalloc(&c->rec, cap * sizeof(float4)));
-            HIP_TRY(c, hipMalloc(&c->rec_jy, cap * sizeof(float)));
+            HIP_TRY(c, hipMalloc(&c->rec, cap * 3 * sizeof(float)));
             c->rec_cap = cap;
         }
         const bool staged = splat_staged(c);
@@ -1709,8 +1698,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
             L.s0 = s;
             L.seed = q->seed;
             L.pixel_list = c->pixel_list;
-            L.rec_rgbx = c->rec;
-            L.rec_jy = c->rec_jy;
+            L.rec = c->rec;
             L.counters = c->counters;
             Ev ev;
             HIP_TRY(c, hipEventCreate(&ev.a));
@@ -1722,7 +1710,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev.b, c->stream));
             if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters, c->stream);
-            nh::launch_splat(make_splat(c, c->rec, c->rec_jy, c->staging, k, staged), c->stream);
+            nh::launch_splat(make_splat(c, c->rec, q->seed, s, c->staging, k, staged), c->stream);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev.d, c->stream));
             evs.push_back(ev);

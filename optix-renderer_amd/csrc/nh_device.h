@@ -119,6 +119,23 @@ NHD Rng path_rng(uint64_t seed, uint64_t pixel, uint64_t sample) {
     r.next_uint();
     return r;
 }
+// path_rng with its splitmix64(seed ^ pixel) already formed (the splat reuses it over a pixel's rounds)
+NHD Rng path_rng_h(uint64_t h, uint64_t sample) {
+    Rng r;
+    r.state = 0u;
+    r.inc = (sample << 1u) | 1u;
+    r.next_uint();
+    r.state += h;
+    r.next_uint();
+    return r;
+}
+// The pixel jitter of a sample (render.cpp:441-442: the camera sample's first next2D): recomputed by the splat from
+// the sample's seed instead of stored in its record
+NHD void sample_jitter_h(uint64_t h, uint64_t sample, float &jx, float &jy) {
+    Rng r = path_rng_h(h, sample);
+    jx = r.next1d();
+    jy = r.next1d();
+}
 
 // ---- scene records -----------------------------------------------------------
 enum : int { SHAPE_MESH = 0, SHAPE_SPHERE = 1 };

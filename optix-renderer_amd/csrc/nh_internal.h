@@ -20,22 +20,32 @@ struct PathLaunch {
     int s0;                 // first sample round of the chunk
     uint64_t seed;
     const int *pixel_list;  // y*W+x per list entry (ordered block by block)
-    float4 *rec_rgbx;       // (r, g, b, jitter.x) per (round, list entry)
-    float *rec_jy;          // jitter.y
+    float *rec;             // (r, g, b) per (round, list entry); the splat recomputes the pixel jitter (sample_jitter)
     unsigned long long *counters;
 };
 // Row pitch (float4) of one (round, block) ImageBlock of (32+2b)^2 pixels in the splat's staging buffer: rows start
 // on 128-B lines, so the merge's 16-pixel row segments (master columns 16a..16a+15 = block columns 0..15 / 16..31)
 // read whole lines instead of straddling three (the unpadded 36-float4 rows start 64 B off a line every other row)
 __host__ __device__ __forceinline__ int stage_pitch(int cols) { return (cols + 7) & ~7; }
+// Offset (float4) of block-array pixel (xt, yt) in one (round, block) ImageBlock of the staging buffer (stride
+// cols * stage_pitch(cols)). band = 1 (the 36x36 arrays of the tabulated splat): the 32x32 core row-major, then the
+// right band (columns 32..35, 36 rows of 4), then the bottom band (rows 32..35, 32 columns), so the merge's reads --
+// a wave's 4 rows x 16 master columns of one block's core, or of a neighbour's band -- are whole 128-B lines
+__host__ __device__ __forceinline__ int stage_off(int cols, int band, int xt, int yt) {
+    if (!band) return yt * stage_pitch(cols) + xt;
+    if (xt >= 32) return 1024 + yt * 4 + (xt - 32);
+    if (yt >= 32) return 1024 + 144 + (yt - 32) * 32 + xt;
+    return yt * 32 + xt;
+}
 
 struct SplatLaunch {
     float *fb;              // master RGBW (W+2b)x(H+2b)
     int width, height, border, reach, nbx, n_rounds, n_list;
     const int *pixel_map;   // image pixel -> list entry or -1
     const int *block_rank;  // BlockGenerator spiral rank per block id
-    const float4 *rec_rgbx;
-    const float *rec_jy;
+    const float *rec;       // (r, g, b) per (round, list entry)
+    uint64_t seed;          // the chunk's seed and first sample round: the jitter of round k's sample at pixel p is
+    int s0;                 // sample_jitter(seed, p, s0 + k), the camera sample's first two draws
     float radius, lookup;
     float table[33];
     // block-local ImageBlocks (one per (round, rendered block)), (32+2b)^2 RGBW each
@@ -47,6 +57,7 @@ struct SplatLaunch {
                             // Fixed when the chunk's staging was sized, so a knob change mid-pipeline cannot
                             // mismatch the two
     int direct;             // rounds the tab splat added to fb for pixels one block covers (the merge starts them there)
+    int band;               // staging offsets: stage_off(.., band, ..) (1: the tabulated splat's core + band layout)
     int debug;              // timing experiments only (NH_SPLAT_DEBUG, images wrong): bits skip the fused splat's
                             // phase 1 (1), phase 2 (2), record fetch (4), master-border strips (8)
 };
@@ -90,7 +101,7 @@ void launch_path(const nhd::DScene *S, const nhd::Traversal &tv, const PathLaunc
 void launch_splat(const SplatLaunch &P, hipStream_t st);
 // false: launch_splat adds the records straight into the master (no per-(round, block) staging buffer)
 bool splat_uses_staging(int border, int reach);
-void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st);
+void launch_count_invalid(const float *rec, size_t n, unsigned long long *out, hipStream_t st);
 void launch_denoise_variance(const DenoiseLaunch &P, hipStream_t st);
 int denoise_band_rows();
 int denoise_max_chunk();
@@ -138,8 +149,7 @@ struct WfLaunch {
     int n_paths, n_list, s0;
     uint64_t seed;
     const int *pixel_list;
-    float4 *rec_rgbx;
-    float *rec_jy;
+    float *rec;
     int in_q;               // buffer (and count slot) read by this bounce
     int first;              // bounce 0: paths come from the camera, not from a buffer
     unsigned *cnt_in;       // count slot of this bounce's input queues

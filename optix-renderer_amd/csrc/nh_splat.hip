@@ -25,6 +25,11 @@ namespace {
 constexpr int kSplatMaxCols = 40;  // 32 + 2*border, border <= 4
 constexpr int kStripRows = 6;      // block-array rows one thread sums in the strip variant
 
+// sample record r: (r, g, b)
+__device__ __forceinline__ F3 load_rec(const float *rec, size_t r) {
+    return f3(rec[3 * r], rec[3 * r + 1], rec[3 * r + 2]);
+}
+
 // phase 1 of the block splat: every sample's footprint (block-array box), filter position and value into LDS
 // (sample (lx, ly) at lx*33 + ly: x-major, the odd stride keeps neighbouring lx on distinct banks)
 struct SplatLds {
@@ -48,9 +53,12 @@ __device__ __forceinline__ void splat_stage(const SplatLaunch &P, SplatLds &L, i
         if (lx < sxb && ly < syb) {
             const int li = P.pixel_map[(oy + ly) * P.width + (ox + lx)];
             if (li >= 0) {
-                const float4 rec = P.rec_rgbx[rbase + li];
-                if (is_valid(f3(rec.x, rec.y, rec.z))) {  // invalid samples drop with their weight
-                    const float spx = (float)(ox + lx) + rec.w, spy = (float)(oy + ly) + P.rec_jy[rbase + li];
+                const F3 rec = load_rec(P.rec, rbase + li);
+                if (is_valid(rec)) {  // invalid samples drop with their weight
+                    float jx, jy;
+                    sample_jitter_h(splitmix64(P.seed ^ (uint64_t)((oy + ly) * P.width + (ox + lx))),
+                                    (uint64_t)(P.s0 + k), jx, jy);
+                    const float spx = (float)(ox + lx) + jx, spy = (float)(oy + ly) + jy;
                     px = spx - 0.5f - (float)(ox - P.border);
                     py = spy - 0.5f - (float)(oy - P.border);
                     int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
@@ -196,7 +204,7 @@ __device__ __forceinline__ int covering_blocks(const SplatLaunch &P, int mx, int
 // at +0 and can never be -0, and finite (v * wx) * 0 is 0, so every sum is the one the reference forms.
 // Each workgroup walks kTabRounds rounds of one block; the next round's records are loaded during the
 // current round's phase 2.
-constexpr int kTabRounds = 4;
+constexpr int kTabRounds = 8;  // 8: the lead workgroups take half the rounds (fewest staged bytes, fastest)
 constexpr int kTabRow = 33;                 // plane row: lx 0..31 + a zero column (lx outside 0..31)
 constexpr int kTabPlane = 40 * kTabRow;     // rows ly = -4..35 (ly + 4): 4 zero rows either side
 constexpr int kTabV = 0, kTabWX = 3, kTabWY = 8, kTabPlanes = 13;
@@ -204,16 +212,18 @@ constexpr int kTabV = 0, kTabWX = 3, kTabWY = 8, kTabPlanes = 13;
 // other rendered block covers (the block's 28x28 interior, and the master border of edge blocks) add each round's
 // value straight into the master in round order -- the merge's sum for a pixel with one covering block -- so only
 // the pixels shared with neighbouring blocks go through the staging buffer and nh_merge_kernel.
-template <bool DIRECT, int ROUNDS = kTabRounds>
-__global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
-    __shared__ float W[kTabPlanes * kTabPlane];
-    __shared__ float tab[33];
+// DIRECT (tab_body): rounds [k0, k1) of the pixels this block alone covers go straight into the master, accumulated
+// in registers; the kernel runs it for all rounds (nh_block_splat_tab_kernel<true>) or, by default, for the first
+// workgroup of each block (rounds 0 .. ROUNDS-1: they come first in the merge's order, which starts those pixels at
+// round P.direct). A separate inlined body per mode keeps the staged-only workgroups at their own register count.
+// (A read-modify-write of the framebuffer per round instead of the registers was built and spills past 256 VGPRs.)
+template <bool DIRECT>
+__device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *tab, int k0, int k1) {
     const int slot = blockIdx.x;
     const int bid = P.blocks[slot];
     const int by = bid / P.nbx, bx = bid - by * P.nbx;
     const int ox = bx * 32, oy = by * 32;
     const int sxb = min(32, P.width - ox), syb = min(32, P.height - oy);
-    const int k0 = DIRECT ? 0 : blockIdx.y * ROUNDS, k1 = DIRECT ? P.n_rounds : min(k0 + ROUNDS, P.n_rounds);
     const float r = P.radius;
     if (threadIdx.x < 33) tab[threadIdx.x] = P.table[threadIdx.x];
     // the zero rows and column are never written again
@@ -228,21 +238,22 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
     // phase-1 samples of this thread: (lx, ly) = (s & 31, s >> 5), s = threadIdx.x + 256 q (block rows are
     // consecutive list entries: neighbouring lanes load neighbouring records)
     int li[4];
-    float4 rec[4];
-    float rjy[4];
+    F3 rec[4];
+    uint64_t hs[4];  // splitmix64(seed ^ pixel) of each sample's path stream: its jitter is recomputed per round
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
         li[q] = (lx < sxb && ly < syb) ? P.pixel_map[(oy + ly) * P.width + (ox + lx)] : -1;
+        hs[q] = splitmix64(P.seed ^ (uint64_t)((oy + ly) * P.width + (ox + lx)));
     }
+    float sjx[4], sjy[4];  // the round's jitter, formed with the record fetch (during the previous round's sums)
     auto fetch = [&](int k) {
         const size_t rbase = (size_t)k * P.n_list;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (li[q] >= 0) {
-                rec[q] = P.rec_rgbx[rbase + li[q]];
-                rjy[q] = P.rec_jy[rbase + li[q]];
-            }
+        for (int q = 0; q < 4; ++q) {
+            if (li[q] >= 0) rec[q] = load_rec(P.rec, rbase + li[q]);
+            sample_jitter_h(hs[q], (uint64_t)(P.s0 + k), sjx[q], sjy[q]);
+        }
     };
     fetch(k0);
     // phase-2 strip of this thread: block-array column xt, rows yt0..yt0+5
@@ -251,29 +262,44 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
     bool own[kStripRows];
     float4 m[kStripRows];
     float4 *const fb4 = reinterpret_cast<float4 *>(P.fb);
-    // LEAD: the first workgroup of the block's rounds (rounds 0 .. ROUNDS-1) adds them straight into the master
-    // for the pixels only this block covers, in round order, read-modify-write (they come first in the merge's
-    // order: the merge starts those pixels at round P.direct), and stages only the shared pixels
-    const bool lead = !DIRECT && P.direct > 0 && blockIdx.y == 0;
+    // Pixels only this block covers (covering_blocks(..) == 1, the merge's test): inside the master and this
+    // block's array, and not in the 4-pixel band a rendered neighbour's array also covers -- left / up neighbours
+    // (full blocks) cover array columns / rows 0..3, right / down ones 32..35, diagonal ones the corner squares
+    unsigned nbr = 0;  // rendered neighbours: bit (dy + 1) * 3 + (dx + 1)
+    if (DIRECT) {
+        const int nby = (P.height + 31) >> 5;
+        for (int d = 0; d < 9; ++d) {
+            const int bx2 = bx + d % 3 - 1, by2 = by + d / 3 - 1;
+            if (d != 4 && bx2 >= 0 && bx2 < P.nbx && by2 >= 0 && by2 < nby && P.block_slot[by2 * P.nbx + bx2] >= 0)
+                nbr |= 1u << d;
+        }
+    }
+    const int cx = xt < 4 ? 0 : xt >= 32 ? 2 : 1;  // the column's band: left / none / right
 #pragma unroll
     for (int j = 0; j < kStripRows; ++j) {
         own[j] = false;
         m[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if ((DIRECT || lead) && threadIdx.x < 36 * 6) {
-            const int mx = ox + xt, my = oy + yt0 + j;  // block-array position -> master pixel
-            int sl[4];
-            own[j] = mx < mcols && my < mrows && covering_blocks(P, mx, my, sl) == 1 && sl[0] == slot;
+        if (DIRECT && threadIdx.x < 36 * 6) {
+            const int yt = yt0 + j, mx = ox + xt, my = oy + yt;  // block-array position -> master pixel
+            const int cy = yt < 4 ? 0 : yt >= 32 ? 2 : 1;
+            // neighbours whose array holds this pixel: the column band's, the row band's and their corner
+            unsigned hold = 0;
+            if (cx != 1) hold |= 1u << (4 + cx - 1);
+            if (cy != 1) hold |= 1u << ((cy - 1 + 1) * 3 + 1);
+            if (cx != 1 && cy != 1) hold |= 1u << (cy * 3 + cx);
+            own[j] = mx < mcols && my < mrows && xt < sxb + 4 && yt < syb + 4 && !(nbr & hold);
             if (DIRECT && own[j]) m[j] = fb4[(size_t)my * mcols + mx];
         }
     }
+#pragma unroll 1
     for (int k = k0; k < k1; ++k) {
         __syncthreads();  // the previous round's phase 2 is done with W (and tab / zero rows are in place)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
             float v[3] = {0.f, 0.f, 0.f}, wx[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, wy[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-            if (li[q] >= 0 && is_valid(f3(rec[q].x, rec[q].y, rec[q].z))) {  // invalid samples drop with their weight
-                const float spx = (float)(ox + lx) + rec[q].w, spy = (float)(oy + ly) + rjy[q];
+            if (li[q] >= 0 && is_valid(rec[q])) {  // invalid samples drop with their weight
+                const float spx = (float)(ox + lx) + sjx[q], spy = (float)(oy + ly) + sjy[q];
                 const float px = spx - 0.5f - (float)(ox - 2), py = spy - 0.5f - (float)(oy - 2);
                 const int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
                 const int x1 = min((int)floorf(px + r), 35), y1 = min((int)floorf(py + r), 35);
@@ -332,16 +358,8 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
                     m[j].y += rg[j].y;
                     m[j].z += bw[j].x;
                     m[j].w += bw[j].y;
-                } else if (!DIRECT && lead && own[j]) {  // the same, through the framebuffer (no registers held)
-                    float4 *mp = fb4 + (size_t)(oy + yt0 + j) * mcols + ox + xt;
-                    float4 mv = *mp;
-                    mv.x += rg[j].x;
-                    mv.y += rg[j].y;
-                    mv.z += bw[j].x;
-                    mv.w += bw[j].y;
-                    *mp = mv;
                 } else {
-                    out[(yt0 + j) * stage_pitch(36) + xt] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
+                    out[stage_off(36, 1, xt, yt0 + j)] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
                 }
             }
         }
@@ -350,6 +368,19 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
 #pragma unroll
         for (int j = 0; j < kStripRows; ++j)
             if (own[j]) fb4[(size_t)(oy + yt0 + j) * mcols + ox + xt] = m[j];
+}
+
+template <bool DIRECT, int ROUNDS = kTabRounds>
+__global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
+    __shared__ float W[kTabPlanes * kTabPlane];
+    __shared__ float tab[33];
+    if (DIRECT) {
+        tab_body<true>(P, W, tab, 0, P.n_rounds);
+        return;
+    }
+    const int k0 = blockIdx.y * ROUNDS, k1 = min(k0 + ROUNDS, P.n_rounds);
+    if (P.direct > 0 && blockIdx.y == 0) tab_body<true>(P, W, tab, k0, k1);
+    else tab_body<false>(P, W, tab, k0, k1);
 }
 
 // Fused splat + merge for the 2-pixel border: one workgroup per 32x32 tile of MASTER pixels walks the chunk's
@@ -505,18 +536,13 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(4)
         const int sx = 32 * bx - 4 + t % kRgn, sy = 32 * by - 4 + t / kRgn;
         li[q] = (t < kRgnPx && sx >= 0 && sy >= 0 && sx < P.width && sy < P.height) ? P.pixel_map[sy * P.width + sx] : -1;
     }
-    float4 rec[3];
-    float rjy[3];
+    F3 rec[3];
     auto fetch = [&](int k) {  // every slot assigned (absent: zeros), so no earlier value stays live
         const size_t rbase = (size_t)k * P.n_list;
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            rec[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-            rjy[q] = 0.f;
-            if (li[q] >= 0) {
-                rec[q] = P.rec_rgbx[rbase + li[q]];
-                rjy[q] = P.rec_jy[rbase + li[q]];
-            }
+            rec[q] = f3(0.f, 0.f, 0.f);
+            if (li[q] >= 0) rec[q] = load_rec(P.rec, rbase + li[q]);
         }
     };
 
@@ -558,8 +584,10 @@ __global__ __launch_bounds__(kTileThreads) __attribute__((amdgpu_waves_per_eu(4)
             const int sx = 32 * bx - 4 + cx, sy = 32 * by - 4 + cy;
             const int lx = sx & 31, ly = sy & 31, ox = sx - lx, oy = sy - ly;  // the sample's own block
             float v[3] = {0.f, 0.f, 0.f}, wx[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, wy[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-            if (li[q] >= 0 && is_valid(f3(rec[q].x, rec[q].y, rec[q].z))) {  // invalid samples drop with their weight
-                const float spx = (float)(ox + lx) + rec[q].w, spy = (float)(oy + ly) + rjy[q];
+            if (li[q] >= 0 && is_valid(rec[q])) {  // invalid samples drop with their weight
+                float jx, jy;
+                sample_jitter_h(splitmix64(P.seed ^ (uint64_t)(sy * P.width + sx)), (uint64_t)(P.s0 + k), jx, jy);
+                const float spx = (float)(ox + lx) + jx, spy = (float)(oy + ly) + jy;
                 const float px = spx - 0.5f - (float)(ox - 2), py = spy - 0.5f - (float)(oy - 2);
                 const int x0 = max((int)ceilf(px - r), 0), y0 = max((int)ceilf(py - r), 0);
                 const int x1 = min((int)floorf(px + r), 35), y1 = min((int)floorf(py + r), 35);
@@ -670,7 +698,7 @@ __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
     for (int q = 0; q < nb; ++q) {
         const int bid = P.blocks[slot[q]];
         const int by = bid / P.nbx, bx = bid - by * P.nbx;
-        off[q] = (my - by * 32) * pitch + (mx - bx * 32);
+        off[q] = stage_off(cols, P.band, mx - bx * 32, my - by * 32);
     }
     float4 *mp = reinterpret_cast<float4 *>(P.fb) + (size_t)my * mcols + mx;
     float4 m = *mp;
@@ -705,13 +733,10 @@ __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
 }
 
 // invalid-sample count (ImageBlock::put drops, block.cpp:94-99)
-__global__ __launch_bounds__(256) void nh_count_invalid_kernel(const float4 *rec, size_t n, unsigned long long *out) {
+__global__ __launch_bounds__(256) void nh_count_invalid_kernel(const float *rec, size_t n, unsigned long long *out) {
     size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     unsigned long long c = 0;
-    if (i < n) {
-        float4 v = rec[i];
-        c = is_valid(f3(v.x, v.y, v.z)) ? 0 : 1;
-    }
+    if (i < n) c = is_valid(load_rec(rec, i)) ? 0 : 1;
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(stat_shard(out) + 4, c);
 }
@@ -754,10 +779,11 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
     }
     SplatLaunch Q = P;
     Q.direct = 0;
+    Q.band = tabulated && P.border == 2 && P.reach == 2 ? 1 : 0;  // the layout the tab kernel writes
     if (tabulated && P.border == 2 && P.reach == 2) {
         const char *d = std::getenv("NH_SPLAT_DIRECT");  // opt-in until measured
         const bool all_direct = d && d[0] == '1';
-        const char *rv = std::getenv("NH_SPLAT_ROUNDS");  // rounds per workgroup: 1, 2, 4 (default) or 8
+        const char *rv = std::getenv("NH_SPLAT_ROUNDS");  // rounds per workgroup: 1, 2, 4 or 8 (default)
         int tr = rv ? std::atoi(rv) : kTabRounds;
         if (tr != 1 && tr != 2 && tr != 4 && tr != 8) tr = kTabRounds;  // 0 / garbage: the default (no 0 divisor)
         const char *ld = std::getenv("NH_SPLAT_LEAD");  // the first workgroup's rounds straight into the master
@@ -767,8 +793,8 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
         if (all_direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
         else if (tr == 1) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 1>), g, dim3(256), 0, st, Q);
         else if (tr == 2) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 2>), g, dim3(256), 0, st, Q);
-        else if (tr == 8) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8>), g, dim3(256), 0, st, Q);
-        else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, kTabRounds>), g, dim3(256), 0, st, Q);
+        else if (tr == 4) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 4>), g, dim3(256), 0, st, Q);
+        else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8>), g, dim3(256), 0, st, Q);
     }
     else if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
     else hipLaunchKernelGGL(nh_block_splat_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);
@@ -777,7 +803,7 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
     hipLaunchKernelGGL(nh_merge_kernel, grid, dim3(256), 0, st, Q);
 }
 
-void launch_count_invalid(const float4 *rec, size_t n, unsigned long long *out, hipStream_t st) {
+void launch_count_invalid(const float *rec, size_t n, unsigned long long *out, hipStream_t st) {
     if (n == 0) return;
     dim3 grid((unsigned)((n + 255) / 256));
     hipLaunchKernelGGL(nh_count_invalid_kernel, grid, dim3(256), 0, st, rec, n, out);
