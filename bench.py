@@ -736,8 +736,8 @@ def main():
     args = parse()
     # one hardware queue per path-pool stream: the benchmark's own configuration (the GPU box exports HIP's default
     # of 4, with which two pool streams share a queue and one pool's tail blocks another's bounces: C1 -15 %,
-    # profiles/round4_hw_queues_ab.txt). Raised before torch may initialise the HIP runtime in a multi-rank run;
-    # the line records the value. (Importing nori_hip only sets it when unset.)
+    # profiles/round4_session3_ab.txt). Raised before torch may initialise the HIP runtime in a multi-rank run (the
+    # binding raises it the same way when imported); the line records the value.
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
         os.environ["GPU_MAX_HW_QUEUES"] = "8"
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

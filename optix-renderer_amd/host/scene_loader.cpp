@@ -730,7 +730,7 @@ void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w
 // word (trunc(x) mod 2^32 for |x| < 2^63, else 0) -- stated explicitly, the C++ cast is undefined for such values
 unsigned x86_f2u(float x) { return std::fabs(x) < 0x1p63f ? (unsigned)(uint64_t)(int64_t)x : 0u; }
 
-// PNGTexture::eval (PNGTexture.cpp:125-160) / ConstantTexture::eval; eulerAngles = 0 only
+// PNGTexture::eval (PNGTexture.cpp:125-160) / ConstantTexture::eval, spherical lookups rotated by eulerAngles
 V3 env_tex_eval(const nh_envmap &e, const float *rgba, float u, float v) {
     if (e.constant) return v3(rgba[0], rgba[1], rgba[2]);
     if (e.spherical) {

@@ -23,9 +23,11 @@ LIB_PATH = os.environ.get("NH_LIB_PATH") or os.path.join(_HERE, "lib", "libnori_
 
 # The wavefront pipeline drives up to three path pools on their own streams; each needs its own hardware
 # queue, or one pool's long tail kernel blocks another's bounces (HIP's default is 4 queues per process, one
-# of which the context's own stream takes). Read once by the HIP runtime when it initialises. Set only when
-# the user or operator has not set it: an explicit value is respected.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# of which the context's own stream takes; the MI355X boxes export that 4 explicitly: C1 -15 %,
+# profiles/round4_session3_ab.txt). Read once by the HIP runtime when it initialises: raised to 8 unless a larger
+# value is set.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"nori_hip: HIP library not built ({LIB_PATH}); run `make` or __graft_entry__.build()")
