@@ -53,6 +53,7 @@ struct WfJob {
     bool ordered, stats;
     bool staged;   // splat layout, decided once when the chunk's buffers are sized (NH_SPLAT_FUSED read then only):
                    // per-(round, block) staging + merge, or the fused tile splat with no staging
+    bool jit;      // NH_SPLAT_JITTER=stored (A/B): the first vertex stores each sample's jitter for the splat
 };
 
 // A path pool: the device state one chunk needs (double-buffered path state, shadow queue, sample
@@ -65,6 +66,8 @@ struct WfPool {
     size_t cap = 0;  // paths
     float *rec = nullptr;  // (r, g, b) per sample
     size_t rec_cap = 0;
+    float2 *jit = nullptr;  // stored jitter (NH_SPLAT_JITTER=stored only)
+    size_t jit_cap = 0;
     float4 *staging = nullptr;
     size_t staging_cap = 0;
     uint32_t *spill = nullptr;
@@ -922,7 +925,7 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
 
 constexpr size_t kWfBytesPerPath = 2 * (16 * 6 + 8 + 1) + 36;  // two buffers + shadow queue
 
-static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t rec_n, size_t staging_f4) {
+static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t rec_n, size_t staging_f4, bool jit = false) {
     if (!p.stream) {  // the stream is created last: a pool with a stream has all of these
         if (!p.h_counts && hipHostMalloc(reinterpret_cast<void **>(&p.h_counts),
                                          (kRing * 2 * kCountGroup + kCountSlot) * sizeof(unsigned)) != hipSuccess) {
@@ -966,8 +969,15 @@ static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t rec_n, size_t stagi
         (void)hipFree(p.rec);
         p.rec = nullptr;
         p.rec_cap = 0;
-        HIP_TRY(c, hipMalloc(&p.rec, rec_n * 3 * sizeof(float)));
+        HIP_TRY(c, hipMalloc(&p.rec, rec_n * kRecFloats * sizeof(float)));
         p.rec_cap = rec_n;
+    }
+    if (jit && p.jit_cap < rec_n) {
+        (void)hipFree(p.jit);
+        p.jit = nullptr;
+        p.jit_cap = 0;
+        HIP_TRY(c, hipMalloc(&p.jit, rec_n * sizeof(float2)));
+        p.jit_cap = rec_n;
     }
     if (p.staging_cap < staging_f4) {
         (void)hipFree(p.staging);
@@ -982,6 +992,7 @@ static int pool_alloc(nh_ctx *c, WfPool &p, size_t n, size_t rec_n, size_t stagi
 static void pool_free(WfPool &p) {
     free_all(p.bufs);
     (void)hipFree(p.rec);
+    (void)hipFree(p.jit);
     (void)hipFree(p.staging);
     (void)hipFree(p.spill);
     if (p.h_counts) (void)hipHostFree(p.h_counts);
@@ -1053,15 +1064,17 @@ static bool tail_async_enabled() {
 static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     WfJob j = job;
     j.staged = splat_staged(c);  // the staging below is sized for this layout; the chunk's splat uses the same
+    const char *jv = std::getenv("NH_SPLAT_JITTER");
+    j.jit = jv && std::strcmp(jv, "stored") == 0;
     const int n_paths = j.rounds * c->n_list;
-    int rc = pool_alloc(c, p, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c, j.staged));
+    int rc = pool_alloc(c, p, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c, j.staged), j.jit);
     if (rc) return rc;
     // the other pools in use get the same capacity now (idle ones only: nothing of theirs is in
     // flight), so the first render call, not a later one, pays for their allocation
     for (int i = 0; i < active_pools(c); ++i) {
         WfPool &o = c->pools[i];
         if (&o == &p || o.state != WfPool::IDLE) continue;
-        if ((rc = pool_alloc(c, o, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c, j.staged))))
+        if ((rc = pool_alloc(c, o, (size_t)n_paths, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c, j.staged), j.jit)))
             return rc;
     }
     // so do the idle tail slots' record and staging buffers: chunks hand theirs over at a tail hand-off and take the
@@ -1071,7 +1084,7 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
         for (int i = kPools; i < kPools + kTails; ++i) {
             WfPool &o = c->pools[i];
             if (o.state != WfPool::IDLE) continue;
-            if ((rc = pool_alloc(c, o, (size_t)kTailCap, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c, j.staged))))
+            if ((rc = pool_alloc(c, o, (size_t)kTailCap, (size_t)n_paths, (size_t)j.rounds * c->n_blocks * block_px(c, j.staged), j.jit)))
                 return rc;
         }
     p.job = j;
@@ -1084,6 +1097,7 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     L.seed = j.seed;
     L.pixel_list = c->pixel_list;
     L.rec = p.rec;
+    L.jit = j.jit ? p.jit : nullptr;
     L.counters = c->counters;
     // scenes whose BVH fits in a few KB (the Cornell box: < 1 KB) are traversed from an LDS copy
     const size_t scene_bytes = 16 * (size_t)(c->n_node_f4 + c->n_prim_f4) + 8 * (size_t)c->n_leaves;
@@ -1191,6 +1205,8 @@ static void chunk_swap(WfPool &a, WfPool &b) {
     std::swap(a.in_s, b.in_s);
     std::swap(a.rec, b.rec);
     std::swap(a.rec_cap, b.rec_cap);
+    std::swap(a.jit, b.jit);
+    std::swap(a.jit_cap, b.jit_cap);
     std::swap(a.staging, b.staging);
     std::swap(a.staging_cap, b.staging_cap);
 }
@@ -1357,7 +1373,9 @@ static int pool_splat(nh_ctx *c, WfPool &p) {
     if (p.job.stats) nh::launch_count_invalid(p.rec, (size_t)p.L.n_paths, c->counters, p.stream);
     if (c->fb_ev_set) HIP_TRY(c, hipStreamWaitEvent(p.stream, c->fb_ev, 0));
     HIP_TRY(c, hipEventRecord(p.ev_splat0, p.stream));
-    nh::launch_splat(make_splat(c, p.rec, p.L.seed, p.L.s0, p.staging, p.job.rounds, p.job.staged), p.stream);
+    SplatLaunch sp = make_splat(c, p.rec, p.L.seed, p.L.s0, p.staging, p.job.rounds, p.job.staged);
+    sp.jit = p.L.jit;
+    nh::launch_splat(sp, p.stream);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(p.ev_splat, p.stream));
     HIP_TRY(c, hipEventRecord(c->fb_ev, p.stream));
@@ -1626,7 +1644,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     if (q->collect_stats)
         HIP_TRY(c, hipMemsetAsync(c->counters, 0, kStatShards * kStatStride * sizeof(unsigned long long), c->stream));
     const size_t per_round = (size_t)c->n_list;
-    const size_t per_round_bytes = per_round * 12 + (size_t)c->n_blocks * block_px(c, splat_staged(c)) * 16 +
+    const size_t per_round_bytes = per_round * kRecFloats * 4 + (size_t)c->n_blocks * block_px(c, splat_staged(c)) * 16 +
                                    (wavefront ? per_round * kWfBytesPerPath : 0);
     // device memory per chunk: sample records + block ImageBlocks (+ path state, per pool). Every
     // wavefront chunk ends in a tail whose length is set by its longest path (C4: ~5-7 ms of
@@ -1644,7 +1662,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
             size_t held = 0;
             for (const WfPool &p : c->pools)
-                held += p.cap * kWfBytesPerPath + p.rec_cap * 20 + p.staging_cap * sizeof(float4);
+                held += p.cap * kWfBytesPerPath + p.rec_cap * kRecFloats * 4 + p.jit_cap * 8 + p.staging_cap * sizeof(float4);
             // asynchronous tails: each tail slot also holds a whole chunk's sample records and staging (and
             // kTailCap paths of state), so it counts as one more chunk-sized share
             const int shares = active_pools(c) + (active_pools(c) > 1 && tail_async_enabled() ? kTails : 0);
@@ -1674,7 +1692,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
             c->rec = nullptr;
             c->rec_cap = 0;
             const size_t cap = (size_t)chunk * per_round;
-            HIP_TRY(c, hipMalloc(&c->rec, cap * 3 * sizeof(float)));
+            HIP_TRY(c, hipMalloc(&c->rec, cap * kRecFloats * sizeof(float)));
             c->rec_cap = cap;
         }
         const bool staged = splat_staged(c);

@@ -14,6 +14,12 @@ struct HitBatch {
     float *t, *u, *v;
     int *k;
 };
+// floats per sample record: (r, g, b), padded to 4 with NH_REC_STRIDE=4 (16-B aligned records, an A/B build)
+#ifndef NH_REC_STRIDE
+#define NH_REC_STRIDE 3
+#endif
+constexpr int kRecFloats = NH_REC_STRIDE;
+
 struct PathLaunch {
     int n_paths;            // n_rounds * n_list
     int n_list;             // pixels rendered by this context
@@ -44,6 +50,7 @@ struct SplatLaunch {
     const int *pixel_map;   // image pixel -> list entry or -1
     const int *block_rank;  // BlockGenerator spiral rank per block id
     const float *rec;       // (r, g, b) per (round, list entry)
+    const float2 *jit;      // the stored jitter per record (A/B knob), else null: recomputed
     uint64_t seed;          // the chunk's seed and first sample round: the jitter of round k's sample at pixel p is
     int s0;                 // sample_jitter(seed, p, s0 + k), the camera sample's first two draws
     float radius, lookup;
@@ -149,7 +156,8 @@ struct WfLaunch {
     int n_paths, n_list, s0;
     uint64_t seed;
     const int *pixel_list;
-    float *rec;
+    float *rec;             // (r, g, b) per (round, list entry)
+    float2 *jit;            // NH_SPLAT_JITTER=stored only: the jitter per record, written at the first vertex
     int in_q;               // buffer (and count slot) read by this bounce
     int first;              // bounce 0: paths come from the camera, not from a buffer
     unsigned *cnt_in;       // count slot of this bounce's input queues

@@ -437,9 +437,9 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
             default: li = li_path_mis<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
         }
         const size_t r = (size_t)k * L.n_list + i;
-        L.rec[3 * r] = li.x;
-        L.rec[3 * r + 1] = li.y;
-        L.rec[3 * r + 2] = li.z;
+        L.rec[kRecFloats * r] = li.x;
+        L.rec[kRecFloats * r + 1] = li.y;
+        L.rec[kRecFloats * r + 2] = li.z;
     }
     if (STATS) flush_stats(st, queries, stat_shard(L.counters));
 }

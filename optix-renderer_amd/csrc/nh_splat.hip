@@ -27,7 +27,7 @@ constexpr int kStripRows = 6;      // block-array rows one thread sums in the st
 
 // sample record r: (r, g, b)
 __device__ __forceinline__ F3 load_rec(const float *rec, size_t r) {
-    return f3(rec[3 * r], rec[3 * r + 1], rec[3 * r + 2]);
+    return f3(rec[kRecFloats * r], rec[kRecFloats * r + 1], rec[kRecFloats * r + 2]);
 }
 
 // phase 1 of the block splat: every sample's footprint (block-array box), filter position and value into LDS
@@ -116,6 +116,18 @@ __global__ __launch_bounds__(256) void nh_block_splat_kernel(SplatLaunch P) {
 // ((v * wx) * wy) products. Every pixel still sums its samples' contributions in getSampleIndices order (the
 // strip walks samples x-major), so the floats are those of nh_block_splat_kernel.
 typedef float sf2 __attribute__((ext_vector_type(2)));
+// a * (b.x, b.x) and a * (b.y, b.y) as one v_pk_mul_f32 with the half of b picked by op_sel (the compiler otherwise
+// copies a scalar operand into the low register of a pair first)
+__device__ __forceinline__ sf2 pk_mul_lo(sf2 a, sf2 b) {
+    sf2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ sf2 pk_mul_hi(sf2 a, sf2 b) {
+    sf2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __global__ __launch_bounds__(256) void nh_block_splat_strip_kernel(SplatLaunch P) {
     __shared__ SplatLds L;
     const int slot = blockIdx.x, k = blockIdx.y;
@@ -207,7 +219,9 @@ __device__ __forceinline__ int covering_blocks(const SplatLaunch &P, int mx, int
 constexpr int kTabRounds = 8;  // 8: the lead workgroups take half the rounds (fewest staged bytes, fastest)
 constexpr int kTabRow = 33;                 // plane row: lx 0..31 + a zero column (lx outside 0..31)
 constexpr int kTabPlane = 40 * kTabRow;     // rows ly = -4..35 (ly + 4): 4 zero rows either side
-constexpr int kTabV = 0, kTabWX = 3, kTabWY = 8, kTabPlanes = 13;
+// planes (kTabPlane floats each): 0-1 the (r, g) pairs, 2-3 the (b, 1) pairs -- float2 planes, so phase 2 loads
+// each packed operand whole instead of assembling it from two planes -- then 5 column and 5 row weights
+constexpr int kTabRG = 0, kTabBW = 2, kTabWX = 4, kTabWY = 9, kTabPlanes = 14;
 // DIRECT: one workgroup walks all the chunk's rounds of its block, and block-array pixels whose master pixel no
 // other rendered block covers (the block's 28x28 interior, and the master border of edge blocks) add each round's
 // value straight into the master in round order -- the merge's sum for a pixel with one covering block -- so only
@@ -227,13 +241,22 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
     const float r = P.radius;
     if (threadIdx.x < 33) tab[threadIdx.x] = P.table[threadIdx.x];
     // the zero rows and column are never written again
-    for (int i = threadIdx.x; i < kTabPlanes * 40; i += 256) {
-        const int p = i / 40, row = i - p * 40;
+    float2 *const W2 = reinterpret_cast<float2 *>(W);  // the pair planes, indexed like one float plane
+    for (int i = threadIdx.x; i < (kTabPlanes - kTabWX) * 40; i += 256) {
+        const int p = kTabWX + i / 40, row = i % 40;
         W[p * kTabPlane + row * kTabRow + 32] = 0.f;
     }
-    for (int i = threadIdx.x; i < kTabPlanes * 8 * 32; i += 256) {
-        const int p = i >> 8, q = i & 255, row = q >> 5;
+    for (int i = threadIdx.x; i < (kTabPlanes - kTabWX) * 8 * 32; i += 256) {
+        const int p = kTabWX + (i >> 8), q = i & 255, row = q >> 5;
         W[p * kTabPlane + (row < 4 ? row : row + 32) * kTabRow + (q & 31)] = 0.f;
+    }
+    for (int i = threadIdx.x; i < 2 * 40; i += 256) {  // pair planes: the zero column, then the zero rows
+        const int p = i / 40, row = i % 40;
+        W2[p * kTabPlane + row * kTabRow + 32] = make_float2(0.f, 0.f);
+    }
+    for (int i = threadIdx.x; i < 2 * 8 * 32; i += 256) {
+        const int p = i >> 8, q = i & 255, row = q >> 5;
+        W2[p * kTabPlane + (row < 4 ? row : row + 32) * kTabRow + (q & 31)] = make_float2(0.f, 0.f);
     }
     // phase-1 samples of this thread: (lx, ly) = (s & 31, s >> 5), s = threadIdx.x + 256 q (block rows are
     // consecutive list entries: neighbouring lanes load neighbouring records)
@@ -252,7 +275,15 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if (li[q] >= 0) rec[q] = load_rec(P.rec, rbase + li[q]);
-            sample_jitter_h(hs[q], (uint64_t)(P.s0 + k), sjx[q], sjy[q]);
+            if (P.jit) {  // NH_SPLAT_JITTER=stored (A/B)
+                if (li[q] >= 0) {
+                    const float2 jj = P.jit[rbase + li[q]];
+                    sjx[q] = jj.x;
+                    sjy[q] = jj.y;
+                }
+            } else {
+                sample_jitter_h(hs[q], (uint64_t)(P.s0 + k), sjx[q], sjy[q]);
+            }
         }
     };
     fetch(k0);
@@ -312,8 +343,8 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
                 v[0] = rec[q].x; v[1] = rec[q].y; v[2] = rec[q].z;
             }
             const int j = (ly + 4) * kTabRow + lx;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) W[(kTabV + c) * kTabPlane + j] = v[c];
+            W2[j] = make_float2(v[0], v[1]);
+            W2[kTabPlane + j] = make_float2(v[2], 1.0f);
 #pragma unroll
             for (int d = 0; d < 5; ++d) {
                 W[(kTabWX + d) * kTabPlane + j] = wx[d];
@@ -334,19 +365,32 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
             for (int e = 0; e < 5; ++e) {  // sample column lx = xt - 4 + e: the pixel is its column offset 4 - e
                 const int lx = xt - 4 + e;
                 const float *base = W + yt0 * kTabRow + ((unsigned)lx < 32u ? lx : 32);
+                const float2 *base2 = W2 + yt0 * kTabRow + ((unsigned)lx < 32u ? lx : 32);
 #pragma unroll
-                for (int i = 0; i < kStripRows + 4; ++i) {  // sample row ly = yt0 - 4 + i (plane row yt0 + i)
-                    const float *w = base + i * kTabRow;
-                    const float wx = w[(kTabWX + 4 - e) * kTabPlane];
-                    const sf2 vrg = sf2{w[(kTabV + 0) * kTabPlane], w[(kTabV + 1) * kTabPlane]} * wx;
-                    const sf2 vbw = sf2{w[(kTabV + 2) * kTabPlane], 1.0f} * wx;
+                for (int i0 = 0; i0 < kStripRows + 4; i0 += 2) {  // sample rows i0, i0 + 1 (ly = yt0 - 4 + i)
+                    // each row weight of the two rows as one register pair (rows i0 and i0+1 of its plane): the
+                    // products take it with the half selected in the instruction (pk_mul_lo / pk_mul_hi)
+                    sf2 wyp[5];
 #pragma unroll
-                    for (int dy = 0; dy < 5; ++dy) {  // row offset dy of the sample: strip row i - 4 + dy
-                        const int j = i - 4 + dy;
-                        if (j < 0 || j >= kStripRows) continue;
-                        const float wy = w[(kTabWY + dy) * kTabPlane];
-                        rg[j] += vrg * wy;
-                        bw[j] += vbw * wy;
+                    for (int dy = 0; dy < 5; ++dy) {
+                        const float *w = base + i0 * kTabRow + (kTabWY + dy) * kTabPlane;
+                        wyp[dy] = sf2{w[0], w[kTabRow]};
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int i = i0 + h;  // sample row ly = yt0 - 4 + i (plane row yt0 + i)
+                        const float *w = base + i * kTabRow;
+                        const float wx = w[(kTabWX + 4 - e) * kTabPlane];
+                        const float2 prg = base2[i * kTabRow], pbw = base2[kTabPlane + i * kTabRow];
+                        const sf2 vrg = sf2{prg.x, prg.y} * wx;
+                        const sf2 vbw = sf2{pbw.x, pbw.y} * wx;
+#pragma unroll
+                        for (int dy = 0; dy < 5; ++dy) {  // row offset dy of the sample: strip row i - 4 + dy
+                            const int j = i - 4 + dy;
+                            if (j < 0 || j >= kStripRows) continue;
+                            rg[j] += h ? pk_mul_hi(vrg, wyp[dy]) : pk_mul_lo(vrg, wyp[dy]);
+                            bw[j] += h ? pk_mul_hi(vbw, wyp[dy]) : pk_mul_lo(vbw, wyp[dy]);
+                        }
                     }
                 }
             }

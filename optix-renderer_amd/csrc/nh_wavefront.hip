@@ -723,7 +723,7 @@ __device__ __forceinline__ PathV path_of(const WfLaunch &L, const PState &o) {
 }
 
 __device__ __forceinline__ void write_radiance(const WfLaunch &L, const PathV &v) {
-    float *r = L.rec + 3 * (size_t)v.pid;
+    float *r = L.rec + kRecFloats * (size_t)v.pid;
     r[0] = v.li.x;
     r[1] = v.li.y;
     r[2] = v.li.z;
@@ -744,6 +744,7 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
         th4 = make_float4(1.f, 1.f, 1.f, 0.f);  // throughput, w_ems
         v.flags = F_FIRST;
         v.pid = s;
+        if (L.jit) L.jit[s] = make_float2(jx, jy);
     } else {
         src.load(ro, rd, li4, th4, v.rng.state);
         const int bits = __float_as_int(rd.w);
@@ -1040,6 +1041,7 @@ __device__ __forceinline__ bool first_vertex(const DScene &S, const Traversal &t
     float4 ro, rd;
     float jx, jy;
     camera_sample(S, L, s, v.rng, ro, rd, jx, jy);
+    if (L.jit) L.jit[s] = make_float2(jx, jy);
     v.org = xyz(ro);
     v.d = xyz(rd);
     v.li = f3(0.f, 0.f, 0.f);
