@@ -70,6 +70,8 @@ def parse():
                         "a fixed image (C4 2048^2 unless --config) and --rounds x --steps spp split by blocks")
     p.add_argument("--strong-spp", type=int, default=256,
                    help="spp of the strong_c4 sub-record (fixed 2048^2 C4 image split over the ranks; 0 = skip)")
+    p.add_argument("--hw-queues", type=int, default=0,
+                   help="GPU_MAX_HW_QUEUES for this run (A/B; default: at least 8)")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the N=1 megakernel and denoiser_test sub-records")
     p.add_argument("--traversal-1m-steps", type=int, default=4,
@@ -738,7 +740,10 @@ def main():
     # of 4, with which two pool streams share a queue and one pool's tail blocks another's bounces: C1 -15 %,
     # profiles/round4_session3_ab.txt). Raised before torch may initialise the HIP runtime in a multi-rank run (the
     # binding raises it the same way when imported); the line records the value.
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
+        os.environ["NH_KEEP_HW_QUEUES"] = "1"
+    elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
         os.environ["GPU_MAX_HW_QUEUES"] = "8"
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))

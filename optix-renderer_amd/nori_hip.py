@@ -26,7 +26,7 @@ LIB_PATH = os.environ.get("NH_LIB_PATH") or os.path.join(_HERE, "lib", "libnori_
 # of which the context's own stream takes; the MI355X boxes export that 4 explicitly: C1 -15 %,
 # profiles/round4_session3_ab.txt). Read once by the HIP runtime when it initialises: raised to 8 unless a larger
 # value is set.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8 and not os.environ.get("NH_KEEP_HW_QUEUES"):
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 if not os.path.exists(LIB_PATH):

@@ -10,7 +10,7 @@ for i in $(seq 1 $n); do
   for v in $variants; do
     name=${v%%:*}; knob=""; [ "$v" != "$name" ] && knob=$(echo "${v#*:}" | tr ',' ' ')
     b=bench.py; [ $name != cur ] && b=ab/$name/bench.py
-    tag=$(echo "${cfg}_$v" | tr ':=,' '___')
+    tag=$(echo "${cfg}_$v" | tr ':=,/.' '_____')
     extra=""; [ $name = cur ] && extra="--strong-spp 0 --no-extras"
     env $knob timeout -k 10 300 python $b --config $cfg --steps 4 --warmup 1 --no-cpu --no-denoise --traversal-1m-steps 0 \
       $extra "$@" > gpurun_out/ab_$tag$i.log 2>&1 || { echo "fail $v$i"; tail -5 gpurun_out/ab_$tag$i.log; exit 99; }
