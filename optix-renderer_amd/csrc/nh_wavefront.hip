@@ -1494,12 +1494,14 @@ void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L
 }
 
 void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
-                       hipStream_t st) {
+                       bool specular, hipStream_t st) {
     const char *e = std::getenv("NH_TAIL_WG");  // threads per tail workgroup: 64 (default) or 256
     const int tb = e && std::atoi(e) == 256 ? 256 : 64;
-    // register budget: 1 wave/SIMD (default; profiles/round4_session4_ab.txt: shorter tails on C1 and C4) or 4
+    // register budget, NH_TAIL_RR_WAVES=1|4: by default 1 wave/SIMD for scenes with mirror / dielectric BSDFs (their
+    // long chains: shorter tails on C1 and C4, profiles/round4_session4_ab.txt) and 4 otherwise (a short tail that
+    // leaves the next chunk's bounce kernels their occupancy: C2 +0.5 %, profiles/round4_session11_12_c2_ab.txt)
     const char *w = std::getenv("NH_TAIL_RR_WAVES");
-    const bool w1 = !(w && std::atoi(w) == 4);
+    const bool w1 = w ? std::atoi(w) == 1 : specular;
     const char *cp = std::getenv("NH_TAIL_COOP");  // lanes per path once <= 4 remain in a wave: 16 (default) or 1
     const int coop = cp && std::atoi(cp) == 1 ? 1 : 16;
     // one path per lane: the grid covers the bound (tail bounds are <= kTailCap paths)
