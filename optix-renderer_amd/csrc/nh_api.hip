@@ -1119,10 +1119,12 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     // unless the reference's own visit order was asked for
     p.wide = p.persistent && j.ordered && c->tv.wnodes != nullptr;
     if (const char *e = std::getenv("NH_WIDE")) p.wide = p.wide && e[0] != '0';
-    // both queries of a bounce in one persistent launch (one tail per bounce instead of two); NH_TRACE2=0: the
-    // closest-hit and any-hit launches of round 3
-    p.trace2 = p.wide;
-    if (const char *e = std::getenv("NH_TRACE2")) p.trace2 = p.trace2 && e[0] != '0';
+    // both queries of a bounce in one persistent launch (one tail per bounce instead of two) while the tree fits in
+    // the 256 MB MALL (perf-1M +10 %, C3 +7 %); past it the two queries' node sets compete for the cache in one
+    // grid (C5, 0.8 GB: 22.3 GB of HBM traffic per fused launch vs 6.9 + 12.3 GB split, 15 % slower), so the
+    // closest-hit and any-hit launches stay separate. NH_TRACE2=0|1 overrides.
+    p.trace2 = p.wide && scene_bytes <= (size_t)256 << 20;
+    if (const char *e = std::getenv("NH_TRACE2")) p.trace2 = p.wide && e[0] != '0';
     c->stats.trace_fused = p.trace2 ? 1 : 0;
     // spill words per lane: binary entries are one word, wide entries two (8-B aligned)
     const int spill_words = p.wide ? 2 * c->depth_wide : (c->depth + 1) / 2 * 2;
