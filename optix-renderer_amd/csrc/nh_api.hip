@@ -1646,7 +1646,9 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     if (q->collect_stats)
         HIP_TRY(c, hipMemsetAsync(c->counters, 0, kStatShards * kStatStride * sizeof(unsigned long long), c->stream));
     const size_t per_round = (size_t)c->n_list;
-    const size_t per_round_bytes = per_round * kRecFloats * 4 + (size_t)c->n_blocks * block_px(c, splat_staged(c)) * 16 +
+    const char *jv = std::getenv("NH_SPLAT_JITTER");  // stored jitter (A/B): 8 more bytes per sample record
+    const size_t rec_bytes = kRecFloats * 4 + (wavefront && jv && std::strcmp(jv, "stored") == 0 ? 8 : 0);
+    const size_t per_round_bytes = per_round * rec_bytes + (size_t)c->n_blocks * block_px(c, splat_staged(c)) * 16 +
                                    (wavefront ? per_round * kWfBytesPerPath : 0);
     // device memory per chunk: sample records + block ImageBlocks (+ path state, per pool). Every
     // wavefront chunk ends in a tail whose length is set by its longest path (C4: ~5-7 ms of
