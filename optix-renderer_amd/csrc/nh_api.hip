@@ -1290,7 +1290,7 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
             p.state = WfPool::SPLAT;
             return NH_OK;
         }
-        if (p.rr) nh::launch_wf_bounce_rr(c->d_scene, c->tv, L, ordered, stats, p.sorted, bound, p.stream);
+        if (p.rr) nh::launch_wf_bounce_rr(c->d_scene, c->tv, L, ordered, stats, p.sorted, c->specular, bound, p.stream);
         else nh::launch_wf_bounce(c->d_scene, c->tv, L, ordered, stats, p.sorted, bound, p.stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], p.stream));

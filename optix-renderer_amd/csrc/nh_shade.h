@@ -129,7 +129,9 @@ __device__ __noinline__ F3 tex_eval(const DTex *texs, const float4 *texels, int 
 }
 // the diffuse albedo of BSDF b at uv: its constant colour unless it has a texture
 __device__ __forceinline__ F3 bsdf_albedo(const DScene &S, const DBsdf &b, float u, float v) {
+#ifndef NH_AB_NO_TEX  // cost attribution builds only (scripts/build_variant.sh): textures compiled out
     if (__builtin_expect(b.tex != 0, 0)) return tex_eval(S.texs, S.texels, b.tex - 1, u, v);
+#endif
     return f3(b.ar, b.ag, b.ab);
 }
 

@@ -496,11 +496,13 @@ NHD bool iso_sphere_hit(const Traversal &tv, int k_prev, F3 o, F3 d, float mint,
 }
 
 // trace (closest hit) of a path's next ray from the surface of primitive k_prev, with the isolated-sphere answer
-template <int DEPTH, bool ORDERED, bool STATS, bool PAIRS = false, int G = 1>
+template <int DEPTH, bool ORDERED, bool STATS, bool PAIRS = false, int G = 1, bool ISO = true>
 NHD bool trace_next(const Traversal &tv, const DScene &S, int k_prev, F3 o, F3 d, float mint, float maxt, Hit &best,
                     uint32_t *stk, int stride, TravStats &st) {
-    if (S.iso_spheres && S.root_kind != 0 && iso_sphere_hit<STATS, G>(tv, k_prev, o, d, mint, maxt, best, st))
+#ifndef NH_AB_NO_ISO  // cost attribution builds only: the isolated-sphere test compiled out
+    if (ISO && S.iso_spheres && S.root_kind != 0 && iso_sphere_hit<STATS, G>(tv, k_prev, o, d, mint, maxt, best, st))
         return true;
+#endif
     return trace<DEPTH, ORDERED, false, STATS, PAIRS, G>(tv, S, o, d, mint, maxt, best, stk, stride, st);
 }
 
