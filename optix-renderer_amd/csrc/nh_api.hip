@@ -140,6 +140,7 @@ struct nh_ctx {
     std::vector<int> shape_bsdf_type;  // BSDF type of each shape (material key of the sorted queues)
     int n_bsdf_types = 0;              // distinct BSDF types in the scene
     bool specular = false;             // a mirror or dielectric BSDF: long discrete chains, long chunk tails
+    bool textured = false;             // a BSDF with an albedo texture
     float *fb = nullptr;
     size_t fb_floats = 0;
     float *rec = nullptr;  // (r, g, b) per sample
@@ -492,6 +493,8 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     }
     c->n_bsdf_types = __builtin_popcount(types);
     c->specular = (types & ((1u << NH_BSDF_MIRROR) | (1u << NH_BSDF_DIELECTRIC))) != 0;
+    c->textured = false;  // any BSDF with an albedo texture (wf_bounce_rr's lean instantiation has no lookup)
+    for (uint32_t i = 0; i < d->n_bsdfs; ++i) c->textured = c->textured || d->bsdfs[i].albedo_texture != 0;
     c->V.assign(d->V, d->V + 3 * nv);
     c->F.assign(d->F, d->F + 3 * (size_t)d->n_faces);
     c->width = d->camera.width;
@@ -1290,7 +1293,8 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
             p.state = WfPool::SPLAT;
             return NH_OK;
         }
-        if (p.rr) nh::launch_wf_bounce_rr(c->d_scene, c->tv, L, ordered, stats, p.sorted, c->specular, bound, p.stream);
+        if (p.rr) nh::launch_wf_bounce_rr(c->d_scene, c->tv, L, ordered, stats, p.sorted, !c->specular && !c->textured, bound,
+                                          p.stream);
         else nh::launch_wf_bounce(c->d_scene, c->tv, L, ordered, stats, p.sorted, bound, p.stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], p.stream));

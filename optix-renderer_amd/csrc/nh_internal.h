@@ -190,8 +190,7 @@ void launch_wf_bounce(const nhd::DScene *S, const nhd::Traversal &tv, const WfLa
 // RR-ahead variants of the fused bounce / tail (nh_wavefront.hip): the stored state is a path after its
 // vertex's Russian roulette
 void launch_wf_bounce_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
-                        bool specular,
-                         int bound, hipStream_t st);
+                         bool lean, int bound, hipStream_t st);
 void launch_wf_tail_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
                        bool specular, hipStream_t st);
 void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,

@@ -612,15 +612,15 @@ __device__ __forceinline__ bool shade_head(const DScene &S, const Traversal &tv,
 // The body of a shade step for a path that survived its head (path_mis.cpp:73-146 / path_mats.cpp:58-76):
 // NEE sample (path_mis), BSDF sample, this bounce's MIS-weighted light term and t *= bsdf weight. Writes the
 // path's next state to o; nee = a light sample whose shadow ray (so, sd) decides o.pe (F_NEE).
-// SKIP = false: the light sample is always computed (the skip below compiled out; rr_step also drops the
-// isolated-sphere test): scenes without mirror / dielectric BSDFs, whose bounce kernel is 1 % faster without them
-// (profiles/round4_session14_c2_ab.txt)
-template <bool SKIP = true>
+// FULL = false (scenes with no mirror / dielectric BSDF and no albedo texture): the light-sample skip and the texture
+// lookup compiled out (rr_step also drops the isolated-sphere test) -- their branches cost C2's bounce kernel ~1 %
+// though they never fire there (profiles/round4_session14_c2_ab.txt, round4_session15_c2_ab.txt)
+template <bool FULL = true>
 __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv, PathV &v, const Its &its, PState &o,
                                            bool &nee, float4 &so, float4 &sd) {
     const DShape shape = S.shapes[its.shape];
     const DBsdf bsdf = S.bsdfs[shape.bsdf];
-    const F3 alb = bsdf_albedo(S, bsdf, its.u, its.v);
+    const F3 alb = FULL ? bsdf_albedo(S, bsdf, its.u, its.v) : f3(bsdf.ar, bsdf.ag, bsdf.ab);
     nee = false;
     if (S.integrator == 1) {  // path_mats: BSDF sample only
         const float bx = v.rng.next1d(), by = v.rng.next1d();
@@ -647,7 +647,7 @@ __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv,
         // finite radiance, every light's box apart from every discrete-BSDF shape's, so the sampled point is never
         // the shading point) rules out a non-finite light sample, and t is checked here: then it is not computed.
 #ifndef NH_AB_NO_NEE_SKIP  // cost attribution builds only: every light sample computed
-        const bool skip_nee = SKIP && discrete && S.nee_finite && isfinite(v.t.x) && isfinite(v.t.y) && isfinite(v.t.z);
+        const bool skip_nee = FULL && discrete && S.nee_finite && isfinite(v.t.x) && isfinite(v.t.y) && isfinite(v.t.z);
 #else
         const bool skip_nee = false;
 #endif
@@ -1079,7 +1079,7 @@ struct TailClocks {
 // body of the current vertex, its light sample's any-hit query, the next ray's closest hit, and the next
 // vertex's head; false once the path has ended (its radiance written). G > 1: the path is carried by a G-lane
 // group (every lane the same state and arithmetic; leaf primitives tested cooperatively; one lane writes and counts).
-template <bool ORDERED, bool STATS, bool CLK = false, int G = 1, bool SKIP = true>
+template <bool ORDERED, bool STATS, bool CLK = false, int G = 1, bool FULL = true>
 __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, const WfLaunch &L, PathV &v, Its &its,
                                         Hit &h, uint32_t *stk, int stride, TravStats &st_e, TravStats &st_s,
                                         unsigned long long &q_e, unsigned long long &q_s, TailClocks *clk = nullptr) {
@@ -1090,7 +1090,7 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     unsigned long long t0 = 0, t1 = 0;
     unsigned long long *cs = CLK ? (G > 1 ? clk->cc : clk->c) : nullptr;
     if constexpr (CLK) t0 = clock64();
-    shade_body<SKIP>(S, tv, v, its, o, nee, so, sd);
+    shade_body<FULL>(S, tv, v, its, o, nee, so, sd);
     if constexpr (CLK) {
         t1 = clock64();
         if (lead) cs[0] += t1 - t0;
@@ -1118,7 +1118,7 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     }
     const bool live = o.rd.w >= o.ro.w;
     if (lead) q_e += live ? 1 : 0;
-    const bool found = live && trace_next<16, ORDERED, STATS, true, G, SKIP>(tv, S, h.k, xyz(o.ro), xyz(o.rd), o.ro.w,
+    const bool found = live && trace_next<16, ORDERED, STATS, true, G, FULL>(tv, S, h.k, xyz(o.ro), xyz(o.rd), o.ro.w,
                                                                       o.rd.w, h, stk, stride, st_e);
     if constexpr (CLK) {
         t1 = clock64();
@@ -1138,7 +1138,7 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     return true;
 }
 
-template <bool ORDERED, bool STATS, bool SORT, bool SKIP = true>
+template <bool ORDERED, bool STATS, bool SORT, bool FULL = true>
 __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScene *__restrict__ Sp, Traversal tv_g,
                                                                      WfLaunch L) {
     __shared__ uint32_t stk[16 * 256];
@@ -1165,7 +1165,7 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScen
         bool alive = true;
         if (L.first) alive = first_vertex<ORDERED, STATS>(S, tv, L, s, v, h, its, my_stk, 256, st_e, q_e);
         else load_post_head(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
-        if (alive) cont = rr_step<ORDERED, STATS, false, 1, SKIP>(S, tv, L, v, its, h, my_stk, 256, st_e, st_s, q_e, q_s);
+        if (alive) cont = rr_step<ORDERED, STATS, false, 1, FULL>(S, tv, L, v, its, h, my_stk, 256, st_e, st_s, q_e, q_s);
         if (cont) cls = prim_material(tv.prims[3 * h.k + 2]);  // a live path's ray has hit something
     }
     int rank = 0;  // survivors ranked by the material class of their hit (sorted queue) or in lane order
@@ -1486,13 +1486,13 @@ void launch_wf_bounce(const DScene *S, const Traversal &tv, const WfLaunch &L, b
 }
 
 void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
-                         bool specular, int bound, hipStream_t st) {
+                         bool lean, int bound, hipStream_t st) {
     int blocks = std::max(1, (bound + 255) / 256);
     blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
     const size_t lds = 16 * (size_t)rr_lds_f4(L);
 #define NH_FB(O, T, SO) hipLaunchKernelGGL((wf_bounce_rr<O, T, SO>), dim3(blocks), dim3(256), lds, st, S, tv, L)
 #define NH_FBN(T, SO) hipLaunchKernelGGL((wf_bounce_rr<true, T, SO, false>), dim3(blocks), dim3(256), lds, st, S, tv, L)
-    if (ordered && !specular) {  // no discrete BSDF: the light-sample skip compiled out
+    if (ordered && lean) {  // no discrete BSDF, no texture: wf_bounce_rr<.., FULL = false>
         if (stats) { if (sort) NH_FBN(true, true); else NH_FBN(true, false); }
         else { if (sort) NH_FBN(false, true); else NH_FBN(false, false); }
     } else if (ordered) {
