@@ -614,7 +614,7 @@ __device__ __forceinline__ bool shade_head(const DScene &S, const Traversal &tv,
 // path's next state to o; nee = a light sample whose shadow ray (so, sd) decides o.pe (F_NEE).
 // FULL = false (scenes with no mirror / dielectric BSDF and no albedo texture): the light-sample skip and the texture
 // lookup compiled out (rr_step also drops the isolated-sphere test) -- their branches cost C2's bounce kernel ~1 %
-// though they never fire there (profiles/round4_session14_c2_ab.txt, round4_session15_c2_ab.txt)
+// though they never fire there (profiles/round4_session14_16_c2_ab.txt)
 template <bool FULL = true>
 __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv, PathV &v, const Its &its, PState &o,
                                            bool &nee, float4 &so, float4 &sd) {
