@@ -231,7 +231,9 @@ constexpr int kTabRG = 0, kTabBW = 2, kTabWX = 4, kTabWY = 9, kTabPlanes = 14;
 // workgroup of each block (rounds 0 .. ROUNDS-1: they come first in the merge's order, which starts those pixels at
 // round P.direct). A separate inlined body per mode keeps the staged-only workgroups at their own register count.
 // (A read-modify-write of the framebuffer per round instead of the registers was built and spills past 256 VGPRs.)
-template <bool DIRECT>
+// JIT: the jitter read from P.jit (NH_SPLAT_JITTER=stored) instead of recomputed -- a template parameter: a runtime
+// choice between the two costs the recomputing kernel 6 % (profiles/round4_session9_10_splat_ab.txt)
+template <bool DIRECT, bool JIT = false>
 __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *tab, int k0, int k1) {
     const int slot = blockIdx.x;
     const int bid = P.blocks[slot];
@@ -275,7 +277,7 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if (li[q] >= 0) rec[q] = load_rec(P.rec, rbase + li[q]);
-            if (P.jit) {  // NH_SPLAT_JITTER=stored (A/B)
+            if (JIT) {  // NH_SPLAT_JITTER=stored (A/B)
                 if (li[q] >= 0) {
                     const float2 jj = P.jit[rbase + li[q]];
                     sjx[q] = jj.x;
@@ -414,17 +416,17 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
             if (own[j]) fb4[(size_t)(oy + yt0 + j) * mcols + ox + xt] = m[j];
 }
 
-template <bool DIRECT, int ROUNDS = kTabRounds>
+template <bool DIRECT, int ROUNDS = kTabRounds, bool JIT = false>
 __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
     __shared__ float W[kTabPlanes * kTabPlane];
     __shared__ float tab[33];
     if (DIRECT) {
-        tab_body<true>(P, W, tab, 0, P.n_rounds);
+        tab_body<true, JIT>(P, W, tab, 0, P.n_rounds);
         return;
     }
     const int k0 = blockIdx.y * ROUNDS, k1 = min(k0 + ROUNDS, P.n_rounds);
-    if (P.direct > 0 && blockIdx.y == 0) tab_body<true>(P, W, tab, k0, k1);
-    else tab_body<false>(P, W, tab, k0, k1);
+    if (P.direct > 0 && blockIdx.y == 0) tab_body<true, JIT>(P, W, tab, k0, k1);
+    else tab_body<false, JIT>(P, W, tab, k0, k1);
 }
 
 // Fused splat + merge for the 2-pixel border: one workgroup per 32x32 tile of MASTER pixels walks the chunk's
@@ -830,11 +832,16 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
         const char *rv = std::getenv("NH_SPLAT_ROUNDS");  // rounds per workgroup: 1, 2, 4 or 8 (default)
         int tr = rv ? std::atoi(rv) : kTabRounds;
         if (tr != 1 && tr != 2 && tr != 4 && tr != 8) tr = kTabRounds;  // 0 / garbage: the default (no 0 divisor)
+        if (P.jit) tr = 8;  // stored jitter (A/B): the default grouping only
         const char *ld = std::getenv("NH_SPLAT_LEAD");  // the first workgroup's rounds straight into the master
         const bool lead = !(ld && ld[0] == '0');
         Q.direct = all_direct ? P.n_rounds : lead ? std::min(tr, P.n_rounds) : 0;
         const dim3 g(P.n_blocks, (P.n_rounds + tr - 1) / tr);
-        if (all_direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
+        if (P.jit) {
+            if (all_direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true, 8, true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
+            else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8, true>), g, dim3(256), 0, st, Q);
+        }
+        else if (all_direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
         else if (tr == 1) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 1>), g, dim3(256), 0, st, Q);
         else if (tr == 2) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 2>), g, dim3(256), 0, st, Q);
         else if (tr == 4) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 4>), g, dim3(256), 0, st, Q);
