@@ -64,6 +64,7 @@ struct SplatLaunch {
                             // Fixed when the chunk's staging was sized, so a knob change mid-pipeline cannot
                             // mismatch the two
     int direct;             // rounds the tab splat added to fb for pixels one block covers (the merge starts them there)
+    int persist;            // tab splat: a grid of this many workgroups walks the items (0: one workgroup per item)
     int band;               // staging offsets: stage_off(.., band, ..) (1: the tabulated splat's core + band layout)
     int debug;              // timing experiments only (NH_SPLAT_DEBUG, images wrong): bits skip the fused splat's
                             // phase 1 (1), phase 2 (2), record fetch (4), master-border strips (8)

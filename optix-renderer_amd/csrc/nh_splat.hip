@@ -234,8 +234,7 @@ constexpr int kTabRG = 0, kTabBW = 2, kTabWX = 4, kTabWY = 9, kTabPlanes = 14;
 // JIT: the jitter read from P.jit (NH_SPLAT_JITTER=stored) instead of recomputed -- a template parameter: a runtime
 // choice between the two costs the recomputing kernel 6 % (profiles/round4_session9_10_splat_ab.txt)
 template <bool DIRECT, bool JIT = false>
-__device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *tab, int k0, int k1) {
-    const int slot = blockIdx.x;
+__device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *tab, int slot, int k0, int k1) {
     const int bid = P.blocks[slot];
     const int by = bid / P.nbx, bx = bid - by * P.nbx;
     const int ox = bx * 32, oy = by * 32;
@@ -416,17 +415,31 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
             if (own[j]) fb4[(size_t)(oy + yt0 + j) * mcols + ox + xt] = m[j];
 }
 
-template <bool DIRECT, int ROUNDS = kTabRounds, bool JIT = false>
+template <bool DIRECT, int ROUNDS = kTabRounds, bool JIT = false, bool PERSIST = false>
 __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
     __shared__ float W[kTabPlanes * kTabPlane];
     __shared__ float tab[33];
     if (DIRECT) {
-        tab_body<true, JIT>(P, W, tab, 0, P.n_rounds);
+        tab_body<true, JIT>(P, W, tab, blockIdx.x, 0, P.n_rounds);
         return;
     }
-    const int k0 = blockIdx.y * ROUNDS, k1 = min(k0 + ROUNDS, P.n_rounds);
-    if (P.direct > 0 && blockIdx.y == 0) tab_body<true, JIT>(P, W, tab, k0, k1);
-    else tab_body<false, JIT>(P, W, tab, k0, k1);
+    if (!PERSIST) {
+        const int k0 = blockIdx.y * ROUNDS, k1 = min(k0 + ROUNDS, P.n_rounds);
+        if (P.direct > 0 && blockIdx.y == 0) tab_body<true, JIT>(P, W, tab, blockIdx.x, k0, k1);
+        else tab_body<false, JIT>(P, W, tab, blockIdx.x, k0, k1);
+        return;
+    }
+    // PERSIST: a grid of P.persist workgroups walks the (block, round group) items, so the splat holds the LDS of
+    // fewer CUs while the other pool's bounce kernels run beside it (A/B knob NH_SPLAT_WGS)
+    const int groups = (P.n_rounds + ROUNDS - 1) / ROUNDS, n_items = P.n_blocks * groups;
+#pragma unroll 1
+    for (int v = blockIdx.x; v < n_items; v += gridDim.x) {
+        const int slot = v % P.n_blocks, grp = v / P.n_blocks;
+        __syncthreads();  // the previous item's sums are done with W before it is set up again
+        const int k0 = grp * ROUNDS, k1 = min(k0 + ROUNDS, P.n_rounds);
+        if (P.direct > 0 && grp == 0) tab_body<true, JIT>(P, W, tab, slot, k0, k1);
+        else tab_body<false, JIT>(P, W, tab, slot, k0, k1);
+    }
 }
 
 // Fused splat + merge for the 2-pixel border: one workgroup per 32x32 tile of MASTER pixels walks the chunk's
@@ -836,7 +849,11 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
         const char *ld = std::getenv("NH_SPLAT_LEAD");  // the first workgroup's rounds straight into the master
         const bool lead = !(ld && ld[0] == '0');
         Q.direct = all_direct ? P.n_rounds : lead ? std::min(tr, P.n_rounds) : 0;
-        const dim3 g(P.n_blocks, (P.n_rounds + tr - 1) / tr);
+        dim3 g(P.n_blocks, (P.n_rounds + tr - 1) / tr);
+        const char *pw = std::getenv("NH_SPLAT_WGS");  // persistent splat grid (A/B): workgroups, 0 = one per item
+        Q.persist = pw ? std::max(0, std::atoi(pw)) : 0;
+        if (all_direct || tr != 8 || P.jit) Q.persist = 0;  // the persistent grid: default grouping only
+        if (Q.persist) g = dim3(std::min<unsigned>((unsigned)Q.persist, g.x * g.y), 1);
         if (P.jit) {
             if (all_direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true, 8, true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
             else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8, true>), g, dim3(256), 0, st, Q);
@@ -845,6 +862,7 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
         else if (tr == 1) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 1>), g, dim3(256), 0, st, Q);
         else if (tr == 2) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 2>), g, dim3(256), 0, st, Q);
         else if (tr == 4) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 4>), g, dim3(256), 0, st, Q);
+        else if (Q.persist) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8, false, true>), g, dim3(256), 0, st, Q);
         else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8>), g, dim3(256), 0, st, Q);
     }
     else if (strip) hipLaunchKernelGGL(nh_block_splat_strip_kernel, dim3(P.n_blocks, P.n_rounds), dim3(256), 0, st, P);

@@ -221,7 +221,8 @@ def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, 
     order, no staging) and the staged pair -- its first workgroup per block adding its rounds of the pixels only that
     block covers straight into the master (default, at 1 / 4 / 8 rounds per workgroup), every workgroup staging
     (NH_SPLAT_LEAD=0), one workgroup per block taking all rounds of those pixels (NH_SPLAT_DIRECT=1), the jitter read
-    from a per-record array instead of recomputed from the path stream (NH_SPLAT_JITTER=stored) -- give the same
+    from a per-record array instead of recomputed from the path stream (NH_SPLAT_JITTER=stored), a persistent grid of
+    3 workgroups walking the items (NH_SPLAT_WGS=3) -- give the same
     framebuffer bit for bit, and the oracle's: partial blocks and the master border of the last block column / row
     (100x70, 33x31), block subsets whose neighbours are absent (every tile quadrant case), several chunks (1 MiB path
     budget) and both render modes."""
@@ -231,9 +232,11 @@ def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, 
     b = nh.Bvh(s)
     out = {}
     variants = ({"NH_SPLAT_DIRECT": "1"}, {"NH_SPLAT_LEAD": "0"}, {}, {"NH_SPLAT_ROUNDS": "4"},
-                {"NH_SPLAT_ROUNDS": "1"}, {"NH_SPLAT_FUSED": "1"}, {"NH_SPLAT_JITTER": "stored"})
+                {"NH_SPLAT_ROUNDS": "1"}, {"NH_SPLAT_FUSED": "1"}, {"NH_SPLAT_JITTER": "stored"},
+                {"NH_SPLAT_WGS": "3"})
     for env in variants:
-        for name in ("NH_SPLAT_DIRECT", "NH_SPLAT_LEAD", "NH_SPLAT_ROUNDS", "NH_SPLAT_FUSED", "NH_SPLAT_JITTER"):
+        for name in ("NH_SPLAT_DIRECT", "NH_SPLAT_LEAD", "NH_SPLAT_ROUNDS", "NH_SPLAT_FUSED", "NH_SPLAT_JITTER",
+                     "NH_SPLAT_WGS"):
             monkeypatch.delenv(name, raising=False)
         for name, val in env.items():
             monkeypatch.setenv(name, val)
