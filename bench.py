@@ -52,6 +52,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "optix-renderer_amd"))
+from nh_env import parse_hw_queues, raise_hw_queues  # noqa: E402  (loads no library)
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 NODE_BYTES, PRIM_BYTES, RECORD_BYTES = 64, 48, 20
@@ -743,8 +744,8 @@ def main():
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
         os.environ["NH_KEEP_HW_QUEUES"] = "1"
-    elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    else:
+        raise_hw_queues()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -817,7 +818,7 @@ def main():
                        "width": W, "height": H, "spp": spp, "rounds_per_step": R,
                        "mode": args.mode, "traversal": args.traversal,
                        "pools": r["pools"] or None,
-                       "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0),
+                       "gpu_max_hw_queues": parse_hw_queues(os.environ.get("GPU_MAX_HW_QUEUES")),
                        "parallelism": (f"{par} + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce"
                                        if world > 1 else "single GPU"),
                        "bvh_build_s": round(r["bvh_s"], 3), "upload_s": round(r["upload_s"], 3),

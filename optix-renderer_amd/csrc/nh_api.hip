@@ -295,6 +295,7 @@ void nh_destroy(nh_ctx *c) {
 // shape with a discrete BSDF (so the sampled point p and the shading point ref always differ: a zero distance is the
 // only way the area light's pdf becomes 0/0, emitter_pdf). Then the wavefront shade may skip the light sample of a
 // discrete BSDF sample, which is zeroed by the reference anyway (path_mis.cpp:136-140).
+// A non-constant envmap also needs a finite, positive luminance normalization.
 static bool nee_finite(const nh_scene_desc *d) {
     auto fin = [](float x) { return std::fabs(x) < 1e15f; };
     for (uint32_t i = 0; i < d->n_emitters; ++i) {
@@ -306,6 +307,10 @@ static bool nee_finite(const nh_scene_desc *d) {
     if (d->envmap >= 0 && d->env.constant && d->env.rgba)
         for (int k = 0; k < 3; ++k)
             if (!std::isfinite(d->env.rgba[k])) return false;
+    // a PNG envmap's luminance table must be a proper distribution: an all-black image leaves its normalization
+    // 1/0, and the reference's light sample is then NaN, which ImageBlock drops with the whole sample
+    if (d->envmap >= 0 && !d->env.constant && !(std::isfinite(d->env.normalization) && d->env.normalization > 0.f))
+        return false;
     struct Box { float lo[3], hi[3]; };
     auto widened = [&](const nh_shape &s, Box &b) {
         float ext = 0.f;
@@ -527,7 +532,47 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
 // real scenes (the Cornell box's spheres clear its floor by 6e-3). Boxes are compared in double, closed: a box
 // that touches or holds a NaN is not apart. NH_ISO_SPHERE=0 leaves every sphere unmarked (every ray walks the
 // tree). Spheres x primitives box tests, skipped (no marks) past 2e8. Returns the number marked.
-static int mark_isolated_spheres(std::vector<float4> &prims) {
+// Primitives whose box meets the query box [qlo, qhi] (double): a walk of the uploaded binary tree (child boxes in
+// the parent, float) with the query grown by `slack` at the node tests, so a node box that rounds inward of its
+// primitives' double boxes cannot hide one; the primitive boxes themselves decide (was a linear scan of
+// every primitive per dielectric sphere).
+static void prims_near_box(const std::vector<float4> &nodes, const std::vector<int2> &leaves, int root_kind,
+                           const double qlo[3], const double qhi[3], double slack, std::vector<uint32_t> &out) {
+    out.clear();
+    auto leaf = [&](int l) {
+        const int2 lf = leaves[(size_t)l];
+        for (int k = 0; k < lf.y; ++k) out.push_back((uint32_t)(lf.x + k));
+    };
+    if (root_kind == 2) leaf(0);
+    if (root_kind != 1) return;
+    auto meets = [&](const float lo[3], const float hi[3]) {
+        for (int a = 0; a < 3; ++a)
+            if ((double)hi[a] < qlo[a] - slack || (double)lo[a] > qhi[a] + slack) return false;
+        return true;
+    };
+    std::vector<int> st{0};
+    while (!st.empty()) {
+        const int g = st.back();
+        st.pop_back();
+        const float4 *n = &nodes[4 * (size_t)g];
+        const float llo[3] = {n[0].x, n[0].y, n[0].z}, lhi[3] = {n[0].w, n[1].x, n[1].y};
+        const float rlo[3] = {n[1].z, n[1].w, n[2].x}, rhi[3] = {n[2].y, n[2].z, n[2].w};
+        int4 r4;
+        std::memcpy(&r4, &n[3], sizeof(int4));
+        const int ref[2] = {r4.x, r4.y};
+        const bool hit[2] = {meets(llo, lhi), meets(rlo, rhi)};
+        for (int ch = 0; ch < 2; ++ch)
+            if (hit[ch]) {
+                if (ref[ch] >= 0) st.push_back(ref[ch]);
+                else leaf(~ref[ch]);
+            }
+    }
+}
+
+// Marks dielectric spheres whose box, grown by 2m (m = 1e-4 of the scene extent), is apart from every other
+// primitive's box (the isolated-sphere closest hit of nh_traverse.h `trace_next`); m goes into the record.
+static int mark_isolated_spheres(std::vector<float4> &prims, const std::vector<float4> &nodes,
+                                 const std::vector<int2> &leaves, int root_kind) {
     const char *e = std::getenv("NH_ISO_SPHERE");
     if (e && e[0] == '0') return 0;
     const size_t n = prims.size() / 3;
@@ -537,32 +582,46 @@ static int mark_isolated_spheres(std::vector<float4> &prims) {
         std::memcpy(&bits, &prims[3 * k + 2].w, 4);
         if ((bits & nhd::kPrimSphere) && ((bits >> nhd::kPrimMatShift) & 3) == nhd::BSDF_DIELECTRIC) sph.push_back(k);
     }
-    if (sph.empty() || (double)sph.size() * (double)n > 2e8) return 0;
-    std::vector<double> lo(3 * n), hi(3 * n);
-    double slo[3] = {INFINITY, INFINITY, INFINITY}, shi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (size_t k = 0; k < n; ++k) {
+    if (sph.empty()) return 0;
+    auto prim_box = [&](size_t k, double lo[3], double hi[3]) {
         const float4 *p = &prims[3 * k];
         int bits;
         std::memcpy(&bits, &p[2].w, 4);
         for (int a = 0; a < 3; ++a) {
             const double v0 = a == 0 ? p[0].x : a == 1 ? p[0].y : p[0].z;
             if (bits & nhd::kPrimSphere) {
-                lo[3 * k + a] = v0 - (double)p[0].w;
-                hi[3 * k + a] = v0 + (double)p[0].w;
+                lo[a] = v0 - (double)p[0].w;
+                hi[a] = v0 + (double)p[0].w;
             } else {
                 const double v1 = a == 0 ? p[1].x : a == 1 ? p[1].y : p[1].z;
                 const double v2 = a == 0 ? p[2].x : a == 1 ? p[2].y : p[2].z;
-                lo[3 * k + a] = std::min(v0, std::min(v1, v2));
-                hi[3 * k + a] = std::max(v0, std::max(v1, v2));
+                lo[a] = std::min(v0, std::min(v1, v2));
+                hi[a] = std::max(v0, std::max(v1, v2));
             }
-            slo[a] = std::min(slo[a], lo[3 * k + a]);
-            shi[a] = std::max(shi[a], hi[3 * k + a]);
         }
+    };
+    // the scene extent from the root box (the union of every primitive's float box)
+    double ext = 0.0, mag = 0.0;
+    if (root_kind == 0) return 0;
+    {
+        double slo[3] = {INFINITY, INFINITY, INFINITY}, shi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t k = 0; k < n; ++k) {
+            double lo[3], hi[3];
+            prim_box(k, lo, hi);
+            for (int a = 0; a < 3; ++a) {
+                slo[a] = std::min(slo[a], lo[a]);
+                shi[a] = std::max(shi[a], hi[a]);
+            }
+        }
+        ext = std::max(shi[0] - slo[0], std::max(shi[1] - slo[1], shi[2] - slo[2]));
+        for (int a = 0; a < 3; ++a) mag = std::max(mag, std::max(std::fabs(slo[a]), std::fabs(shi[a])));
     }
-    const double ext = std::max(shi[0] - slo[0], std::max(shi[1] - slo[1], shi[2] - slo[2]));
     if (!(ext > 0.0) || !std::isfinite(ext)) return 0;
     const float m = (float)(1e-4 * ext);
+    // far above the float rounding (2^-24 relative) of any node box coordinate in the scene
+    const double slack = 1e-6 * (ext + mag);
     int marked = 0;
+    std::vector<uint32_t> near;
     for (size_t s : sph) {
         const float4 a = prims[3 * s];
         if (!(a.w > 0.f) || !std::isfinite(a.w) || !std::isfinite(a.x) || !std::isfinite(a.y) || !std::isfinite(a.z))
@@ -570,13 +629,18 @@ static int mark_isolated_spheres(std::vector<float4> &prims) {
         const double g = (double)a.w + 2.0 * (double)m;
         const double glo[3] = {(double)a.x - g, (double)a.y - g, (double)a.z - g};
         const double ghi[3] = {(double)a.x + g, (double)a.y + g, (double)a.z + g};
+        prims_near_box(nodes, leaves, root_kind, glo, ghi, slack, near);
         bool apart = true;
-        for (size_t k = 0; k < n && apart; ++k) {
+        for (uint32_t k : near) {
             if (k == s) continue;
+            double lo[3], hi[3];
+            prim_box(k, lo, hi);
             bool sep = false;
-            for (int ax = 0; ax < 3; ++ax)
-                sep = sep || hi[3 * k + ax] < glo[ax] || lo[3 * k + ax] > ghi[ax];
-            apart = sep;
+            for (int ax = 0; ax < 3; ++ax) sep = sep || hi[ax] < glo[ax] || lo[ax] > ghi[ax];
+            if (!sep) {
+                apart = false;
+                break;
+            }
         }
         if (!apart) continue;
         int bits;
@@ -804,7 +868,7 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
             p[2] = make_float4(p2[0], p2[1], p2[2], f0);
         }
     }
-    S.iso_spheres = mark_isolated_spheres(prims);
+    S.iso_spheres = mark_isolated_spheres(prims, nodes, leaves, S.root_kind);
     // leaf-end bits: the 4-wide traversal walks a leaf's records until this bit
     for (const int2 &lf : leaves)
         if (lf.y > 0) {

@@ -108,7 +108,6 @@ inline void pre_affine(Mat4 &t, const Mat4 &a) {
     t = o;
 }
 
-// parser.cpp:343-359: columns left, newUp, dir, origin
 // PNGTexture's spherical-lookup rotation (PNGTexture.cpp:28, :133-139):
 //   eulerAngles = degrees * M_PI / 180.f;
 //   rot = Quaternionf(Identity * AngleAxisf(e.x, UnitZ) * AngleAxisf(e.y, UnitX)) * AngleAxisf(e.z, UnitZ).toRotationMatrix()
@@ -159,6 +158,7 @@ inline void png_rotation(Vec3 deg, float out[9]) {
         for (int j = 0; j < 3; ++j) out[3 * i + j] = dot3(a[i][0], a[i][1], a[i][2], b[0][j], b[1][j], b[2][j]);
 }
 
+// parser.cpp:343-359: columns left, newUp, dir, origin
 inline Mat4 lookat_matrix(Vec3 origin, Vec3 target, Vec3 up) {
     const Vec3 dir = normalized({target.x - origin.x, target.y - origin.y, target.z - origin.z});
     const Vec3 left = normalized(cross(normalized(up), dir));

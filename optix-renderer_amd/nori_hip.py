@@ -21,13 +21,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NH_LIB_PATH: an alternative in-tree build, for A/B measurements in one GPU session
 LIB_PATH = os.environ.get("NH_LIB_PATH") or os.path.join(_HERE, "lib", "libnori_hip.so")
 
-# The wavefront pipeline drives up to three path pools on their own streams; each needs its own hardware
-# queue, or one pool's long tail kernel blocks another's bounces (HIP's default is 4 queues per process, one
-# of which the context's own stream takes; the MI355X boxes export that 4 explicitly: C1 -15 %,
-# profiles/round4_session3_ab.txt). Read once by the HIP runtime when it initialises: raised to 8 unless a larger
-# value is set.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8 and not os.environ.get("NH_KEEP_HW_QUEUES"):
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# One hardware queue per path-pool stream (nh_env.py): raised to 8 before the library's first HIP call unless a
+# larger value is set or NH_KEEP_HW_QUEUES keeps the caller's.
+from nh_env import raise_hw_queues  # noqa: E402  (nori_hip's own directory is on sys.path)
+
+raise_hw_queues()
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"nori_hip: HIP library not built ({LIB_PATH}); run `make` or __graft_entry__.build()")

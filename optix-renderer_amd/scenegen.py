@@ -215,17 +215,18 @@ def sky_image(width: int, height: int, seed: int = 7) -> np.ndarray:
 
 def envmap_xml(out_dir: str, width: int = 64, height: int = 48, spp: int = 16, texture: str = "png",
                tex_size=(96, 48), spherical: bool = True, area_light: bool = True, integrator: str = "path_mis",
-               mesh: str | None = None, euler=None) -> str:
+               mesh: str | None = None, euler=None, black: bool = False) -> str:
     """Open scene lit by an envmap (+ optionally a small area light): a ground quad, a diffuse
     and a microfacet sphere, a mirror sphere. texture: png | constant | none (EnvMap's 0.5
     fallback). mesh: optional OBJ path added with a diffuse BSDF. euler: the png_texture's eulerAngles
-    (degrees) of the spherical lookup."""
+    (degrees) of the spherical lookup. black: an all-black PNG (its luminance table sums to 0)."""
     os.makedirs(out_dir, exist_ok=True)
     tex_xml = ""
     if texture == "png":
-        png = os.path.join(out_dir, f"sky_{tex_size[0]}x{tex_size[1]}.png")
+        png = os.path.join(out_dir, f"{'black' if black else 'sky'}_{tex_size[0]}x{tex_size[1]}.png")
         if not os.path.exists(png):
-            write_png(png, sky_image(*tex_size))
+            img = sky_image(*tex_size)
+            write_png(png, np.zeros_like(img) if black else img)
         tex_xml = f"""<texture type="png_texture" name="albedo">
       <string name="filename" value="{os.path.basename(png)}"/>
       <boolean name="sphericalTexture" value="{'true' if spherical else 'false'}"/>
@@ -272,7 +273,7 @@ def envmap_xml(out_dir: str, width: int = 64, height: int = 48, spp: int = 16, t
   {extra}
 </scene>
 """
-    key = repr((width, height, spp, texture, tex_size, spherical, area_light, integrator, mesh, euler)).encode()
+    key = repr((width, height, spp, texture, tex_size, spherical, area_light, integrator, mesh, euler, black)).encode()
     dst = os.path.join(out_dir, f"envmap_{hashlib.sha1(key).hexdigest()[:10]}.xml")
     with open(dst, "w") as f:
         f.write(text)

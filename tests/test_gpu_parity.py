@@ -300,6 +300,17 @@ def test_render_parity_envmap(gpu, tmp_path, texture, integrator, mode):
     assert nh.to_rgb(r, s.border).mean() > 0.05
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_render_parity_black_envmap_mirror(gpu, tmp_path, mode):
+    """An all-black PNG envmap (luminance table sums to 0: DiscretePDF's normalization 0) beside an area light and a
+    mirror sphere. The reference's envmap light sample is then non-finite, so the light-sample skip at mirror hits
+    must stay off (nee_finite); GPU vs oracle bit for bit. Parity unpinned (no reference output)."""
+    xml = scenegen.envmap_xml(str(tmp_path), texture="png", tex_size=(32, 16), black=True)
+    g, r, s = render_pair(xml, 64, 48, 8, mode=mode, traversal=nh.TRAVERSAL_ORDERED)
+    np.testing.assert_array_equal(g, r)
+    assert np.isfinite(g).all()
+
+
 @pytest.mark.parametrize("knob", ["NH_PERSISTENT=1", "NH_PERSISTENT=1,NH_WIDE=0", "NH_PERSISTENT=0",
                                   "NH_LDS_SCENE=0", "NH_TAIL=0", "NH_TAIL=1000000", "NH_PERSISTENT=1,NH_TAIL=1000000",
                                   "NH_FUSED=0", "NH_SORT=0", "NH_SORT=1", "NH_FUSED=1,NH_TAIL=0",
