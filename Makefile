@@ -22,10 +22,13 @@ HIP_FLAGS  := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) $(FP_FLAGS) \
 
 HOST_SRC := $(PKG)/host/xml_lite.cpp $(PKG)/host/scene_loader.cpp $(PKG)/host/bvh_build.cpp $(PKG)/host/image_io.cpp \
             $(PKG)/host/png_decode.cpp
-HIP_SRC  := $(PKG)/csrc/nh_kernels.hip $(PKG)/csrc/nh_wavefront.hip $(PKG)/csrc/nh_denoise.hip $(PKG)/csrc/nh_splat.hip \
-            $(PKG)/csrc/nh_api.hip
+HIP_SRC  := $(PKG)/csrc/nh_kernels.hip $(PKG)/csrc/nh_denoise.hip $(PKG)/csrc/nh_splat.hip $(PKG)/csrc/nh_api.hip
 HOST_OBJ := $(patsubst $(PKG)/host/%.cpp,$(OBJDIR)/host_%.o,$(HOST_SRC))
-HIP_OBJ  := $(patsubst $(PKG)/csrc/%.hip,$(OBJDIR)/hip_%.o,$(HIP_SRC))
+# nh_wavefront.hip is compiled as four translation units (-DNH_WF_PART=k, each instantiating its own kernels) so
+# its kernels build in parallel
+WF_PARTS := 0 1 2 3
+HIP_OBJ  := $(patsubst $(PKG)/csrc/%.hip,$(OBJDIR)/hip_%.o,$(HIP_SRC)) \
+            $(foreach k,$(WF_PARTS),$(OBJDIR)/hip_nh_wavefront_p$(k).o)
 HIP_DEPS := $(wildcard $(PKG)/csrc/*.h) include/nori_hip.h
 
 LIB      := $(LIBDIR)/libnori_hip.so
@@ -60,6 +63,10 @@ $(VALUBENCH): tools/valu_issue.hip
 $(OBJDIR)/host_%.o: $(PKG)/host/%.cpp $(wildcard $(PKG)/host/*.h) include/nori_hip.h
 	@mkdir -p $(OBJDIR)
 	$(CXX) $(HOST_FLAGS) -c $< -o $@
+
+$(OBJDIR)/hip_nh_wavefront_p%.o: $(PKG)/csrc/nh_wavefront.hip $(HIP_DEPS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIP_FLAGS) -DNH_WF_PART=$* -c $< -o $@
 
 $(OBJDIR)/hip_%.o: $(PKG)/csrc/%.hip $(HIP_DEPS)
 	@mkdir -p $(OBJDIR)

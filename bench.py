@@ -40,6 +40,8 @@ The JSON line also carries:
   denoiser_test (N=1) scenes/project/denoiser/denoiser-test.xml (800x600, checkerboard floor, curvy bowl, two area
                 lights) as the reference's report times it (reports/project-report/denoising.html:79-81): 1024 spp
                 ground truth ("5 minutes"), 16 spp ("roughly 20 seconds") + SimpleDenoiser ("about one second")
+  project_scenes (N=1) the reference's envmap scene (envmap_sphere.xml, 800x800, 128 spp) and its two thin-lens
+                scenes (dof-val.xml, table_path_mis.xml) at their own sizes and sample counts
 """
 import argparse
 import json
@@ -74,7 +76,7 @@ def parse():
     p.add_argument("--hw-queues", type=int, default=0,
                    help="GPU_MAX_HW_QUEUES for this run (A/B; default: at least 8)")
     p.add_argument("--no-extras", action="store_true",
-                   help="skip the N=1 megakernel and denoiser_test sub-records")
+                   help="skip the N=1 megakernel, denoiser_test and project_scenes sub-records")
     p.add_argument("--traversal-1m-steps", type=int, default=4,
                    help="N=1: also time the perf-1M traversal kernel (0 = skip)")
     p.add_argument("--width", type=int, default=None)
@@ -155,6 +157,19 @@ def pmc_record(workload_key):
         return json.load(open(path)).get(workload_key) or {}
     except (OSError, ValueError):
         return {}
+
+
+_LIB_SHA = {}
+
+
+def lib_sha16():
+    """The build identity PMC records are checked against: the first 16 hex digits of the SHA-256 of the library
+    this process loaded (scripts/pmc_traffic.py records the same for the library its passes loaded)."""
+    import nori_hip as nh
+    if nh.LIB_PATH not in _LIB_SHA:
+        import hashlib
+        _LIB_SHA[nh.LIB_PATH] = hashlib.sha256(open(nh.LIB_PATH, "rb").read()).hexdigest()[:16]
+    return _LIB_SHA[nh.LIB_PATH]
 
 
 def stage_work(calib):
@@ -251,6 +266,8 @@ def roofline(args, calib, st, W, H, R):
             r["accounting_error"] = "global-memory GB/s above the HBM peak"
         srec = pmc_record(f"{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}/{k}") \
             if int(os.environ.get("WORLD_SIZE", "1")) == 1 else {}
+        if srec.get("lib_sha16") != lib_sha16():
+            srec = {}  # another build's counters
         if srec.get("hbm_bytes_per_launch"):  # measured HBM bytes of this stage's kernel (committed PMC passes)
             r["measured_hbm_bytes_per_launch"] = srec["hbm_bytes_per_launch"]
             r["measured_hbm_gbs"] = round(srec["hbm_bytes_per_launch"] / (avg * 1e-3) / 1e9, 1)
@@ -270,14 +287,20 @@ def roofline(args, calib, st, W, H, R):
     key = f"{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}/{dom}"
     single = int(os.environ.get("WORLD_SIZE", "1")) == 1
     rec = pmc_record(key) if single else {}
-    if rec and rec.get("kernel", "").split("<")[0] != kernel.split(" ")[0]:
-        rec = {}  # the committed counters are for another kernel of this workload
+    stale = None
+    if rec and rec.get("lib_sha16") != lib_sha16():
+        # counters of another build (or of another kernel instantiation): not this run's kernel, not reported
+        stale = (f"the committed record ({rec.get('kernel', '?')}) is from library build {rec.get('lib_sha16')}, "
+                 f"this run loaded {lib_sha16()}: not used")
+        rec = {}
     traffic = rec.get("hbm_bytes_per_launch")
     achieved = d["global_gbs"]
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "traffic_source": (f"profiles/pmc_traffic.json[{key}]: {rec.get('source', '')}" if traffic else
-                               "not collected for this workload (rocprofv3 PMC runs separately)"),
+            "traffic_source": (f"profiles/pmc_traffic.json[{key}]: {rec.get('source', '')}; kernel "
+                               f"{rec.get('kernel')}, library build {rec.get('lib_sha16')}" if traffic else
+                               stale or "not collected for this workload (rocprofv3 PMC runs separately)"),
+            "lib_sha16": lib_sha16(),
             "kernel": kernel, "avg_launch_ms": d["avg_launch_ms"], "launches": d["launches"],
             "algorithmic_bytes_per_launch": d["global_bytes_per_launch"],
             "bytes_per_sample": round(stages[dom]["hbm_bytes"] / paths, 1), "node_bytes": node_b,
@@ -471,11 +494,15 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
     for s in range(steps):
         ctx.render(s * R, (s + 1) * R, seed=a.seed, blocks=blocks, traversal=trav, clear=False, mode=mode)
     reduced = None
+    ranks = None
     if dist is not None:
+        ctx.synchronize()  # (the reduce waits for every chunk anyway): the render time of this rank alone
+        t_render = time.perf_counter() - t_start
         reduced = reduce_framebuffer(ctx, dist, args, local, rank)
     ctx.synchronize()
     elapsed = time.perf_counter() - t_start
     if dist is not None:
+        ranks = rank_breakdown(dist, args, local, t_render, elapsed - t_render, ctx.stats()["launches_splat"])
         elapsed = max_over_ranks(elapsed, dist, args, local)
     if args.dump_framebuffer and rank == 0:
         np.save(args.dump_framebuffer, reduced if reduced is not None else ctx.framebuffer())
@@ -508,7 +535,7 @@ def run_workload(nh, args, config, steps, warmup, local, blocks=None, world=1, r
         roof["timed"] = roof_pass or "the timed region"
     return {"scene": scene, "W": W, "H": H, "R": R, "desc": scene_desc, "elapsed": elapsed, "samples": samples,
             "roof": roof, "bvh_s": bvh_s, "upload_s": upload_s, "ctx": ctx, "chunks": chunks,
-            "pools": pools}
+            "pools": pools, "ranks": ranks}
 
 
 def reduce_framebuffer(ctx, dist, args, local, rank):
@@ -516,15 +543,40 @@ def reduce_framebuffer(ctx, dist, args, local, rank):
     (gloo) reduce, None otherwise (RCCL reduces in place into rank 0's device framebuffer)."""
     import torch
     ptr, n = ctx.framebuffer_device_ptr()  # completes every submitted chunk first
-    if args.dist_backend == "nccl":
-        fb = _wrap_device(ptr, n, local)
+    try:
+        if args.dist_backend == "nccl":
+            fb = _wrap_device(ptr, n, local)
+            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+            torch.cuda.synchronize()
+            return None
+        host = ctx.framebuffer()
+        fb = torch.from_numpy(host.reshape(-1))
         dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
-        torch.cuda.synchronize()
-        return None
-    host = ctx.framebuffer()
-    fb = torch.from_numpy(host.reshape(-1))
-    dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+    except Exception as e:  # the RCCL (or gloo) error, then a non-zero exit: no retry
+        print(f"bench: rank {rank}: framebuffer reduce ({args.dist_backend}) failed: {e!r}", file=sys.stderr,
+              flush=True)
+        sys.exit(3)
     return host if rank == 0 else None
+
+
+def rank_breakdown(dist, args, local, render_s, reduce_s, chunks):
+    """Per-rank diagnosis of an N-rank timing (verdict r4 item 7): every rank's render time (its nh_render calls
+    until its last chunk is done), the framebuffer reduce alone, and its chunk count, gathered to every rank.
+    render + reduce = the rank's timed region; the line's time is the max over ranks of that sum."""
+    import torch
+    dev = f"cuda:{local}" if args.dist_backend == "nccl" else "cpu"
+    mine = torch.tensor([render_s, reduce_s, float(chunks)], dtype=torch.float64, device=dev)
+    rows = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(rows, mine)
+    rows = [r.cpu().tolist() for r in rows]
+    render = [r[0] for r in rows]
+    reduce = [r[1] for r in rows]
+    total = [a + b for a, b in zip(render, reduce)]
+    return {"render_s": [round(x, 6) for x in render], "reduce_s": [round(x, 6) for x in reduce],
+            "total_s": [round(x, 6) for x in total], "chunks": [int(r[2]) for r in rows],
+            "render_s_min": round(min(render), 6), "render_s_max": round(max(render), 6),
+            "reduce_s_max": round(max(reduce), 6),
+            "render_imbalance": round(max(render) / min(render), 4) if min(render) > 0 else None}
 
 
 def max_over_ranks(elapsed, dist, args, local):
@@ -630,13 +682,17 @@ def strong_c4_record(nh, args, world, rank, local, dist):
         dist.barrier()
     t0 = time.perf_counter()
     ctx.render(0, spp, seed=args.seed, blocks=blocks, traversal=trav, clear=False, mode=nh.MODE_WAVEFRONT)
+    ranks = None
     if dist is not None:
+        ctx.synchronize()
+        t_render = time.perf_counter() - t0
         reduce_framebuffer(ctx, dist, args, local, rank)
     ctx.synchronize()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        elapsed = max_over_ranks(elapsed, dist, args, local)
     st = ctx.stats()
+    if dist is not None:
+        ranks = rank_breakdown(dist, args, local, t_render, elapsed - t_render, st["launches_splat"])
+        elapsed = max_over_ranks(elapsed, dist, args, local)
     ctx.close()
     samples = W * H * spp
     return {"workload": f"{desc}, {spp} spp, path_mis (fixed image, BASELINE configs[3])", "n_gpus": world,
@@ -644,7 +700,8 @@ def strong_c4_record(nh, args, world, rank, local, dist):
             "msamples_s": round(samples / elapsed / 1e6, 3), "scaling": "strong",
             "partition": f"32x32 blocks round-robin over {world} rank(s), one nh_render call each"
                          + (f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} reduce" if world > 1 else ""),
-            "chunks_rank0": int(st["launches_splat"]), "pools_rank0": int(st.get("pools_active", 0))}
+            "chunks_rank0": int(st["launches_splat"]), "pools_rank0": int(st.get("pools_active", 0)),
+            "ranks": ranks}
 
 
 def megakernel_record(nh, args, local):
@@ -703,6 +760,35 @@ def denoiser_test_record(nh, local):
             "speedup_groundtruth": round(pub_gt / t_gt, 1)}
 
 
+def project_scenes_record(nh, local):
+    """The reference's own project scenes at their own resolution and sample count (tests/golden/project_scenes.json.gz),
+    one warm render then one timed render each: the envmap scene (envmap_sphere.xml, the shipped wooden_motel.png,
+    800x800, 128 spp) and the two thin-lens scenes (dof-val.xml 800x400 256 spp, table_path_mis.xml 800x600 512 spp:
+    lens samples in the serial render order, nh_shade.h lens_uniform)."""
+    import scenegen
+    d = scenegen.materialize(tempfile.mkdtemp(prefix="nh_proj_"))
+    out = {}
+    for key, rel in (("envmap_sphere", "scenes/project/envmap/envmap_sphere.xml"),
+                     ("dof_val", "scenes/project/dof/dof-val.xml"),
+                     ("dof_table", "scenes/project/dof/table_path_mis.xml")):
+        scene = nh.Scene(os.path.join(d, rel))
+        W, H, spp = scene.width, scene.height, scene.spp
+        bvh = nh.Bvh(scene, n_threads=16)
+        ctx = nh.Context(local)
+        ctx.upload(scene, bvh)
+        trav, mode = nh.TRAVERSAL_ORDERED, nh.MODE_WAVEFRONT
+        ctx.render(0, spp, seed=1, traversal=trav, clear=True, mode=mode)
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        ctx.render(0, spp, seed=2, traversal=trav, clear=True, mode=mode)
+        ctx.synchronize()
+        t = time.perf_counter() - t0
+        ctx.close()
+        out[key] = {"scene": rel, "image": f"{W}x{H}", "spp": spp, "s": round(t, 4),
+                    "msamples_s": round(W * H * spp / t / 1e6, 3)}
+    return out
+
+
 def free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -759,12 +845,17 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            local = 0  # rehearsal: every rank on GPU 0
-            dist.init_process_group("gloo")
+        try:
+            if args.dist_backend == "nccl":
+                torch.cuda.set_device(local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                local = 0  # rehearsal: every rank on GPU 0
+                dist.init_process_group("gloo")
+        except Exception as e:  # no retry, no re-exec: the run fails with the backend's own error
+            print(f"bench: rank {rank}: init_process_group({args.dist_backend}) failed: {e!r}", file=sys.stderr,
+                  flush=True)
+            sys.exit(3)
     import nori_hip as nh
 
     if args.scaling == "strong" and args.config == "c2" and not args.config_given:
@@ -790,12 +881,13 @@ def main():
         if world == 1 and args.traversal_1m_steps > 0 and args.config != "bumpy1m":
             r["ctx"].close()
             t1m = traversal_1m(nh, args, local)
-        mk = dn_scene = None
+        mk = dn_scene = proj = None
         if world == 1 and not args.no_extras:
             r["ctx"].close()
             if args.mode == "wavefront":
                 mk = megakernel_record(nh, args, local)
             dn_scene = denoiser_test_record(nh, local)
+            proj = project_scenes_record(nh, local)
         spp = R * args.steps
         if args.scaling == "strong":
             par = f"tile-shard x{world}, strong scaling: fixed {W}x{H} image, {spp} spp split by blocks"
@@ -823,6 +915,7 @@ def main():
                                        if world > 1 else "single GPU"),
                        "bvh_build_s": round(r["bvh_s"], 3), "upload_s": round(r["upload_s"], 3),
                        "timed_chunks": r["chunks"]},
+            "ranks": r["ranks"],
             "roofline": roof,
             "traversal": traversal_record(roof) if roof else None,
             "traversal_1m": t1m,
@@ -831,6 +924,7 @@ def main():
             "strong_c4": strong,
             "megakernel": mk,
             "denoiser_test": dn_scene,
+            "project_scenes": proj,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

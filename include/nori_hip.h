@@ -133,6 +133,9 @@ typedef struct nh_camera {
     float camera_to_world[16];
     float inv_output_size[2];
     float near_clip, far_clip;
+    /* after cloneAndInit's fstop <-> lensRadius coupling (perspective.cpp:37-42). lens_radius > 1e-4 (Epsilon):
+       thin lens (perspective.cpp:114-130); camera ray k of the serial render order (round, BlockGenerator
+       spiral, x-major pixels) takes draws 2k, 2k+1 of a default-state pcg32 -- the reference's static sampler */
     float lens_radius, focal_distance;
 } nh_camera;
 

@@ -229,6 +229,25 @@ std::vector<int> spiral_rank(int w, int h, int bs, int &nbx, int &nby) {
     return rank;
 }
 
+// The position of each pixel's camera ray within one sample round of the reference's serial render order: blocks
+// in BlockGenerator order (edge blocks clipped, block.cpp:174-176), then Independent::getSampleIndices' x-major
+// pixel order (independent.cpp:85-99: x outer, y inner)
+std::vector<uint32_t> serial_ray_index(int w, int h, int bs) {
+    int nbx = 0, nby = 0;
+    const std::vector<int> rank = spiral_rank(w, h, bs, nbx, nby);
+    std::vector<int> by_rank(rank.size());
+    for (size_t b = 0; b < rank.size(); ++b) by_rank[(size_t)rank[b]] = (int)b;
+    std::vector<uint32_t> idx((size_t)w * h);
+    uint32_t k = 0;
+    for (int b : by_rank) {
+        const int ox = (b % nbx) * bs, oy = (b / nbx) * bs;
+        const int sx = std::min(bs, w - ox), sy = std::min(bs, h - oy);
+        for (int x = 0; x < sx; ++x)
+            for (int y = 0; y < sy; ++y) idx[(size_t)(oy + y) * w + (ox + x)] = k++;
+    }
+    return idx;
+}
+
 }  // namespace
 
 extern "C" {
@@ -350,8 +369,6 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     if (int rc_ = pipeline_drain(c)) return rc_;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (d->camera.width <= 0 || d->camera.height <= 0) return fail(c, "invalid camera resolution"), NH_ERR_INVALID;
-    if (d->camera.lens_radius > 1e-4f)
-        return fail(c, "depth of field is not supported (reference uses a shared static sampler)"), NH_ERR_UNSUPPORTED;
     if (d->envmap >= 0) {
         const nh_envmap &e = d->env;
         if ((uint32_t)d->envmap >= d->n_emitters || d->emitters[d->envmap].type != NH_EMITTER_ENVMAP)
@@ -483,6 +500,18 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     S.far_clip = d->camera.far_clip;
     S.width = d->camera.width;
     S.height = d->camera.height;
+    // depth of field (perspective.cpp:114: lensRadius > Epsilon): each pixel's camera-ray position within a sample
+    // round of the serial render order, which places its lens sample in the camera's static pcg32 stream
+    // (nh_shade.h lens_uniform)
+    S.dof = d->camera.lens_radius > 1e-4f ? 1 : 0;
+    S.lens_radius = d->camera.lens_radius;
+    S.focal_distance = d->camera.focal_distance;
+    S.lens_index = nullptr;
+    std::vector<uint32_t> lens_index;
+    if (S.dof) {
+        lens_index = serial_ray_index(S.width, S.height, 32);
+        if ((rc = upload(c, c->scene_bufs, lens_index.data(), lens_index.size(), &S.lens_index))) return rc;
+    }
     S.filter_radius = d->filter.radius;
     S.lookup = d->filter.lookup_factor;
     S.border = d->filter.border;

@@ -103,6 +103,22 @@ struct Rng {
     }
     NHD float next1d() { return __uint_as_float((next_uint() >> 9) | 0x3f800000u) - 1.0f; }
 };
+// pcg32() default state and stream (pcg32.h:29-30, :40) and pcg32::advance (pcg32.h:131-150): Brown's
+// arbitrary-stride jump, O(log delta)
+constexpr uint64_t kPcgDefaultState = 0x853c49e6748fea9bULL, kPcgDefaultStream = 0xda3e39cb94b95bdbULL;
+NHD uint64_t pcg_advance(uint64_t state, uint64_t inc, uint64_t delta) {
+    uint64_t cur_mult = kPcgMult, cur_plus = inc, acc_mult = 1u, acc_plus = 0u;
+    while (delta > 0) {
+        if (delta & 1) {
+            acc_mult *= cur_mult;
+            acc_plus = acc_plus * cur_mult + cur_plus;
+        }
+        cur_plus = (cur_mult + 1) * cur_plus;
+        cur_mult *= cur_mult;
+        delta /= 2;
+    }
+    return acc_mult * state + acc_plus;
+}
 NHD uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -198,6 +214,11 @@ struct DScene {
     float s2c[16], c2w[16];
     float inv_w, inv_h, near_clip, far_clip;
     int width, height;
+    // depth of field (perspective.cpp:114-130), on when lensRadius > Epsilon: lens_index[pixel] = the position of the
+    // pixel's camera ray within one sample round of the serial render order (spiral blocks, x-major pixels)
+    int dof;
+    float lens_radius, focal_distance;
+    const uint32_t *lens_index;
     float filter_radius, lookup;
     int border;
     float table[33];

@@ -426,7 +426,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
         const float spx = (float)px + jx, spy = (float)py + jy;
         F3 o, d;
         float mint, maxt;
-        camera_ray(S, spx, spy, o, d, mint, maxt);
+        camera_ray(S, spx, spy, o, d, mint, maxt, sample, pix);
         F3 li;
         switch (S.integrator) {
             case 1: li = li_path_mats<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;

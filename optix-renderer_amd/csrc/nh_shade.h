@@ -262,9 +262,27 @@ __device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e,
     return f3(ev.x / probs, ev.y / probs, ev.z / probs);
 }
 
-// PerspectiveCamera::sampleRay without depth of field (perspective.cpp:97-141)
+// The lens sample of a camera ray (perspective.cpp:118-122). The reference draws it from one static Independent
+// sampler that is never prepare()d -- a default-state pcg32 (pcg32.h:40), two floats per sampleRay call, shared
+// by every render thread. In the serial render order (sample rounds; blocks in BlockGenerator spiral order; a
+// block's pixels x-major, render.cpp:281-347, :436, block.cpp:151-199, independent.cpp:85-99) camera ray
+// k = round * W * H + lens_index[pixel] takes draws 2k and 2k + 1, which pcg32::advance reaches directly: every
+// ray's lens sample is independent of how the rays are distributed over threads, blocks and ranks. (With several
+// threads the reference's draws race, so only its single-thread order is reproducible: DESIGN.md §7.)
+NHD void lens_uniform(const DScene &S, int round, int pix, float &u, float &v) {
+    const uint64_t k = (uint64_t)(uint32_t)round * (uint64_t)((uint32_t)S.width * (uint32_t)S.height) +
+                       (uint64_t)S.lens_index[pix];
+    Rng r;
+    r.inc = kPcgDefaultStream;
+    r.state = pcg_advance(kPcgDefaultState, kPcgDefaultStream, 2 * k);
+    u = r.next1d();
+    v = r.next1d();
+}
+
+// PerspectiveCamera::sampleRay (perspective.cpp:97-141); `round` and `pix` place the ray in the serial order of the
+// lens samples (used only with depth of field)
 __device__ __forceinline__ void camera_ray(const DScene &S, float px, float py, F3 &o, F3 &d, float &mint,
-                                           float &maxt) {
+                                           float &maxt, int round, int pix) {
     const float in0 = px * S.inv_w, in1 = py * S.inv_h;
     float r[4];
 #pragma unroll
@@ -275,20 +293,36 @@ __device__ __forceinline__ void camera_ray(const DScene &S, float px, float py, 
         acc = acc + S.s2c[4 * i + 3] * 1.0f;
         r[i] = acc;
     }
-    F3 dl = normalized(f3(r[0] / r[3], r[1] / r[3], r[2] / r[3]));
+    const F3 dl = normalized(f3(r[0] / r[3], r[1] / r[3], r[2] / r[3]));
+    F3 lo = f3(0.0f, 0.0f, 0.0f), ld = dl;  // local ray
+    if (S.dof) {
+        float su, sv;
+        lens_uniform(S, round, pix, su, sv);
+        // squareToUniformDisk (warp.cpp:48-52)
+        const float rho = f_sqrt(su), theta = sv * 2.0f * kPi;
+        float st, ct;
+        f_sincos(theta, st, ct);
+        const float lx = S.lens_radius * (rho * ct), ly = S.lens_radius * (rho * st);
+        const float ft = S.focal_distance / dl.z;
+        // pFocus = ray(ft) = o + ft * d with o = 0 (ray.h:80)
+        const F3 pf = f3(0.0f + ft * dl.x, 0.0f + ft * dl.y, 0.0f + ft * dl.z);
+        lo = f3(lx, ly, 0.f);
+        ld = normalized(f3(pf.x - lo.x, pf.y - lo.y, pf.z - lo.z));
+    }
     float ow[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        float acc = S.c2w[4 * i] * 0.0f;
-        acc = acc + S.c2w[4 * i + 1] * 0.0f;
-        acc = acc + S.c2w[4 * i + 2] * 0.0f;
+        float acc = S.c2w[4 * i] * lo.x;
+        acc = acc + S.c2w[4 * i + 1] * lo.y;
+        acc = acc + S.c2w[4 * i + 2] * lo.z;
         acc = acc + S.c2w[4 * i + 3] * 1.0f;
         ow[i] = acc;
     }
     o = f3(ow[0] / ow[3], ow[1] / ow[3], ow[2] / ow[3]);
     const float *w = S.c2w;
-    d = f3(w[0] * dl.x + (w[1] * dl.y + w[2] * dl.z), w[4] * dl.x + (w[5] * dl.y + w[6] * dl.z),
-           w[8] * dl.x + (w[9] * dl.y + w[10] * dl.z));
+    d = f3(w[0] * ld.x + (w[1] * ld.y + w[2] * ld.z), w[4] * ld.x + (w[5] * ld.y + w[6] * ld.z),
+           w[8] * ld.x + (w[9] * ld.y + w[10] * ld.z));
+    // the clip range follows the pinhole direction (perspective.cpp:135-137)
     const float inv_z = 1.0f / dl.z;
     mint = S.near_clip * inv_z;
     maxt = S.far_clip * inv_z;

@@ -117,10 +117,11 @@ struct P3 {
 NHD P3 psub(P3 a, P3 b) { return P3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 NHD P3 pcross(P3 a, P3 b) { return P3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 NHD f2 pdot(P3 a, P3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
-NHD void tri_test_pair_p(const P3 &p0, const P3 &p1, const P3 &p2, F3 o, F3 d, float mint, f2 &t, f2 &u, f2 &v,
+// the pair test from the vertex p0 and the edges e1 = p1 - p0, e2 = p2 - p0 (mesh.cpp:105-106), which the LDS pair
+// records of small scenes hold precomputed (the same IEEE subtractions, done once when the records are staged)
+NHD void tri_test_pair_e(const P3 &p0, const P3 &e1, const P3 &e2, F3 o, F3 d, float mint, f2 &t, f2 &u, f2 &v,
                          bool &ok0, bool &ok1) {
     const P3 po{f2{o.x, o.x}, f2{o.y, o.y}, f2{o.z, o.z}}, pd{f2{d.x, d.x}, f2{d.y, d.y}, f2{d.z, d.z}};
-    const P3 e1 = psub(p1, p0), e2 = psub(p2, p0);
     const P3 pvec = pcross(pd, e2);
     const f2 det = pdot(e1, pvec);
     const f2 inv_det = f2{tri_inv_det(det.x), tri_inv_det(det.y)};
@@ -134,6 +135,10 @@ NHD void tri_test_pair_p(const P3 &p0, const P3 &p1, const P3 &p2, F3 o, F3 d, f
           (t.x >= mint);
     ok1 = !(det.y > -1e-8f && det.y < 1e-8f) & !(u.y < 0.0f || u.y > 1.0f) & !(v.y < 0.0f || uv.y > 1.0f) &
           (t.y >= mint);
+}
+NHD void tri_test_pair_p(const P3 &p0, const P3 &p1, const P3 &p2, F3 o, F3 d, float mint, f2 &t, f2 &u, f2 &v,
+                         bool &ok0, bool &ok1) {
+    tri_test_pair_e(p0, psub(p1, p0), psub(p2, p0), o, d, mint, t, u, v, ok0, ok1);
 }
 NHD void tri_test_pair(float4 a0, float4 b0, float4 c0, float4 a1, float4 b1, float4 c1, F3 o, F3 d, float mint,
                        f2 &t, f2 &u, f2 &v, bool &ok0, bool &ok1) {
@@ -222,8 +227,9 @@ struct Traversal {
     // them first); the persistent traversal kernels read those from an LDS copy
     int n_top;
 };
-// pair k: (a.x a.x') (a.y a.y') | (a.z a.z') (a.w a.w') | (b.x b.x') (b.y b.y') | (b.z b.z') (c.x c.x') |
-//         (c.y c.y') (c.z c.z') | (c.w c.w') (0 0)      -- unprimed record k, primed record k+1
+// pair k: (a.x a.x') (a.y a.y') | (a.z a.z') (a.w a.w') | (e1.x e1.x') (e1.y e1.y') | (e1.z e1.z') (e2.x e2.x') |
+//         (e2.y e2.y') (e2.z e2.z') | (c.w c.w') (0 0)   -- unprimed record k, primed record k+1; a = p0 (a sphere's
+//         centre and radius), e1 = p1 - p0, e2 = p2 - p0 (triangles only)
 constexpr int kPairF4 = 6;
 
 // primitive record type / leaf-end bits (word 2 .w of the record), and the BSDF type of the owning
@@ -244,11 +250,11 @@ NHD bool leaf_test(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float 
             const float4 *pp = tv.ppairs + (size_t)kPairF4 * k;
             const float4 q0 = pp[0], q1 = pp[1], q2 = pp[2], q3 = pp[3], q4 = pp[4], q5 = pp[5];
             const P3 p0{f2{q0.x, q0.y}, f2{q0.z, q0.w}, f2{q1.x, q1.y}};
-            const P3 p1{f2{q2.x, q2.y}, f2{q2.z, q2.w}, f2{q3.x, q3.y}};
-            const P3 p2{f2{q3.z, q3.w}, f2{q4.x, q4.y}, f2{q4.z, q4.w}};
+            const P3 e1{f2{q2.x, q2.y}, f2{q2.z, q2.w}, f2{q3.x, q3.y}};
+            const P3 e2{f2{q3.z, q3.w}, f2{q4.x, q4.y}, f2{q4.z, q4.w}};
             f2 pt, pu, pv;
             bool ok0, ok1;
-            tri_test_pair_p(p0, p1, p2, o, d, mint, pt, pu, pv, ok0, ok1);
+            tri_test_pair_e(p0, e1, e2, o, d, mint, pt, pu, pv, ok0, ok1);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 if (j == 1 && k + 1 >= e) break;
@@ -378,11 +384,27 @@ NHD bool leaf_any(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float &
     else return leaf_test<ANY, STATS, PAIRS>(tv, leaf, o, d, mint, maxt, best, found, st);
 }
 
-// Child box of an inner node: side 0 = left, 1 = right.
+// Child box of an inner node: side 0 = left, 1 = right. fin: every 1/d component is finite (box_test_finite applies)
 NHD bool child_box_test(const float4 &n0, const float4 &n1, const float4 &n2, int side, F3 o, F3 d, F3 r, float mint,
-                        float maxt, float &near_t) {
+                        float maxt, float &near_t, bool fin) {
+    if (fin)
+        return side == 0 ? box_test_finite(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, r, mint, maxt, near_t)
+                         : box_test_finite(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, r, mint, maxt, near_t);
     return side == 0 ? box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, near_t)
                      : box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, near_t);
+}
+
+// Both child boxes of an inner node; rays with all 1/d finite take the branch-free packed slab test (box_test_finite:
+// the same answers as the reference's branchy form for them), the others the reference's form
+NHD void node_box_tests(const float4 &n0, const float4 &n1, const float4 &n2, F3 o, F3 d, F3 r, float mint,
+                        float maxt, bool fin, bool &hl, bool &hr, float &nl, float &nr) {
+    if (fin) {
+        box_test_finite_pair(f2{n0.x, n1.z}, f2{n0.y, n1.w}, f2{n0.z, n2.x}, f2{n0.w, n2.y}, f2{n1.x, n2.z},
+                             f2{n1.y, n2.w}, o, r, mint, maxt, hl, hr, nl, nr);
+    } else {
+        hl = box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, nl);
+        hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
+    }
 }
 
 // Closest / any hit. stk points at this thread's first LDS stack slot; consecutive
@@ -401,11 +423,14 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
     best.t = INFINITY;
     if (S.root_kind == 0 || maxt < mint) return false;
     const F3 r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const bool fin = isfinite(r.x) & isfinite(r.y) & isfinite(r.z);
     bool found = false;
     float near_t;
     if (STATS && lead) st.boxes++;
-    if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d, r,
-                  mint, maxt, near_t))
+    if (fin ? !box_test_finite(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1],
+                               S.root_max[2], o, r, mint, maxt, near_t)
+            : !box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o,
+                        d, r, mint, maxt, near_t))
         return false;
     if (S.root_kind == 2) {
         bool any = leaf_any<ANY, STATS, PAIRS, G>(tv, 0, o, d, mint, maxt, best, found, st);
@@ -419,8 +444,8 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
             const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * cur + 3]);
             if (STATS && lead) { st.nodes++; st.boxes += 2; }
             float nl, nr;
-            const bool hl = box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, nl);
-            const bool hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
+            bool hl, hr;
+            node_box_tests(n0, n1, n2, o, d, r, mint, maxt, fin, hl, hr, nl, nr);
             int next;
             if (hl && hr) {
                 const bool right_first = ORDERED && nr < nl;
@@ -449,7 +474,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
             const int parent = (int)(e >> 1), side = (int)(e & 1u);
             const float4 n0 = tv.nodes[4 * parent], n1 = tv.nodes[4 * parent + 1], n2 = tv.nodes[4 * parent + 2];
             if (STATS && lead) st.boxes++;
-            if (!child_box_test(n0, n1, n2, side, o, d, r, mint, maxt, near_t)) continue;
+            if (!child_box_test(n0, n1, n2, side, o, d, r, mint, maxt, near_t, fin)) continue;
             const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * parent + 3]);
             const int ref = side ? n3.y : n3.x;
             if (ref >= 0) {
@@ -543,6 +568,7 @@ struct Tracer {
     int k, kend;  // primitive range of the leaf under test
     int sp;
     bool found, done;
+    bool fin;  // every 1/d component finite: branch-free slab tests (box_test_finite)
     Hit best;
 
     NHD void begin(const DScene &S, const Traversal &tv, F3 o_, F3 d_, float mint_, float maxt_, TravStats &st) {
@@ -561,10 +587,13 @@ struct Tracer {
         k = kend = 0;
         if (S.root_kind == 0 || maxt < mint) return;
         r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        fin = isfinite(r.x) & isfinite(r.y) & isfinite(r.z);
         float near_t;
         if (STATS) st.boxes++;
-        if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d,
-                      r, mint, maxt, near_t))
+        if (fin ? !box_test_finite(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1],
+                                   S.root_max[2], o, r, mint, maxt, near_t)
+                : !box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2],
+                            o, d, r, mint, maxt, near_t))
             return;
         done = false;
         if (S.root_kind == 2) {
@@ -606,8 +635,8 @@ struct Tracer {
             const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * cur + 3]);
             if (STATS) { st.nodes++; st.boxes += 2; }
             float nl, nr;
-            const bool hl = box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, nl);
-            const bool hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
+            bool hl, hr;
+            node_box_tests(n0, n1, n2, o, d, r, mint, maxt, fin, hl, hr, nl, nr);
             int next;
             if (hl && hr) {
                 const bool right_first = ORDERED && nr < nl;
@@ -632,7 +661,7 @@ struct Tracer {
             const float4 n0 = tv.nodes[4 * parent], n1 = tv.nodes[4 * parent + 1], n2 = tv.nodes[4 * parent + 2];
             if (STATS) st.boxes++;
             float near_t;
-            if (!child_box_test(n0, n1, n2, side, o, d, r, mint, maxt, near_t)) return;
+            if (!child_box_test(n0, n1, n2, side, o, d, r, mint, maxt, near_t, fin)) return;
             const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * parent + 3]);
             enter(tv, side ? n3.y : n3.x);
             return;

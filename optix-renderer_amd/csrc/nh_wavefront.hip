@@ -134,11 +134,11 @@ __device__ __forceinline__ void camera_sample(const DScene &S, const WfLaunch &L
     rng = path_rng(L.seed, (uint64_t)pix, (uint64_t)(L.s0 + k));
     jx = rng.next1d();
     jy = rng.next1d();
-    rng.next1d();  // apertureSample (render.cpp:443), unused without depth of field
+    rng.next1d();  // apertureSample (render.cpp:443): unused (the lens sample comes from the camera's own sampler)
     rng.next1d();
     F3 o, d;
     float mint, maxt;
-    camera_ray(S, (float)px + jx, (float)py + jy, o, d, mint, maxt);
+    camera_ray(S, (float)px + jx, (float)py + jy, o, d, mint, maxt, L.s0 + k, pix);
     ro = make_float4(o.x, o.y, o.z, mint);
     rd = make_float4(d.x, d.y, d.z, maxt);
 }
@@ -192,11 +192,12 @@ __device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, cons
             const float4 a1 = nx ? tv.prims[3 * k + 3] : z, b1 = nx ? tv.prims[3 * k + 4] : z,
                          c1 = nx ? tv.prims[3 * k + 5] : z;
             float4 *q = pairs + (size_t)kPairF4 * k;
+            // Moller-Trumbore's edges (mesh.cpp:105-106), subtracted once here instead of in every test
             q[0] = make_float4(a.x, a1.x, a.y, a1.y);
             q[1] = make_float4(a.z, a1.z, a.w, a1.w);
-            q[2] = make_float4(b.x, b1.x, b.y, b1.y);
-            q[3] = make_float4(b.z, b1.z, c.x, c1.x);
-            q[4] = make_float4(c.y, c1.y, c.z, c1.z);
+            q[2] = make_float4(b.x - a.x, b1.x - a1.x, b.y - a.y, b1.y - a1.y);
+            q[3] = make_float4(b.z - a.z, b1.z - a1.z, c.x - a.x, c1.x - a1.x);
+            q[4] = make_float4(c.y - a.y, c1.y - a1.y, c.z - a.z, c1.z - a1.z);
             q[5] = make_float4(c.w, c1.w, 0.f, 0.f);
         }
         t.ppairs = pairs;
@@ -1299,6 +1300,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
 // Asynchronous tail hand-off: the chunk's live paths (RR-ahead state, 88 B each) are copied into a small buffer
 // of their own, densely from slot 0 (all in count shard 0; the other shards and groups are zeroed by the host),
 // so the pool's path state is free for the next chunk while this chunk's tail kernel runs on another stream.
+#if !defined(NH_WF_PART) || NH_WF_PART == 1  // a non-template kernel: defined in one part only
 __global__ __launch_bounds__(256) void wf_pack_rr(WfLaunch L, WfBuf dst, unsigned *dst_counts) {
     const QView qv = queue_view(L.cnt_in);
     const int q = blockIdx.x * 256 + threadIdx.x;
@@ -1313,6 +1315,7 @@ __global__ __launch_bounds__(256) void wf_pack_rr(WfLaunch L, WfBuf dst, unsigne
     dst.rng[q] = B.rng[s];
     dst.hit[q] = B.hit[s];
 }
+#endif
 
 // Tail of a chunk: once few paths are alive, per-bounce launches cost more than the work they
 // carry (three kernels + count traffic for a few thousand paths). wf_tail takes the live queue
@@ -1366,9 +1369,19 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAV
     }
 }
 
+// The launchers are split into parts so the build can compile this file as several translation units in parallel
+// (Makefile: -DNH_WF_PART=k; each part instantiates only its own kernels). Without NH_WF_PART: every part.
+#ifdef NH_WF_PART
+#define NH_WF_HAS_PART(k) (NH_WF_PART == (k))
+#else
+#define NH_WF_HAS_PART(k) 1
+#endif
+
 namespace nh {
 
+#if NH_WF_HAS_PART(0)
 int tree_top_nodes() { return kTopNodes; }
+#endif
 
 // Persistent grids hold exactly the workgroups that are resident at once (occupancy of this
 // instantiation x CUs, at most kPersistentBlocks -- the spill area's size): a workgroup that
@@ -1386,6 +1399,7 @@ static void launch_persistent(int want, hipStream_t st, const DScene *S, const T
     hipLaunchKernelGGL(KERN, dim3(std::min(want, resident)), dim3(128), 0, st, S, tv, L);
 }
 
+#if NH_WF_HAS_PART(0) || NH_WF_HAS_PART(3)
 template <int DEPTH>
 static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                               bool shadow, bool persistent, bool wide, int bound, hipStream_t st) {
@@ -1425,14 +1439,27 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
 #undef NH_WF
 }
 
+#endif
+
+void launch_wf_trace_deep(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
+                          bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st);
+#if NH_WF_HAS_PART(0)
 void launch_wf_trace(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool shadow,
                      bool persistent, bool wide, int bound, int depth, hipStream_t st) {
     if (depth <= 16) launch_wf_trace_d<16>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
     else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
-    else if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
+    else launch_wf_trace_deep(S, tv, L, ordered, stats, shadow, persistent, wide, bound, depth, st);
+}
+#endif
+#if NH_WF_HAS_PART(3)
+void launch_wf_trace_deep(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
+                          bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st) {
+    if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
     else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
 }
+#endif
 
+#if NH_WF_HAS_PART(1)
 template <int DEPTH>
 static void launch_wf_tail_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                              bool wide, int bound, hipStream_t st) {
@@ -1485,6 +1512,9 @@ void launch_wf_bounce(const DScene *S, const Traversal &tv, const WfLaunch &L, b
 #undef NH_FB
 }
 
+#endif
+
+#if NH_WF_HAS_PART(2)
 void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
                          bool lean, int bound, hipStream_t st) {
     int blocks = std::max(1, (bound + 255) / 256);
@@ -1531,6 +1561,9 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
 #undef NH_TR
 }
 
+#endif
+
+#if NH_WF_HAS_PART(1)
 void launch_wf_pack_rr(const WfLaunch &L, const WfBuf &dst, unsigned *dst_counts, int bound, hipStream_t st) {
     hipLaunchKernelGGL(wf_pack_rr, dim3(std::max(1, (bound + 255) / 256)), dim3(256), 0, st, L, dst, dst_counts);
 }
@@ -1542,5 +1575,7 @@ void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, bo
     if (sort) hipLaunchKernelGGL(wf_shade<true>, dim3(blocks), dim3(256), 0, st, S, tv, L);
     else hipLaunchKernelGGL(wf_shade<false>, dim3(blocks), dim3(256), 0, st, S, tv, L);
 }
+
+#endif
 
 }  // namespace nh

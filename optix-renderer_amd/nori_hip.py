@@ -314,6 +314,11 @@ class Scene:
     def border(self):
         return self.desc.filter.border
 
+    @property
+    def spp(self):
+        """the sampler's sampleCount"""
+        return self.desc.sample_count
+
     def framebuffer_shape(self):
         d = self.desc
         b = d.filter.border

@@ -18,24 +18,31 @@ import numpy as np
 _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIXTURE = os.path.join(_REPO, "tests", "golden", "reference_scenes.json")
 TEXTURED_FIXTURE = os.path.join(_REPO, "tests", "golden", "textured_scenes.json.gz")
+PROJECT_FIXTURE = os.path.join(_REPO, "tests", "golden", "project_scenes.json.gz")
 
 C2_ALBEDO = "0.725 0.71 0.68"
 
 
 def materialize(out_dir: str) -> str:
-    """Write the reference scene fixtures (reference_scenes.json and the textured scenes of
-    textured_scenes.json.gz) under out_dir; returns out_dir."""
+    """Write the reference scene fixtures (reference_scenes.json, the textured scenes of textured_scenes.json.gz and
+    the depth-of-field / envmap scenes of project_scenes.json.gz) under out_dir; returns out_dir."""
+    import base64
+    import gzip
     with open(FIXTURE) as f:
         files = json.load(f)
-    if os.path.exists(TEXTURED_FIXTURE):
-        import gzip
-        with gzip.open(TEXTURED_FIXTURE, "rt") as f:
-            files.update(json.load(f))
+    for bundle in (TEXTURED_FIXTURE, PROJECT_FIXTURE):
+        if os.path.exists(bundle):
+            with gzip.open(bundle, "rt") as f:
+                files.update(json.load(f))
     for rel, text in files.items():
         p = os.path.join(out_dir, rel)
         os.makedirs(os.path.dirname(p), exist_ok=True)
-        with open(p, "w") as g:
-            g.write(text)
+        if isinstance(text, dict):  # binary file (a PNG)
+            with open(p, "wb") as g:
+                g.write(base64.b64decode(text["base64"]))
+        else:
+            with open(p, "w") as g:
+                g.write(text)
     return out_dir
 
 

@@ -72,6 +72,20 @@ struct Pcg32 {
         std::memcpy(&f, &u, 4);
         return f - 1.0f;
     }
+    void advance(int64_t delta_) {  // pcg32.h:131-150
+        uint64_t cur_mult = kPcgMult, cur_plus = inc, acc_mult = 1u, acc_plus = 0u;
+        uint64_t delta = (uint64_t)delta_;
+        while (delta > 0) {
+            if (delta & 1) {
+                acc_mult *= cur_mult;
+                acc_plus = acc_plus * cur_mult + cur_plus;
+            }
+            cur_plus = (cur_mult + 1) * cur_plus;
+            cur_mult *= cur_mult;
+            delta /= 2;
+        }
+        state = acc_mult * state + acc_plus;
+    }
 };
 
 inline uint64_t splitmix64(uint64_t x) {
@@ -1062,8 +1076,11 @@ V3 li_direct(const no_scene &s, Sampler &smp, const Ray &ray) {
     return result;
 }
 
-// PerspectiveCamera::sampleRay (perspective.cpp:97-141), no depth of field
-Ray camera_ray(const nh_camera &c, float px, float py) {
+inline bool has_dof(const nh_camera &c) { return c.lens_radius > kEps; }  // perspective.cpp:114
+
+// PerspectiveCamera::sampleRay (perspective.cpp:97-141). lens: the two floats the static camera sampler returns
+// for this ray (perspective.cpp:118-122), read only with depth of field.
+Ray camera_ray(const nh_camera &c, float px, float py, const float *lens = nullptr) {
     const float *m = c.sample_to_camera;
     float in[4] = {px * c.inv_output_size[0], py * c.inv_output_size[1], 0.0f, 1.0f};
     float r[4];
@@ -1075,21 +1092,32 @@ Ray camera_ray(const nh_camera &c, float px, float py) {
         r[i] = acc;
     }
     V3 near_p = mk(r[0] / r[3], r[1] / r[3], r[2] / r[3]);
-    V3 d = normalized(near_p);
+    const V3 d = normalized(near_p);
+    V3 lo = mk(0.0f, 0.0f, 0.0f), ld = d;  // ray.o = Point3f(0, 0, 0), ray.d = d
+    if (has_dof(c)) {
+        float dx, dy;
+        square_to_uniform_disk(lens[0], lens[1], dx, dy);
+        const float plx = c.lens_radius * dx, ply = c.lens_radius * dy;  // m_lensRadius * Point2f
+        const float ft = c.focal_distance / ld.z;
+        const V3 pf = mk(lo.x + ft * ld.x, lo.y + ft * ld.y, lo.z + ft * ld.z);  // ray(ft) = o + t * d
+        lo = mk(plx, ply, 0.f);
+        ld = normalized(mk(pf.x - lo.x, pf.y - lo.y, pf.z - lo.z));
+    }
     const float *w = c.camera_to_world;
     float o4[4];
+    const float pin[4] = {lo.x, lo.y, lo.z, 1.0f};
     for (int i = 0; i < 4; ++i) {
-        float acc = w[4 * i + 0] * 0.0f;
-        acc = acc + w[4 * i + 1] * 0.0f;
-        acc = acc + w[4 * i + 2] * 0.0f;
-        acc = acc + w[4 * i + 3] * 1.0f;
+        float acc = w[4 * i + 0] * pin[0];
+        acc = acc + w[4 * i + 1] * pin[1];
+        acc = acc + w[4 * i + 2] * pin[2];
+        acc = acc + w[4 * i + 3] * pin[3];
         o4[i] = acc;
     }
     Ray ray;
     ray.o = mk(o4[0] / o4[3], o4[1] / o4[3], o4[2] / o4[3]);
-    ray.d = mk(w[0] * d.x + (w[1] * d.y + w[2] * d.z), w[4] * d.x + (w[5] * d.y + w[6] * d.z),
-               w[8] * d.x + (w[9] * d.y + w[10] * d.z));
-    float inv_z = 1.0f / d.z;
+    ray.d = mk(w[0] * ld.x + (w[1] * ld.y + w[2] * ld.z), w[4] * ld.x + (w[5] * ld.y + w[6] * ld.z),
+               w[8] * ld.x + (w[9] * ld.y + w[10] * ld.z));
+    float inv_z = 1.0f / d.z;  // the pinhole direction (perspective.cpp:135)
     ray.mint = c.near_clip * inv_z;
     ray.maxt = c.far_clip * inv_z;
     ray.drcp = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
@@ -1161,6 +1189,30 @@ std::vector<std::pair<int, int>> spiral_blocks(int w, int h, int bs) {
         } while (bx < 0 || by < 0 || bx >= nbx || by >= nby);
     }
     return out;
+}
+
+// Position of each pixel's camera ray within one sample round of the reference's serial render order: blocks in
+// BlockGenerator order, edge blocks clipped (block.cpp:174-176), a block's pixels x-major
+// (Independent::getSampleIndices, independent.cpp:85-99)
+std::vector<uint32_t> serial_ray_index(int w, int h, int bs) {
+    std::vector<uint32_t> idx((size_t)w * h);
+    uint32_t k = 0;
+    for (auto &b : spiral_blocks(w, h, bs)) {
+        const int ox = b.first * bs, oy = b.second * bs, sx = std::min(bs, w - ox), sy = std::min(bs, h - oy);
+        for (int x = 0; x < sx; ++x)
+            for (int y = 0; y < sy; ++y) idx[(size_t)(oy + y) * w + (ox + x)] = k++;
+    }
+    return idx;
+}
+
+// The lens sample of serial camera ray k (perspective.cpp:118-122): the camera's static Independent sampler is a
+// default-state pcg32 that is never prepared (pcg32.h:40), two floats per sampleRay call, so ray k reads draws
+// 2k and 2k + 1 -- pcg32::advance gets there without the k - 1 rays before it
+void lens_jump(uint64_t k, float out[2]) {
+    Pcg32 r;
+    r.advance((int64_t)(2 * k));
+    out[0] = r.next_float();
+    out[1] = r.next_float();
 }
 
 }  // namespace
@@ -1619,7 +1671,13 @@ int no_path_radiance(const no_scene *s, uint64_t seed, int32_t px, int32_t py, i
     smp.next2d(jx, jy);
     smp.next2d(ax, ay);  // apertureSample (render.cpp:443), unused without DOF
     float spx = (float)px + jx, spy = (float)py + jy;
-    Ray ray = camera_ray(s->cam, spx, spy);
+    float lens[2] = {0.f, 0.f};
+    if (has_dof(s->cam)) {
+        const int W = s->cam.width, H = s->cam.height;
+        const uint64_t pos = serial_ray_index(W, H, 32)[(size_t)py * W + px];
+        lens_jump((uint64_t)(uint32_t)sample * (uint64_t)W * (uint64_t)H + pos, lens);
+    }
+    Ray ray = camera_ray(s->cam, spx, spy, lens);
     V3 v = li(*s, smp, ray);
     rgb3[0] = v.x; rgb3[1] = v.y; rgb3[2] = v.z;
     if (jitter2) { jitter2[0] = jx; jitter2[1] = jy; }
@@ -1629,8 +1687,16 @@ int no_path_radiance(const no_scene *s, uint64_t seed, int32_t px, int32_t py, i
 int no_render(const no_scene *s, int32_t mode, uint64_t seed, int32_t s0, int32_t s1, const int32_t *blocks,
               int32_t n_blocks, int32_t n_threads, float *rgbw, uint64_t *n_invalid) {
     if (!s || !rgbw || s1 < s0) return NH_ERR_INVALID;
+    // NO_RENDER_LENS_SERIAL: the lens samples come from one sequential stream in the serial loop itself, literally
+    // as the reference's single-thread render draws them (needs the whole image, one thread, round 0 onwards)
+    const bool lens_serial = (mode & NO_RENDER_LENS_SERIAL) != 0;
+    mode &= ~NO_RENDER_LENS_SERIAL;
+    if (lens_serial && (blocks || n_threads != 1 || s0 != 0)) return NH_ERR_INVALID;
     if (mode == NO_SAMPLER_NORI_BLOCK && s0 != 0) return NH_ERR_INVALID;
     const int W = s->cam.width, H = s->cam.height, B = 32, border = s->filter.border;
+    const bool dof = has_dof(s->cam);
+    const std::vector<uint32_t> ray_pos = dof ? serial_ray_index(W, H, B) : std::vector<uint32_t>();
+    Pcg32 lens_stream;  // the camera's static sampler (perspective.cpp:118-119), NO_RENDER_LENS_SERIAL only
     const int nbx = (W + B - 1) / B;
     auto order = spiral_blocks(W, H, B);
     std::vector<char> keep(order.size() ? (size_t)nbx * ((H + B - 1) / B) : 0, blocks ? 0 : 1);
@@ -1675,7 +1741,15 @@ int no_render(const no_scene *s, int32_t mode, uint64_t seed, int32_t s0, int32_
                         smp.next2d(jx, jy);
                         smp.next2d(ax, ay);
                         float spx = (float)px + jx, spy = (float)py + jy;
-                        Ray ray = camera_ray(s->cam, spx, spy);
+                        float lens[2] = {0.f, 0.f};
+                        if (dof && lens_serial) {
+                            lens[0] = lens_stream.next_float();  // sampler->next2D()
+                            lens[1] = lens_stream.next_float();
+                        } else if (dof) {
+                            lens_jump((uint64_t)(uint32_t)smp_i * (uint64_t)W * (uint64_t)H +
+                                          ray_pos[(size_t)py * W + px], lens);
+                        }
+                        Ray ray = camera_ray(s->cam, spx, spy, lens);
                         V3 v = li(*s, smp, ray);
                         v = v * 1.0f;  // value = Color3f(1) * Li
                         if (!block_put(b, s->filter, spx, spy, v)) invalid++;
@@ -1714,7 +1788,9 @@ int no_ttest_scene(const no_scene *s, uint64_t *state, uint64_t *inc, int32_t n,
         float spx = a * (float)s->cam.width, spy = b * (float)s->cam.height;
         float ax, ay;
         smp.next2d(ax, ay);
-        Ray ray = camera_ray(s->cam, spx, spy);
+        float lens[2] = {0.f, 0.f};
+        if (has_dof(s->cam)) lens_jump((uint64_t)k, lens);  // the k-th sampleRay of this serial loop
+        Ray ray = camera_ray(s->cam, spx, spy, lens);
         V3 v = li(*s, smp, ray);
         double r = (double)luminance(v);
         double delta = r - m;

@@ -29,6 +29,10 @@ extern "C" {
 typedef struct no_scene no_scene;
 
 enum { NO_SAMPLER_PER_PATH = 0, NO_SAMPLER_NORI_BLOCK = 1 };
+/* or'ed into no_render's sampler_mode: depth-of-field lens samples drawn from one sequential stream inside the
+ * serial render loop, literally as the reference's single-thread render does (perspective.cpp:118-122); requires
+ * blocks == NULL, n_threads == 1, s0 == 0. Without it each ray's lens sample is reached by pcg32::advance. */
+enum { NO_RENDER_LENS_SERIAL = 0x100 };
 
 /* copies the scene and builds the BVH with a serial restatement of BVH::build */
 int no_scene_create(const nh_scene_desc *desc, no_scene **out);

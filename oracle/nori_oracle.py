@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(_HERE, "_build", "libnori_oracle.so")
 _lib = C.CDLL(LIB_PATH)
 
 PER_PATH, NORI_BLOCK = 0, 1
+LENS_SERIAL = 0x100  # or into `mode`: lens samples from one sequential stream in the serial loop (nori_oracle.h)
 PCG32_DEFAULT_STATE = 0x853C49E6748FEA9B
 PCG32_DEFAULT_STREAM = 0xDA3E39CB94B95BDB
 

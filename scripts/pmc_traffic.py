@@ -4,7 +4,11 @@ usage: python scripts/pmc_traffic.py gpurun_out/pmc_TAG WORKLOAD_KEY KERNEL_SUBS
 FETCH_SIZE (KB) is doubled (gfx950 reports half the bytes of wide coalesced reads,
 MI355X_MICROARCH.md HBM section); WRITE_SIZE (KB) is taken as is. Both are averaged over the
 kernel's dispatches, like the bench's achieved bytes per launch.
+The record names the full kernel instantiation the counters came from (one distinct kernel name must match
+KERNEL_SUBSTRING) and the build it ran: lib_sha16, the first 16 hex digits of the SHA-256 of the library the passes
+loaded (NH_LIB_PATH, else optix-renderer_amd/lib/libnori_hip.so). bench.py uses a record only for that same build.
 """
+import hashlib
 import csv
 import glob
 import json
@@ -13,19 +17,28 @@ import sys
 from collections import defaultdict
 
 root, key, pat = sys.argv[1:4]
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+lib = os.environ.get("NH_LIB_PATH") or os.path.join(REPO, "optix-renderer_amd", "lib", "libnori_hip.so")
+lib_sha16 = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
 vals = defaultdict(list)
+names = set()
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
+        if pat in r["Kernel_Name"]:
+            names.add(r["Kernel_Name"])
         if pat in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU",
                                                              "GRBM_GUI_ACTIVE", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES",
                                                              "SQ_ACTIVE_INST_VALU", "VALUBusy", "VALUUtilization",
                                                              "TCC_HIT_sum", "TCC_MISS_sum"):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+if len(names) != 1:
+    sys.exit(f"pmc_traffic: {len(names)} distinct kernels match {pat!r}: {sorted(names)}")
+kernel = names.pop()
 fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"]) * 2 * 1024  # x2: gfx950 FETCH_SIZE (HBM section)
 write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"]) * 1024
 out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
 data = json.load(open(out)) if os.path.exists(out) else {}
-data[key] = {"kernel": pat, "hbm_bytes_per_launch": int(fetch + write), "read_bytes_per_launch": int(fetch),
+data[key] = {"kernel": kernel, "lib_sha16": lib_sha16, "hbm_bytes_per_launch": int(fetch + write), "read_bytes_per_launch": int(fetch),
              "write_bytes_per_launch": int(write), "dispatches": len(vals["FETCH_SIZE"]),
              "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {os.path.basename(root)}"}
 avg = lambda k: sum(vals[k]) / len(vals[k]) if vals[k] else None  # noqa: E731

@@ -17,7 +17,12 @@ Writes (all data, no reference source):
                           scenes/pa1/mesh-texture.xml and sphere-texture.xml (checkerboard_color),
                           scenes/project/textures/aircraft.xml (png_texture; its aircraft_base.png and .hdr
                           envmap are absent from the reference checkout)
+  project_scenes.json.gz  the reference's depth-of-field scenes (scenes/project/dof/dof-val.xml and
+                          table_path_mis.xml, path_mis, thin lens) with their meshes, and its envmap scene
+                          scenes/project/envmap/envmap_sphere.xml with the shipped res/wooden_motel.png (binary
+                          files stored as {"base64": ...})
 """
+import base64
 import gzip
 import json
 import os
@@ -73,6 +78,31 @@ TEXTURED_FILES = [
     "scenes/project/meshes/aircraft/aircraft_glass.obj",
 ]
 
+PROJECT_FILES = [
+    "scenes/project/dof/dof-val.xml",
+    "scenes/project/dof/center-cube.obj",
+    "scenes/project/dof/center-lights.obj",
+    "scenes/project/dof/cube-array.obj",
+    "scenes/project/dof/floor.obj",
+    "scenes/project/dof/light-array.obj",
+    "scenes/project/dof/table_path_mis.xml",
+    "scenes/project/meshes/table/plane.obj",
+    "scenes/project/meshes/table/curvy_bowl.obj",
+    "scenes/project/meshes/table/circle.obj",
+    "scenes/project/meshes/table/wine_glass.obj",
+    "scenes/project/meshes/table/wine_glass_inner.obj",
+    "scenes/project/envmap/envmap_sphere.xml",
+    "scenes/project/res/wooden_motel.png",
+]
+
+
+def read_fixture(ref, rel):
+    data = open(os.path.join(ref, rel), "rb").read()
+    try:
+        return data.decode("utf-8")
+    except UnicodeDecodeError:
+        return {"base64": base64.b64encode(data).decode("ascii")}
+
 
 def parse_demo(text):
     rounds = []
@@ -120,7 +150,10 @@ def main():
     textured = {p: open(os.path.join(ref, p)).read() for p in TEXTURED_FILES}
     with open(os.path.join(HERE, "textured_scenes.json.gz"), "wb") as f:
         f.write(gzip.compress(json.dumps(textured, indent=0).encode(), mtime=0))
-    print("wrote pcg32_kat.json, reference_scenes.json, textured_scenes.json.gz")
+    project = {p: read_fixture(ref, p) for p in PROJECT_FILES}
+    with open(os.path.join(HERE, "project_scenes.json.gz"), "wb") as f:
+        f.write(gzip.compress(json.dumps(project, indent=0).encode(), mtime=0))
+    print("wrote pcg32_kat.json, reference_scenes.json, textured_scenes.json.gz, project_scenes.json.gz")
 
 
 if __name__ == "__main__":

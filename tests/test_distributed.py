@@ -65,6 +65,19 @@ def _bench(args, timeout=600):
     return json.loads(lines[0])
 
 
+def check_rank_breakdown(rk, elapsed_s, world=2):
+    """The N>1 diagnosis (verdict r4 item 7): per-rank render and reduce times and chunk counts, consistent with
+    the line's own time (= the max over ranks of render + reduce)."""
+    for key in ("render_s", "reduce_s", "total_s", "chunks"):
+        assert len(rk[key]) == world, rk
+    assert all(c >= 1 for c in rk["chunks"]) and all(x >= 0 for x in rk["reduce_s"]), rk
+    for a, b, t in zip(rk["render_s"], rk["reduce_s"], rk["total_s"]):
+        assert abs(a + b - t) < 1e-5, rk
+    assert rk["render_s_min"] == min(rk["render_s"]) and rk["render_s_max"] == max(rk["render_s"])
+    assert rk["reduce_s_max"] == max(rk["reduce_s"])
+    assert abs(max(rk["total_s"]) - elapsed_s) <= 2e-3 * max(1.0, elapsed_s) + 1e-3, (rk, elapsed_s)
+
+
 def test_bench_gpus_n_launches_n_ranks():
     """`python bench.py --gpus 2` with no launcher around it starts two ranks itself (a child
     torch.distributed.run); here only their rendezvous runs (gloo, no GPU)."""
@@ -87,6 +100,7 @@ def test_bench_two_hip_ranks_reduce_to_one_rank_render(tmp_path, gpu):
                    "--traversal-1m-steps", "0", "--roofline-steps", "0", "--strong-spp", "0", "--no-extras",
                    "--dump-framebuffer", out])
     assert line["n_gpus"] == 2 and line["value"] > 0
+    check_rank_breakdown(line["ranks"], line["ms_per_step"] * line["steps"] / 1e3)
     reduced = np.load(out).astype(np.float64)
     xml = scenegen.cbox_xml(str(tmp_path), "c2", width=160, height=96)
     s = nh.Scene(xml)
@@ -118,6 +132,8 @@ def test_bench_two_hip_ranks_strong_scaling_equals_one_rank_render(tmp_path, gpu
     assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["config"]["spp"] == 6
     sc = line["strong_c4"]
     assert sc["n_gpus"] == 2 and sc["spp"] == 2 and sc["msamples_s"] > 0
+    check_rank_breakdown(line["ranks"], line["ms_per_step"] * line["steps"] / 1e3)
+    check_rank_breakdown(sc["ranks"], sc["ms"] / 1e3)
     reduced = np.load(out).astype(np.float64)
     xml = scenegen.cbox_xml(str(tmp_path), "c1", width=160, height=96)
     s = nh.Scene(xml)
