@@ -229,6 +229,19 @@ std::vector<int> spiral_rank(int w, int h, int bs, int &nbx, int &nby) {
     return rank;
 }
 
+// DScene::emit_faces: each emitting face's vertices and the normal Mesh::sampleSurface computes for it
+// (normalized(cross(p1 - p0, p2 - p0)), mesh.cpp:64-69), by the device functions the light sample would run
+__global__ void emit_face_kernel(const float *V, const uint4 *tri, int n, float4 *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 t = tri[i];
+    const nhd::F3 p0 = nhd::ldv(V, t.x), p1 = nhd::ldv(V, t.y), p2 = nhd::ldv(V, t.z);
+    const nhd::F3 nn = nhd::normalized(nhd::cross(nhd::sub(p1, p0), nhd::sub(p2, p0)));
+    out[3 * i] = make_float4(p0.x, p0.y, p0.z, nn.x);
+    out[3 * i + 1] = make_float4(p1.x, p1.y, p1.z, nn.y);
+    out[3 * i + 2] = make_float4(p2.x, p2.y, p2.z, nn.z);
+}
+
 // The position of each pixel's camera ray within one sample round of the reference's serial render order: blocks
 // in BlockGenerator order (edge blocks clipped, block.cpp:174-176), then Independent::getSampleIndices' x-major
 // pixel order (independent.cpp:85-99: x outer, y inner)
@@ -399,7 +412,24 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         o.pdf_off = (int)s.pdf_offset;
         o.pdf_norm = s.pdf_normalization;
         o.tex_uv = d->bsdfs[s.bsdf].type == NH_BSDF_DIFFUSE && d->bsdfs[s.bsdf].albedo_texture != 0;
+        o.ef_off = -1;
     }
+    // emitting meshes without vertex normals: one emit_faces record per face (vertex index triples here)
+    std::vector<uint4> ef_tri;
+    if (!(std::getenv("NH_EMIT_FACES") && std::getenv("NH_EMIT_FACES")[0] == '0'))
+        for (uint32_t i = 0; i < d->n_shapes; ++i) {
+            const nh_shape &s = d->shapes[i];
+            if (s.type != NH_SHAPE_MESH || s.emitter < 0 || s.has_normals) continue;
+            if ((uint64_t)s.f_offset + s.n_faces > d->n_faces) return fail(c, "shape faces out of range"), NH_ERR_INVALID;
+            ds[i].ef_off = (int)ef_tri.size();
+            for (uint32_t f = 0; f < s.n_faces; ++f) {
+                const uint32_t *fi = &d->F[3 * ((size_t)s.f_offset + f)];
+                const uint32_t i0 = s.v_offset + fi[0], i1 = s.v_offset + fi[1], i2 = s.v_offset + fi[2];
+                if (i0 >= d->n_vertices || i1 >= d->n_vertices || i2 >= d->n_vertices)
+                    return fail(c, "face vertex index out of range"), NH_ERR_INVALID;
+                ef_tri.push_back(make_uint4(i0, i1, i2, 0u));
+            }
+        }
     std::vector<DBsdf> db(d->n_bsdfs);
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
         const nh_bsdf &b = d->bsdfs[i];
@@ -458,6 +488,18 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     if ((rc = upload(c, c->scene_bufs, d->T, 3 * nv, &S.T))) return rc;
     if ((rc = upload(c, c->scene_bufs, d->BT, 3 * nv, &S.BT))) return rc;
     if ((rc = upload(c, c->scene_bufs, d->F, 3 * (size_t)d->n_faces, &S.F))) return rc;
+    S.emit_faces = nullptr;
+    if (!ef_tri.empty()) {
+        const uint4 *tri = nullptr;
+        if ((rc = upload(c, c->scene_bufs, ef_tri.data(), ef_tri.size(), &tri))) return rc;
+        float4 *faces = nullptr;
+        HIP_TRY(c, hipMalloc(&faces, 3 * ef_tri.size() * sizeof(float4)));
+        c->scene_bufs.push_back(faces);
+        const int n = (int)ef_tri.size();
+        hipLaunchKernelGGL(emit_face_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, S.V, tri, n, faces);
+        HIP_TRY(c, hipGetLastError());
+        S.emit_faces = faces;
+    }
     if ((rc = upload(c, c->scene_bufs, d->area_cdf, (size_t)d->n_area_cdf, &S.area_cdf))) return rc;
     if (!dt.empty() && (rc = upload(c, c->scene_bufs, dt.data(), dt.size(), &S.texs))) return rc;
     if (d->n_texels) {
@@ -1203,6 +1245,10 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
         L.small_nodes = c->n_node_f4;
         L.small_leaves = c->n_leaves;
         L.small_prims = c->n_prim_f4;
+        // the flat triangles' shading frames staged beside the records (hit_info reads them instead of a
+        // normalize + frame construction per hit) while they add little LDS
+        L.small_frames = c->n_prim_f4 / 3 <= kSmallFramesMaxPrims;
+        if (const char *e = std::getenv("NH_LDS_FRAMES")) L.small_frames = L.small_frames && e[0] != '0';
     }
     const int per_chunk = 256;  // wf_shade's chunk
     const int max_chunks = (n_paths + per_chunk - 1) / per_chunk;

@@ -166,7 +166,7 @@ struct alignas(16) DShape {
     int pdf_off;
     float pdf_norm;
     int tex_uv;  // its BSDF reads Intersection::uv (a textured diffuse albedo): hit_info computes uv only then
-    int pad1;
+    int ef_off;  // emitting mesh without normals: its faces' first record in DScene::emit_faces, else -1
 };
 struct alignas(16) DBsdf {
     int type;
@@ -210,6 +210,10 @@ struct DScene {
     const float *V, *N, *UV, *T, *BT;
     const uint32_t *F;
     const float *area_cdf;
+    // emitting meshes without vertex normals, per face: (p0, n.x) (p1, n.y) (p2, n.z) with the face normal
+    // normalized(cross(p1 - p0, p2 - p0)) of Mesh::sampleSurface (mesh.cpp:64-69), computed once at upload by the
+    // same device arithmetic (nh_api.hip emit_face_kernel) instead of per light sample
+    const float4 *emit_faces;
     // camera (perspective.cpp) and filter table (block.cpp)
     float s2c[16], c2w[16];
     float inv_w, inv_h, near_clip, far_clip;

@@ -167,6 +167,7 @@ struct WfLaunch {
     // small scenes: float4 / int2 counts of the BVH arrays staged into LDS by the traversal
     // kernels (0 = traverse from HBM)
     int small_nodes, small_leaves, small_prims;
+    int small_frames;  // 1: the fused kernels also stage the flat triangles' shading frames (Traversal::frames)
     // persistent traversal: per-lane stack spill area (kPersistentBlocks * 128 lanes x spill_depth
     // 32-bit words; the 4-wide traversal spills (ref, distance) pairs)
     uint32_t *trav_spill;
@@ -176,6 +177,7 @@ struct WfLaunch {
 // persistent traversal grid: 16 workgroups of 128 lanes per CU (the 8 waves/SIMD its registers allow)
 constexpr int kPersistentBlocks = 256 * 16;
 constexpr size_t kSmallSceneBytes = 16384;
+constexpr int kSmallFramesMaxPrims = 256;  // frames staged (48 B per record) only for scenes this small
 namespace nh {
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                      bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st);

@@ -12,6 +12,16 @@ struct Its {  // Intersection (include/nori/shape.h:41-79); geoFrame only where 
     int shape;
 };
 
+// the geometric frame of triangle record k, as staged (Traversal::frames)
+__device__ __forceinline__ Frame staged_frame(const float4 *frames, int k) {
+    const float4 fs = frames[3 * k], ft = frames[3 * k + 1], fn = frames[3 * k + 2];
+    Frame f;
+    f.s = f3(fs.x, fs.y, fs.z);
+    f.t = f3(ft.x, ft.y, ft.z);
+    f.n = f3(fn.x, fn.y, fn.z);
+    return f;
+}
+
 // Mesh::setHitInformation (mesh.cpp:141-196) / Sphere::setHitInformation (sphere.cpp:96-124)
 __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, const Hit &h, F3 o, F3 d, Its &its) {
     const float4 a = tv.prims[3 * h.k], b = tv.prims[3 * h.k + 1];
@@ -44,7 +54,7 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
     its.u = h.u;
     its.v = h.v;
     if (!sh.has_uv && !sh.has_n) {
-        its.sh = frame_from_n(normalized(cross(sub(p1, p0), sub(p2, p0))));
+        its.sh = tv.frames ? staged_frame(tv.frames, h.k) : frame_from_n(normalized(cross(sub(p1, p0), sub(p2, p0))));
         return;
     }
     const int local = __float_as_int(a.w);
@@ -64,7 +74,7 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
             its.sh = frame_from_n(nrm);
         }
     } else {
-        its.sh = frame_from_n(normalized(cross(sub(p1, p0), sub(p2, p0))));
+        its.sh = tv.frames ? staged_frame(tv.frames, h.k) : frame_from_n(normalized(cross(sub(p1, p0), sub(p2, p0))));
     }
 }
 
@@ -235,14 +245,21 @@ __device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e,
         sx = (sx - cdf[idt]) / (cdf[idt + 1] - cdf[idt]);
         float su1 = f_sqrt(sx);  // squareToUniformTriangle (warp.cpp:162-166)
         float bu = 1.f - su1, bv = sy * su1, bw = 1.f - bu - bv;
-        const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + idt);
-        const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
-        const F3 p0 = ldv(S.V, i0), p1 = ldv(S.V, i1), p2 = ldv(S.V, i2);
-        p = add(add(scl(bu, p0), scl(bv, p1)), scl(bw, p2));
-        if (sh.has_n)
-            n = normalized(add(add(scl(bu, ldv(S.N, i0)), scl(bv, ldv(S.N, i1))), scl(bw, ldv(S.N, i2))));
-        else
-            n = normalized(cross(sub(p1, p0), sub(p2, p0)));
+        if (sh.ef_off >= 0) {  // the face's vertices and its normal, precomputed (DScene::emit_faces)
+            const float4 *q = S.emit_faces + 3 * (size_t)(sh.ef_off + idt);
+            const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+            p = add(add(scl(bu, f3(q0.x, q0.y, q0.z)), scl(bv, f3(q1.x, q1.y, q1.z))), scl(bw, f3(q2.x, q2.y, q2.z)));
+            n = f3(q0.w, q1.w, q2.w);
+        } else {
+            const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + idt);
+            const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
+            const F3 p0 = ldv(S.V, i0), p1 = ldv(S.V, i1), p2 = ldv(S.V, i2);
+            p = add(add(scl(bu, p0), scl(bv, p1)), scl(bw, p2));
+            if (sh.has_n)
+                n = normalized(add(add(scl(bu, ldv(S.N, i0)), scl(bv, ldv(S.N, i1))), scl(bw, ldv(S.N, i2))));
+            else
+                n = normalized(cross(sub(p1, p0), sub(p2, p0)));
+        }
     } else {  // Sphere::sampleSurface (sphere.cpp:126-131)
         F3 q = uniform_sphere(sx, sy);
         p = add(f3(sh.cx, sh.cy, sh.cz), scl(sh.radius, q));

@@ -223,6 +223,10 @@ struct Traversal {
     // LDS-staged scenes (wf_bounce): records k and k+1 interleaved component by component, kPairF4 float4
     // per k, so a primitive pair loads straight into packed-FP32 register pairs (leaf_test<.., PAIRS>)
     const float4 *ppairs;
+    // LDS-staged scenes: each triangle's shading frame when its mesh has no normals (Mesh::setHitInformation's
+    // Frame(normalized(cross(p1 - p0, p2 - p0))), mesh.cpp:180-190), 3 float4 (s, t, n) per record, computed at
+    // staging by the same arithmetic; nullptr: hit_info computes it
+    const float4 *frames;
     // the first n_top wide nodes are the top of the tree (the nodes most rays visit, nh_api.hip numbers
     // them first); the persistent traversal kernels read those from an LDS copy
     int n_top;

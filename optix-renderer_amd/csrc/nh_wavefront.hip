@@ -180,6 +180,7 @@ __device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, cons
     t.prims = prims;
     t.leaves = leaves;
     t.ppairs = nullptr;
+    t.frames = nullptr;
     t.wnodes = tv.wnodes;
     t.n_top = 0;
     if constexpr (PAIRS) {
@@ -201,14 +202,29 @@ __device__ __forceinline__ Traversal stage_small_scene(const Traversal &tv, cons
             q[5] = make_float4(c.w, c1.w, 0.f, 0.f);
         }
         t.ppairs = pairs;
+        if (L.small_frames) {  // flat triangles' shading frames (hit_info), from the records just read
+            float4 *fr = pairs + (size_t)kPairF4 * n;
+            for (int k = threadIdx.x; k < n; k += blockDim.x) {
+                const float4 a = tv.prims[3 * k], b = tv.prims[3 * k + 1], c = tv.prims[3 * k + 2];
+                Frame f{};
+                if (prim_is_tri(c)) {
+                    const F3 p0 = f3(a.x, a.y, a.z);
+                    f = frame_from_n(normalized(cross(sub(f3(b.x, b.y, b.z), p0), sub(f3(c.x, c.y, c.z), p0))));
+                }
+                fr[3 * k] = make_float4(f.s.x, f.s.y, f.s.z, 0.f);
+                fr[3 * k + 1] = make_float4(f.t.x, f.t.y, f.t.z, 0.f);
+                fr[3 * k + 2] = make_float4(f.n.x, f.n.y, f.n.z, 0.f);
+            }
+            t.frames = fr;
+        }
     }
     __syncthreads();
     return t;
 }
 
-// float4 count of the dynamic LDS of the fused kernels: BVH + pair records
+// float4 count of the dynamic LDS of the fused kernels: BVH + pair records + the flat triangles' frames
 __host__ __device__ __forceinline__ int rr_lds_f4(const WfLaunch &L) {
-    return small_pairs_offset_f4(L) + kPairF4 * (L.small_prims / 3);
+    return small_pairs_offset_f4(L) + kPairF4 * (L.small_prims / 3) + (L.small_frames ? 3 * (L.small_prims / 3) : 0);
 }
 
 template <bool SMALL>
@@ -1500,7 +1516,7 @@ void launch_wf_bounce(const DScene *S, const Traversal &tv, const WfLaunch &L, b
                       int bound, hipStream_t st) {
     int blocks = std::max(1, (bound + 255) / 256);
     blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
-    const size_t lds = 16 * ((size_t)small_pairs_offset_f4(L) + (size_t)kPairF4 * (L.small_prims / 3));
+    const size_t lds = 16 * (size_t)rr_lds_f4(L);
 #define NH_FB(O, T, SO) hipLaunchKernelGGL((wf_bounce<O, T, SO>), dim3(blocks), dim3(256), lds, st, S, tv, L)
     if (ordered) {
         if (stats) { if (sort) NH_FB(true, true, true); else NH_FB(true, true, false); }
