@@ -328,6 +328,15 @@ def roofline(args, calib, st, W, H, R):
             roof["tail_profile"]["coop_bounces"] = nc
             roof["tail_profile"]["coop_cycles_per_bounce"] = {
                 k: round(calib[f"tail_coop_cycles_{k}"] / nc, 1) for k in ("body", "shadow", "closest", "head")}
+    nbb = calib.get("bounce_bounces", 0)
+    if nbb:
+        # the RR-ahead bounce kernel's phases in its calibration launch (clock64, summed over lanes; the
+        # instrumentation itself adds ~10 % of wave-cycles): where one path-bounce's wave-cycles go
+        ph = ("load", "body", "shadow", "closest", "head", "store")
+        roof["bounce_profile"] = {
+            "path_bounces": nbb,
+            "cycles_per_bounce": {k: round(calib[f"bounce_cycles_{k}"] / nbb, 1) for k in ph},
+            "source": "wf_bounce_rr calibration launch (collect_stats), clock64 per phase"}
     return roof
 
 

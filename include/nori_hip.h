@@ -323,6 +323,11 @@ typedef struct nh_render_stats {
        carried by a 16-lane group once <= 4 remain in its wave): the latency of one bounce of the last chains */
     uint64_t tail_coop_cycles_body, tail_coop_cycles_shadow, tail_coop_cycles_closest, tail_coop_cycles_head;
     uint64_t tail_coop_bounces;
+    /* RR-ahead bounce kernel (wf_bounce_rr), collect_stats only: cycles its lanes spent loading the path (state and
+       the Intersection of its hit), in the body, the any-hit query, the closest hit, the head and ranking + storing
+       the survivors (clock64, summed over lanes), and the path-bounces it ran */
+    uint64_t bounce_cycles_load, bounce_cycles_body, bounce_cycles_shadow, bounce_cycles_closest, bounce_cycles_head;
+    uint64_t bounce_cycles_store, bounce_bounces;
 } nh_render_stats;
 
 typedef struct nh_scene nh_scene;

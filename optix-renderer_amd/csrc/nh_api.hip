@@ -1914,6 +1914,13 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
         c->stats.tail_coop_cycles_closest += h[kStatTailCoopClk + 2];
         c->stats.tail_coop_cycles_head += h[kStatTailCoopClk + 3];
         c->stats.tail_coop_bounces += h[kStatTailCoopClk + 4];
+        c->stats.bounce_cycles_load += h[kStatBounceClk];
+        c->stats.bounce_cycles_body += h[kStatBounceClk + 1];
+        c->stats.bounce_cycles_shadow += h[kStatBounceClk + 2];
+        c->stats.bounce_cycles_closest += h[kStatBounceClk + 3];
+        c->stats.bounce_cycles_head += h[kStatBounceClk + 4];
+        c->stats.bounce_cycles_store += h[kStatBounceClk + 5];
+        c->stats.bounce_bounces += h[kStatBounceClk + 6];
         const unsigned long long *cl = h, *an = h + kStatAny, *tc = h + kStatTail, *ta = h + kStatTailAny;
         c->stats.ray_queries += cl[0] + an[0] + tc[0] + ta[0];
         c->stats.nodes_visited += cl[1] + an[1] + tc[1] + ta[1];

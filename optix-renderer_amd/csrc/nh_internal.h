@@ -90,10 +90,13 @@ struct DenoiseLaunch {
 // [4] invalid samples, [8-11] the any-hit share, [16-19] / [20-23] the closest / any-hit work of
 // the tail kernel, one copy per XCD (workgroup b adds to copy b % 8) so the per-wave atomics of
 // concurrent workgroups do not serialise on one address.
-constexpr int kStatShards = 8, kStatStride = 40, kStatAny = 8, kStatTail = 16, kStatTailAny = 20;
+constexpr int kStatShards = 8, kStatStride = 48, kStatAny = 8, kStatTail = 16, kStatTailAny = 20;
 // wf_tail_rr calibration clocks: 4 phase cycle sums, path-bounces, longest chain (max over shards)
 constexpr int kStatTailClk = 24;
 constexpr int kStatTailCoopClk = 32;  // [32-35] the same phases for bounces carried by lane groups, [36] their count
+// wf_bounce_rr calibration clocks: [40-45] cycle sums of its phases (load, body, shadow, closest, head, store),
+// [46] the path-bounces it ran
+constexpr int kStatBounceClk = 40;
 __device__ __forceinline__ unsigned long long *stat_shard(unsigned long long *c) {
     return c + (blockIdx.x & (kStatShards - 1)) * kStatStride;
 }

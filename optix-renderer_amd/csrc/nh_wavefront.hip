@@ -1176,14 +1176,22 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScen
     PathV v;
     Hit h;
     int cls = kMatClasses - 1;
+    // STATS (calibration launch): clock64 per phase -- load (path state + its hit's Intersection, or the camera
+    // ray and its closest hit at bounce 0), then rr_step's body / shadow / closest / head, then rank + store
+    TailClocks clk;
+    unsigned long long c_load = 0, c_store = 0, t_ph = 0;
     if (q < qv.n) {
         const int s = queue_slot(qv.pre, L.seg_cap, q);
         Its its;
         bool alive = true;
+        if constexpr (STATS) t_ph = clock64();
         if (L.first) alive = first_vertex<ORDERED, STATS>(S, tv, L, s, v, h, its, my_stk, 256, st_e, q_e);
         else load_post_head(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
-        if (alive) cont = rr_step<ORDERED, STATS, false, 1, FULL>(S, tv, L, v, its, h, my_stk, 256, st_e, st_s, q_e, q_s);
+        if constexpr (STATS) c_load = clock64() - t_ph;
+        if (alive) cont = rr_step<ORDERED, STATS, STATS, 1, FULL>(S, tv, L, v, its, h, my_stk, 256, st_e, st_s, q_e,
+                                                                  q_s, &clk);
         if (cont) cls = prim_material(tv.prims[3 * h.k + 2]);  // a live path's ray has hit something
+        if constexpr (STATS) t_ph = clock64();
     }
     int rank = 0;  // survivors ranked by the material class of their hit (sorted queue) or in lane order
     if (SORT) {
@@ -1208,8 +1216,15 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScen
     __syncthreads();
     if (cont) store_post_head(L.st.buf[1 - L.in_q], shard * L.seg_cap + (int)(s_base + s_off[cls]) + rank, v, h);
     if (STATS) {
+        if (q < qv.n) c_store = clock64() - t_ph;
         flush_trav_stats(stat_shard(L.counters), q_e, st_e);
         flush_trav_stats(stat_shard(L.counters) + kStatAny, q_s, st_s);
+        unsigned long long *dst = stat_shard(L.counters) + kStatBounceClk;
+        for (int j = 0; j < 7; ++j) {
+            unsigned long long x = j == 0 ? c_load : j < 5 ? clk.c[j - 1] : j == 5 ? c_store : clk.bounces;
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            if ((threadIdx.x & 63) == 0) atomicAdd(&dst[j], x);
+        }
     }
 }
 

@@ -166,7 +166,9 @@ class nh_render_stats(C.Structure):
         (n, C.c_uint64) for n in ("tail_cycles_body", "tail_cycles_shadow", "tail_cycles_closest", "tail_cycles_head",
                                   "tail_bounces", "tail_max_bounces", "tail_coop_cycles_body",
                                   "tail_coop_cycles_shadow", "tail_coop_cycles_closest", "tail_coop_cycles_head",
-                                  "tail_coop_bounces")]
+                                  "tail_coop_bounces", "bounce_cycles_load", "bounce_cycles_body",
+                                  "bounce_cycles_shadow", "bounce_cycles_closest", "bounce_cycles_head",
+                                  "bounce_cycles_store", "bounce_bounces")]
 
 
 def _sig(name, res, *args):
