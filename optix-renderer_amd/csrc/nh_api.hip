@@ -1396,6 +1396,29 @@ static int pool_handoff(nh_ctx *c, WfPool &p, WfPool &T, int bound, hipEvent_t *
     return NH_OK;
 }
 
+// NH_COUNT_KERNEL=0: the runtime's device-to-host copy and memset per bounce instead of wf_counts_kernel (A/B)
+static bool count_kernel() {
+    static const bool on = [] {
+        const char *e = std::getenv("NH_COUNT_KERNEL");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// after bounce `it`'s appending kernel: its output counts (slot `out`) to the pinned ring, its input slot `in_slot`
+// (the next bounce's output) cleared, then the event the host polls before reading the ring
+static int count_service(nh_ctx *c, WfPool &p, unsigned *out, unsigned *in_slot, int it) {
+    unsigned *h = p.h_counts + (size_t)(it % kRing) * 2 * kCountGroup;
+    if (count_kernel()) {
+        nh::launch_wf_counts(out, h, 2 * kCountGroup, in_slot, kCountSlot, p.stream);
+        HIP_TRY(c, hipGetLastError());
+    } else {
+        HIP_TRY(c, hipMemcpyAsync(h, out, 2 * kCountGroup * sizeof(unsigned), hipMemcpyDeviceToHost, p.stream));
+    }
+    HIP_TRY(c, hipEventRecord(p.copy_ev[it % kRing], p.stream));
+    return NH_OK;
+}
+
 // enqueue bounce p.it (extend, any-hit, then shade or, once few paths are left, the tail kernel)
 static int pool_enqueue(nh_ctx *c, WfPool &p) {
     WfLaunch &L = p.L;
@@ -1415,7 +1438,9 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
     // has read the counts up to bounce it-2)
     const int bound = (int)p.in_e[it == 0 ? 0 : it - 1];
     const bool ordered = p.job.ordered, stats = p.job.stats;
-    HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), p.stream));
+    // this bounce's output slot must start at zero: bounce 0's is cleared here, every later one by the count
+    // kernel of the bounce before it (count_service)
+    if (it == 0 || !count_kernel()) HIP_TRY(c, hipMemsetAsync(slot[in ^ 1], 0, kCountSlot * sizeof(unsigned), p.stream));
     HIP_TRY(c, hipEventRecord(ev[0], p.stream));
     if (p.fused) {  // one kernel per bounce: its input already carries the hits (and no pending light samples)
         if (it > 0 && (int64_t)bound <= p.tail_at)
@@ -1437,9 +1462,7 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
         else nh::launch_wf_bounce(c->d_scene, c->tv, L, ordered, stats, p.sorted, bound, p.stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], p.stream));
-        unsigned *h = p.h_counts + (size_t)(it % kRing) * 2 * kCountGroup;
-        HIP_TRY(c, hipMemcpyAsync(h, slot[in ^ 1], 2 * kCountGroup * sizeof(unsigned), hipMemcpyDeviceToHost, p.stream));
-        HIP_TRY(c, hipEventRecord(p.copy_ev[it % kRing], p.stream));
+        if (int rc_ = count_service(c, p, slot[in ^ 1], slot[in], it)) return rc_;
         if (it == 0) p.it = 1;
         else p.state = WfPool::COUNTS;
         return NH_OK;
@@ -1469,9 +1492,7 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
     nh::launch_wf_shade(c->d_scene, c->tv, L, p.shade_sorted, bound, p.stream);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(ev[3], p.stream));
-    unsigned *h = p.h_counts + (size_t)(it % kRing) * 2 * kCountGroup;
-    HIP_TRY(c, hipMemcpyAsync(h, slot[in ^ 1], 2 * kCountGroup * sizeof(unsigned), hipMemcpyDeviceToHost, p.stream));
-    HIP_TRY(c, hipEventRecord(p.copy_ev[it % kRing], p.stream));
+    if (int rc_ = count_service(c, p, slot[in ^ 1], slot[in], it)) return rc_;
     if (it == 0) {
         p.it = 1;  // bounce 1 is sized by bounce 0's input: enqueue it before reading any count
     } else {

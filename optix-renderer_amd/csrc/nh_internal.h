@@ -203,4 +203,6 @@ void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaun
                     bool wide, int bound, int depth, hipStream_t st);
 // copies the live RR-ahead paths of L's input queue (at most bound) densely into dst, count into dst_counts[0]
 void launch_wf_pack_rr(const WfLaunch &L, const WfBuf &dst, unsigned *dst_counts, int bound, hipStream_t st);
+// n_copy count words src -> host_dst (pinned, device-visible), then n_zero words of zero cleared (wf_counts_kernel)
+void launch_wf_counts(const unsigned *src, unsigned *host_dst, int n_copy, unsigned *zero, int n_zero, hipStream_t st);
 }  // namespace nh

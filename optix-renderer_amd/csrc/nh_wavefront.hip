@@ -1331,6 +1331,19 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
 // Asynchronous tail hand-off: the chunk's live paths (RR-ahead state, 88 B each) are copied into a small buffer
 // of their own, densely from slot 0 (all in count shard 0; the other shards and groups are zeroed by the host),
 // so the pool's path state is free for the next chunk while this chunk's tail kernel runs on another stream.
+#if !defined(NH_WF_PART) || NH_WF_PART == 1  // non-template kernels: defined in one part only
+// After a bounce's appending kernel: its output counts (n_copy words) to the pool's pinned host ring, and the
+// count slot its input came from (dead now, the next bounce's output) zeroed -- one kernel in place of the
+// runtime's two blit kernels (a device-to-host copy and a memset) per bounce. The host reads the ring once the
+// event recorded after this kernel has completed: system-scope stores, then a system fence.
+__global__ __launch_bounds__(256) void wf_counts_kernel(const unsigned *src, unsigned *host_dst, int n_copy,
+                                                        unsigned *zero, int n_zero) {
+    for (int i = threadIdx.x; i < n_copy; i += 256)
+        __hip_atomic_store(&host_dst[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int i = threadIdx.x; i < n_zero; i += 256) zero[i] = 0u;
+    __threadfence_system();
+}
+#endif
 #if !defined(NH_WF_PART) || NH_WF_PART == 1  // a non-template kernel: defined in one part only
 __global__ __launch_bounds__(256) void wf_pack_rr(WfLaunch L, WfBuf dst, unsigned *dst_counts) {
     const QView qv = queue_view(L.cnt_in);
@@ -1595,6 +1608,10 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
 #endif
 
 #if NH_WF_HAS_PART(1)
+void launch_wf_counts(const unsigned *src, unsigned *host_dst, int n_copy, unsigned *zero, int n_zero, hipStream_t st) {
+    hipLaunchKernelGGL(wf_counts_kernel, dim3(1), dim3(256), 0, st, src, host_dst, n_copy, zero, n_zero);
+}
+
 void launch_wf_pack_rr(const WfLaunch &L, const WfBuf &dst, unsigned *dst_counts, int bound, hipStream_t st) {
     hipLaunchKernelGGL(wf_pack_rr, dim3(std::max(1, (bound + 255) / 256)), dim3(256), 0, st, L, dst, dst_counts);
 }
