@@ -515,6 +515,32 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         if ((rc = upload(c, c->scene_bufs, e.rgba, 4 * texels, &rgba))) return rc;
         S.env_rgba = reinterpret_cast<const float4 *>(rgba);
         if ((rc = upload(c, c->scene_bufs, e.cdf, texels + 1, &S.env_cdf))) return rc;
+        // guide table of the CDF search (nh_device.h dpdf_sample_guided): guide[j] = the first index i in [0, n]
+        // with !(cdf[i] < j / 2^bits) (n + 1 if none), the same float comparison as the device's search; about 4
+        // texels per bracket (NH_ENV_GUIDE=0: the plain search)
+        S.env_guide = nullptr;
+        S.env_guide_bits = 0;
+        // (only for a non-decreasing CDF without NaN, where the first entry not below x is monotone in x)
+        bool monotone = true;
+        for (size_t i = 0; i <= texels && monotone; ++i)
+            monotone = !std::isnan(e.cdf[i]) && (i == 0 || !(e.cdf[i] < e.cdf[i - 1]));
+        if (monotone && texels >= 64 && !(std::getenv("NH_ENV_GUIDE") && std::getenv("NH_ENV_GUIDE")[0] == '0')) {
+            int bits = 0;
+            while (bits < 20 && ((size_t)1 << (bits + 2)) < texels) ++bits;
+            const size_t M = (size_t)1 << bits;
+            std::vector<int> guide(M + 1);
+            size_t i = 0;
+            for (size_t j = 0; j <= M; ++j) {
+                const float t = (float)((double)j / (double)M);  // exact: j / 2^bits
+                while (i <= texels && e.cdf[i] < t) ++i;
+                guide[j] = (int)i;
+            }
+            const int *g = nullptr;
+            if ((rc = upload(c, c->scene_bufs, guide.data(), guide.size(), &g))) return rc;
+            HIP_TRY(c, hipStreamSynchronize(c->stream));  // (guide is a local)
+            S.env_guide = g;
+            S.env_guide_bits = bits;
+        }
         S.env_w = e.width;
         S.env_h = e.height;
         S.env_spherical = e.spherical;
@@ -1257,6 +1283,9 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     // traverse faster with one ray per lane
     p.persistent = c->depth > 20;
     if (const char *e = std::getenv("NH_PERSISTENT")) p.persistent = e[0] == '1';
+    // the persistent kernels generate pinhole camera rays only (camera_ray<false>: the lens arithmetic spilled their
+    // refill code): thin-lens scenes trace with one ray per lane
+    if (c->S.dof) p.persistent = false;
     // the persistent kernels walk the 4-wide collapse of the tree (half the dependent node fetches)
     // unless the reference's own visit order was asked for
     p.wide = p.persistent && j.ordered && c->tv.wnodes != nullptr;

@@ -209,7 +209,9 @@ __device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e,
                                              ESample &es) {
     if (e.type == EMITTER_ENVMAP) {  // EnvMap::sample (environmentmap.cpp:73-101)
         const unsigned W = (unsigned)S.env_w, H = (unsigned)S.env_h;
-        const unsigned elem = (unsigned)dpdf_sample(S.env_cdf, (int)(W * H), sx);
+        const unsigned elem = (unsigned)(S.env_guide ? dpdf_sample_guided(S.env_cdf, (int)(W * H), sx, S.env_guide,
+                                                                          S.env_guide_bits)
+                                                     : dpdf_sample(S.env_cdf, (int)(W * H), sx));
         const float i = (int)(elem / W) / (float)H, j = (int)(elem % W) / (float)W;
         const F3 v = (W == 1 && H == 1) ? uniform_sphere(sx, sy) : spherical_direction(j * kPi, i * 2.0f * kPi);
         es.p = f3(v.x * 1.f / kEps, v.y * 1.f / kEps, v.z * 1.f / kEps);
@@ -296,8 +298,27 @@ NHD void lens_uniform(const DScene &S, int round, int pix, float &u, float &v) {
     v = r.next1d();
 }
 
+// The thin-lens part of sampleRay (perspective.cpp:120-130): the local ray's origin on the lens and its direction
+// through the focal point
+__device__ __forceinline__ void camera_lens(const DScene &S, int round, int pix, F3 dl, F3 &lo, F3 &ld) {
+    float su, sv;
+    lens_uniform(S, round, pix, su, sv);
+    // squareToUniformDisk (warp.cpp:48-52)
+    const float rho = f_sqrt(su), theta = sv * 2.0f * kPi;
+    float st, ct;
+    f_sincos(theta, st, ct);
+    const float lx = S.lens_radius * (rho * ct), ly = S.lens_radius * (rho * st);
+    const float ft = S.focal_distance / dl.z;
+    // pFocus = ray(ft) = o + ft * d with o = 0 (ray.h:80)
+    const F3 pf = f3(0.0f + ft * dl.x, 0.0f + ft * dl.y, 0.0f + ft * dl.z);
+    lo = f3(lx, ly, 0.f);
+    ld = normalized(f3(pf.x - lo.x, pf.y - lo.y, pf.z - lo.z));
+}
+
 // PerspectiveCamera::sampleRay (perspective.cpp:97-141); `round` and `pix` place the ray in the serial order of the
-// lens samples (used only with depth of field)
+// lens samples (used only with depth of field). DOF = false: the pinhole path alone, for the persistent traversal
+// kernels, whose refill code the lens arithmetic pushed into spills (the host never runs them on a DOF scene)
+template <bool DOF = true>
 __device__ __forceinline__ void camera_ray(const DScene &S, float px, float py, F3 &o, F3 &d, float &mint,
                                            float &maxt, int round, int pix) {
     const float in0 = px * S.inv_w, in1 = py * S.inv_h;
@@ -312,20 +333,7 @@ __device__ __forceinline__ void camera_ray(const DScene &S, float px, float py, 
     }
     const F3 dl = normalized(f3(r[0] / r[3], r[1] / r[3], r[2] / r[3]));
     F3 lo = f3(0.0f, 0.0f, 0.0f), ld = dl;  // local ray
-    if (S.dof) {
-        float su, sv;
-        lens_uniform(S, round, pix, su, sv);
-        // squareToUniformDisk (warp.cpp:48-52)
-        const float rho = f_sqrt(su), theta = sv * 2.0f * kPi;
-        float st, ct;
-        f_sincos(theta, st, ct);
-        const float lx = S.lens_radius * (rho * ct), ly = S.lens_radius * (rho * st);
-        const float ft = S.focal_distance / dl.z;
-        // pFocus = ray(ft) = o + ft * d with o = 0 (ray.h:80)
-        const F3 pf = f3(0.0f + ft * dl.x, 0.0f + ft * dl.y, 0.0f + ft * dl.z);
-        lo = f3(lx, ly, 0.f);
-        ld = normalized(f3(pf.x - lo.x, pf.y - lo.y, pf.z - lo.z));
-    }
+    if (DOF && S.dof) camera_lens(S, round, pix, dl, lo, ld);
     float ow[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

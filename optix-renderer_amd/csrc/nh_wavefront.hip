@@ -126,6 +126,7 @@ __device__ __forceinline__ void unpack_ray(float4 &ro, float4 &rd) {
 // pixel jitter, the unused aperture sample, PerspectiveCamera::sampleRay (perspective.cpp:97-141).
 // Bounce 0 evaluates it in place -- in the extend kernel for the ray, again in the shade kernel
 // for its state -- instead of a generate kernel writing ~100 B per path that both read back.
+template <bool DOF = true>
 __device__ __forceinline__ void camera_sample(const DScene &S, const WfLaunch &L, int p, Rng &rng, float4 &ro,
                                               float4 &rd, float &jx, float &jy) {
     const int k = p / L.n_list, i = p - k * L.n_list;
@@ -138,18 +139,19 @@ __device__ __forceinline__ void camera_sample(const DScene &S, const WfLaunch &L
     rng.next1d();
     F3 o, d;
     float mint, maxt;
-    camera_ray(S, (float)px + jx, (float)py + jy, o, d, mint, maxt, L.s0 + k, pix);
+    camera_ray<DOF>(S, (float)px + jx, (float)py + jy, o, d, mint, maxt, L.s0 + k, pix);
     ro = make_float4(o.x, o.y, o.z, mint);
     rd = make_float4(d.x, d.y, d.z, maxt);
 }
 
-// the ray of queue entry q / slot s of this bounce
+// the ray of queue entry q / slot s of this bounce (DOF: camera rays may be thin-lens ones, camera_ray)
+template <bool DOF = true>
 __device__ __forceinline__ void load_ray(const DScene &S, const WfLaunch &L, const WfBuf &B, int q, int s, float4 &ro,
                                          float4 &rd) {
     if (L.first) {  // dense queue: slot = path id
         Rng rng;
         float jx, jy;
-        camera_sample(S, L, q, rng, ro, rd, jx, jy);
+        camera_sample<DOF>(S, L, q, rng, ro, rd, jx, jy);
     } else {
         ro = B.ray_o[s];
         rd = B.ray_d[s];
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
                     ro = L.st.sh_o[slot];
                     rd = L.st.sh_d[slot];
                 } else {
-                    load_ray(S, L, B, q, slot, ro, rd);
+                    load_ray<false>(S, L, B, q, slot, ro, rd);  // (never a DOF scene, nh_api.hip)
                 }
                 // a zero BSDF direction (maxt = -inf) misses every primitive without a traversal
                 if (STATS && (ANY || rd.w >= ro.w)) ++queries;
@@ -495,7 +497,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
                     if (STATS) ++q_s;
                 } else {
                     slot = queue_slot(qe.pre, L.seg_cap, q);
-                    load_ray(S, L, B, q, slot, ro, rd);
+                    load_ray<false>(S, L, B, q, slot, ro, rd);  // (never a DOF scene, nh_api.hip)
                     // a zero BSDF direction (maxt = -inf) misses every primitive without a traversal
                     if (STATS && rd.w >= ro.w) ++q_e;
                 }

@@ -301,6 +301,21 @@ def test_render_parity_envmap(gpu, tmp_path, texture, integrator, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+def test_envmap_guide_table(gpu, tmp_path, monkeypatch, mode):
+    """EnvMap::sample's CDF search bracketed by the guide table (nh_device.h dpdf_sample_guided) gives the plain binary
+    search's texel: images with and without the table (NH_ENV_GUIDE=0) equal each other and the oracle, on a sky large
+    enough for a 2^12-entry table and with a hot spot (the bright sun: most samples land in a few brackets)."""
+    xml = scenegen.envmap_xml(str(tmp_path), texture="png", tex_size=(256, 128))
+    out = []
+    for guide in ("1", "0"):
+        monkeypatch.setenv("NH_ENV_GUIDE", guide)
+        g, r, s = render_pair(xml, 48, 32, 8, mode=mode, traversal=nh.TRAVERSAL_ORDERED)
+        out.append((g, r))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][0], out[0][1])
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_render_parity_black_envmap_mirror(gpu, tmp_path, mode):
     """An all-black PNG envmap (luminance table sums to 0: DiscretePDF's normalization 0) beside an area light and a
     mirror sphere. The reference's envmap light sample is then non-finite, so the light-sample skip at mirror hits
