@@ -21,7 +21,7 @@ HIP_FLAGS  := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) $(FP_FLAGS) \
               -Iinclude -I$(PKG)/csrc -Wno-unused-result $(EXTRA_HIP)
 
 HOST_SRC := $(PKG)/host/xml_lite.cpp $(PKG)/host/scene_loader.cpp $(PKG)/host/bvh_build.cpp $(PKG)/host/image_io.cpp \
-            $(PKG)/host/png_decode.cpp
+            $(PKG)/host/png_decode.cpp $(PKG)/host/hdr_decode.cpp
 HIP_SRC  := $(PKG)/csrc/nh_kernels.hip $(PKG)/csrc/nh_denoise.hip $(PKG)/csrc/nh_splat.hip $(PKG)/csrc/nh_api.hip
 HOST_OBJ := $(patsubst $(PKG)/host/%.cpp,$(OBJDIR)/host_%.o,$(HOST_SRC))
 # nh_wavefront.hip is compiled as four translation units (-DNH_WF_PART=k, each instantiating its own kernels) so

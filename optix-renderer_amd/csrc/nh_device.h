@@ -57,10 +57,17 @@ NHD void f_sincos(float xf, float &s_out, float &c_out) {
     s_out = (float)sv;
     c_out = (float)cv;
 }
+#ifndef NH_AB_FAST_TRANSC  // cost attribution builds only (scripts/build_variant.sh): fp32 library forms, NOT exact
 NHD float f_exp(float x) { return (float)exp((double)x); }
 NHD float f_log(float x) { return (float)log((double)x); }
 NHD float f_acos(float x) { return (float)acos((double)x); }
 NHD float f_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+#else
+NHD float f_exp(float x) { return expf(x); }
+NHD float f_log(float x) { return logf(x); }
+NHD float f_acos(float x) { return acosf(x); }
+NHD float f_atan2(float y, float x) { return atan2f(y, x); }
+#endif
 NHD float f_sqrt(float x) { return __builtin_sqrtf(x); }  // correctly rounded (HIP default)
 NHD float e_min(float a, float b) { return (b < a) ? b : a; }  // std::min
 NHD float e_max(float a, float b) { return (a < b) ? b : a; }  // std::max

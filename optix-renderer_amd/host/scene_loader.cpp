@@ -717,7 +717,11 @@ void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w
     const std::string ext = dot == std::string::npos ? std::string() : fn.substr(dot);
     // PNGTexture::loadFromFile's order (PNGTexture.cpp:63-72): existence first, then the extension
     if (!std::ifstream(fn).good()) throw SceneError("PNGTexture: image file not found " + fn);
-    if (ext == ".hdr") throw SceneError("PNGTexture: .hdr images (HDRLoader) are not supported by the HIP path");
+    if (ext == ".hdr") {  // PNGTexture.cpp:97-117: the HDRLoader's floats as they are (no gamma)
+        std::string err;
+        if (!hdr_decode_rgba(fn, out, w, h, err)) throw SceneError("Could not load HDR file... (" + err + ")");
+        return;
+    }
     if (ext != ".png") throw SceneError("PNGTexture: file extension " + ext + " unknown.");
     std::vector<uint8_t> px;
     std::string err;

@@ -205,6 +205,85 @@ def write_png(path: str, img: np.ndarray) -> None:
         f.write(chunk(b"IEND", b""))
 
 
+def rgbe_encode(rgb: np.ndarray) -> np.ndarray:
+    """float RGB (h, w, 3) -> RGBE bytes (h, w, 4): shared exponent of the largest channel, mantissas m such that
+    (m / 256) * 2^(e - 128) approximates each channel (any RGBE bytes are valid input for the decoder tests)."""
+    rgb = np.asarray(rgb, np.float64)
+    mx = rgb.max(axis=-1)
+    out = np.zeros(rgb.shape[:-1] + (4,), np.uint8)
+    nz = mx > 1e-32
+    e = np.floor(np.log2(mx[nz])) + 1
+    out[nz, 3] = np.clip(e + 128, 0, 255)
+    scale = 256.0 / np.exp2(out[nz, 3].astype(np.float64) - 128)
+    out[nz, :3] = np.clip(np.floor(rgb[nz] * scale[:, None]), 0, 255)
+    return out
+
+
+def write_hdr(path: str, rgbe: np.ndarray, mode: str = "rle", header: str = "FORMAT=32-bit_rle_rgbe") -> None:
+    """Radiance .hdr of RGBE bytes (h, w, 4) in one of the encodings HDRLoader reads (include/nori/HDRLoader.h):
+    rle   new-style scanlines (2, 2, w >> 8, w & 255, then each component as runs / literal chunks);
+    flat  plain RGBE pixels;
+    old   plain pixels with the old (1, 1, 1, n) repeat codes for runs of identical pixels (n << 8 chained for long
+          runs)."""
+    h, w, _ = rgbe.shape
+    out = bytearray(b"#?RADIANCE\n" + header.encode() + b"\n\n" + f"-Y {h} +X {w}\n".encode())
+    if mode == "rle" and not 8 <= w <= 0x7FFF:
+        raise ValueError("run-length scanlines need 8 <= width <= 0x7fff (HDRLoader.h:89-90)")
+    for y in range(h):
+        line = rgbe[y]
+        if mode == "rle":
+            out += bytes([2, 2, w >> 8, w & 255])
+            for c in range(4):
+                comp = line[:, c]
+                j = 0
+                while j < w:
+                    r = 1
+                    while j + r < w and r < 127 and comp[j + r] == comp[j]:
+                        r += 1
+                    if r >= 3:
+                        out += bytes([128 + r, int(comp[j])])
+                        j += r
+                    else:
+                        k = j
+                        while k < w and k - j < 128 and not (k + 2 < w and comp[k] == comp[k + 1] == comp[k + 2]):
+                            k += 1
+                        k = max(k, j + 1)
+                        out += bytes([k - j]) + bytes(int(v) for v in comp[j:k])
+                        j = k
+        elif mode == "flat":
+            out += line.astype(np.uint8).tobytes()
+        elif mode == "old":
+            x = 0
+            while x < w:
+                out += line[x].astype(np.uint8).tobytes()
+                r = 0
+                while x + 1 + r < w and (line[x + 1 + r] == line[x]).all():
+                    r += 1
+                x += 1
+                # runs of identical pixels: (1, 1, 1, n) repeats the previous pixel n times; a second code in a row
+                # counts n << 8 (HDRLoader.h oldDecrunch)
+                if r >= 2 and not (line[x - 1][:3] == 1).all():
+                    hi, lo = r >> 8, r & 255
+                    out += bytes([1, 1, 1, lo])  # (a zero count still shifts the next code by 8)
+                    if hi:
+                        out += bytes([1, 1, 1, hi])
+                    x += r
+        else:
+            raise ValueError(mode)
+    with open(path, "wb") as f:
+        f.write(bytes(out))
+
+
+def rgbe_decode_reference(rgbe: np.ndarray) -> np.ndarray:
+    """HDRLoader's floats (HDRLoader.h:27-44) of RGBE bytes: (m / 256.0f) * (float)pow(2, e - 128), alpha 0 -- float32
+    arithmetic as the reference's."""
+    m = rgbe[..., :3].astype(np.float32) / np.float32(256.0)
+    d = np.exp2(rgbe[..., 3:4].astype(np.float64) - 128.0).astype(np.float32)
+    out = np.zeros(rgbe.shape[:-1] + (4,), np.float32)
+    out[..., :3] = m * d
+    return out
+
+
 def sky_image(width: int, height: int, seed: int = 7) -> np.ndarray:
     """Synthetic lat-long sky (rows = polar angle), uint8 RGB."""
     rng = np.random.default_rng(seed)
@@ -224,8 +303,8 @@ def envmap_xml(out_dir: str, width: int = 64, height: int = 48, spp: int = 16, t
                tex_size=(96, 48), spherical: bool = True, area_light: bool = True, integrator: str = "path_mis",
                mesh: str | None = None, euler=None, black: bool = False) -> str:
     """Open scene lit by an envmap (+ optionally a small area light): a ground quad, a diffuse
-    and a microfacet sphere, a mirror sphere. texture: png | constant | none (EnvMap's 0.5
-    fallback). mesh: optional OBJ path added with a diffuse BSDF. euler: the png_texture's eulerAngles
+    and a microfacet sphere, a mirror sphere. texture: png | hdr | constant | none (EnvMap's 0.5
+    fallback); hdr is a Radiance RGBE sky (.hdr, run-length scanlines). mesh: optional OBJ path added with a diffuse BSDF. euler: the png_texture's eulerAngles
     (degrees) of the spherical lookup. black: an all-black PNG (its luminance table sums to 0)."""
     os.makedirs(out_dir, exist_ok=True)
     tex_xml = ""
@@ -238,6 +317,15 @@ def envmap_xml(out_dir: str, width: int = 64, height: int = 48, spp: int = 16, t
       <string name="filename" value="{os.path.basename(png)}"/>
       <boolean name="sphericalTexture" value="{'true' if spherical else 'false'}"/>
       {f'<vector name="eulerAngles" value="{euler[0]},{euler[1]},{euler[2]}"/>' if euler else ''}
+    </texture>"""
+    elif texture == "hdr":  # a Radiance RGBE sky (PNGTexture's .hdr branch)
+        hdr = os.path.join(out_dir, f"sky_{tex_size[0]}x{tex_size[1]}.hdr")
+        if not os.path.exists(hdr):
+            sky = sky_image(*tex_size).astype(np.float64) / 255.0 * 3.0
+            write_hdr(hdr, rgbe_encode(sky), mode="rle" if 8 <= tex_size[0] <= 0x7FFF else "flat")
+        tex_xml = f"""<texture type="png_texture" name="albedo">
+      <string name="filename" value="{os.path.basename(hdr)}"/>
+      <boolean name="sphericalTexture" value="{'true' if spherical else 'false'}"/>
     </texture>"""
     elif texture == "constant":
         tex_xml = '<texture type="constant_color" name="albedo"><color name="value" value="0.8 0.7 0.6"/></texture>'

@@ -288,10 +288,11 @@ def test_wavefront_matches_megakernel(gpu, tmp_path, monkeypatch):
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("texture,integrator", [("png", nh.INTEGRATOR_PATH_MIS), ("png", nh.INTEGRATOR_PATH_MATS),
-                                                ("constant", nh.INTEGRATOR_PATH_MIS),
+                                                ("hdr", nh.INTEGRATOR_PATH_MIS), ("constant", nh.INTEGRATOR_PATH_MIS),
                                                 ("none", nh.INTEGRATOR_PATH_MIS)])
 def test_render_parity_envmap(gpu, tmp_path, texture, integrator, mode):
-    """EnvMap emitter (NEE by luminance CDF, escaped-ray term) + png_texture lookups, GPU vs oracle."""
+    """EnvMap emitter (NEE by luminance CDF, escaped-ray term) + png_texture lookups (a PNG or a Radiance .hdr sky),
+    GPU vs oracle."""
     xml = scenegen.envmap_xml(str(tmp_path), texture=texture, tex_size=(96, 48))
     g, r, s = render_pair(xml, 64, 48, 8, integrator=integrator, mode=mode, traversal=nh.TRAVERSAL_ORDERED)
     e = rel_l2(g, r)

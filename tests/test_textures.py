@@ -205,7 +205,7 @@ def test_texture_loader_errors(tmp_path):
     d = str(tmp_path)
     png = os.path.join(d, "t.png")
     scenegen.write_png(png, np.full((4, 4, 4), 128, np.uint8))
-    open(png[:-4] + ".hdr", "wb").write(b"#?RADIANCE\n")  # an existing .hdr image: HDRLoader is not restated
+    open(png[:-4] + ".hdr", "wb").write(b"#?RADIANCE\n")  # a truncated .hdr image (test_hdr.py: the decoder)
     cases = {
         # an albedo colour already creates the albedo texture (diffuse.cpp:33-40, :75-79)
         '<bsdf type="diffuse"><color name="albedo" value="0.5,0.5,0.5"/><texture type="constant_color" name="albedo">'
@@ -213,7 +213,7 @@ def test_texture_loader_errors(tmp_path):
         '<bsdf type="diffuse"><texture type="constant_color" name="kd"><color name="value" value="1,1,1"/></texture>'
         '</bsdf>': "does not match any field",
         f'<bsdf type="diffuse"><texture type="png_texture" name="albedo"><string name="filename" value="{png[:-4]}.hdr"/>'
-        '</texture></bsdf>': ".hdr",
+        '</texture></bsdf>': "Could not load HDR file",
         '<bsdf type="diffuse"><texture type="png_texture" name="albedo"><string name="filename" value="nope.png"/>'
         '</texture></bsdf>': "image file not found",
         '<bsdf type="diffuse"><texture type="checkerboard_color" name="albedo"><vector name="scale" value="1,2,3,4"/>'
@@ -233,26 +233,26 @@ def test_texture_loader_errors(tmp_path):
 
 
 def aircraft_substituted(tex_dir):
-    """aircraft.xml with synthetic stand-ins for its two absent images (a random 128x64 aircraft_base.png, the
-    envmap pointed at a png sky); returns the scene file's path."""
+    """aircraft.xml with synthetic stand-ins for its two absent images, written where the scene expects them: a
+    random 128x64 res/aircraft_base.png and a 96x48 run-length Radiance sky as res/dikhololo_night_4k.hdr (so the
+    scene file loads unmodified); returns the scene file's path."""
     src = os.path.join(tex_dir, "scenes/project/textures/aircraft.xml")
     res = os.path.join(tex_dir, "scenes/project/res")
     os.makedirs(res, exist_ok=True)
     rng = np.random.default_rng(2)
     scenegen.write_png(os.path.join(res, "aircraft_base.png"), rng.integers(0, 256, (64, 128, 4), dtype=np.uint8))
-    scenegen.write_png(os.path.join(res, "sky_substitute.png"), scenegen.sky_image(96, 48))
-    text = open(src).read().replace("../res/dikhololo_night_4k.hdr", "../res/sky_substitute.png")
-    xml = os.path.join(os.path.dirname(src), "aircraft_substituted.xml")
-    open(xml, "w").write(text)
-    return xml
+    sky = scenegen.sky_image(96, 48).astype(np.float64) / 255.0 * 4.0
+    scenegen.write_hdr(os.path.join(res, "dikhololo_night_4k.hdr"), scenegen.rgbe_encode(sky), mode="rle")
+    return src
 
 
 def test_aircraft_scene(tex_dir, tmp_path):
     """scenes/project/textures/aircraft.xml: png_texture albedo on the aircraft body, glass dielectric, spherical
     envmap texture with eulerAngles (0, 270, 0). Its two images (res/aircraft_base.png, res/dikhololo_night_4k.hdr)
     are absent from the reference checkout, so it fails to load as the reference would (PNGTexture: image file not
-    found); with a synthetic aircraft_base.png and the envmap pointed at a synthetic png sky it loads, with the
-    reference's rotation (Eigen-pinned, test_transforms.py) and the aircraft's texture coordinates."""
+    found); with a synthetic aircraft_base.png and a synthetic Radiance sky in their places it loads, with the
+    reference's rotation (Eigen-pinned, test_transforms.py), the .hdr texels and the aircraft's texture
+    coordinates."""
     src = os.path.join(tex_dir, "scenes/project/textures/aircraft.xml")
     if not os.path.exists(os.path.join(tex_dir, "scenes/project/res/aircraft_base.png")):
         with pytest.raises(nh.NoriError, match="image file not found"):
@@ -261,7 +261,10 @@ def test_aircraft_scene(tex_dir, tmp_path):
     d = s.desc
     assert d.n_textures == 1 and d.textures[0].type == nh.TEXTURE_PNG and d.textures[0].spherical == 0
     assert (d.textures[0].width, d.textures[0].height) == (128, 64)
-    assert d.envmap >= 0 and d.env.spherical == 1
+    assert d.envmap >= 0 and d.env.spherical == 1 and (d.env.width, d.env.height) == (96, 48)
+    hdr = scenegen.rgbe_encode(scenegen.sky_image(96, 48).astype(np.float64) / 255.0 * 4.0)
+    np.testing.assert_array_equal(np.ctypeslib.as_array(d.env.rgba, shape=(48, 96, 4)),
+                                  scenegen.rgbe_decode_reference(hdr))
     rot = np.array(list(d.env.rotation), np.float32).reshape(3, 3)
     assert not np.array_equal(rot, np.eye(3, dtype=np.float32))  # eulerAngles (0, 270, 0): a rotation about x
     assert abs(abs(rot[1, 2]) - 1) < 1e-6 and abs(rot[0, 0] - 1) < 1e-6
