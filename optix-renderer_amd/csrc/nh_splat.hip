@@ -233,8 +233,12 @@ constexpr int kTabRG = 0, kTabBW = 2, kTabWX = 4, kTabWY = 9, kTabPlanes = 14;
 // (A read-modify-write of the framebuffer per round instead of the registers was built and spills past 256 VGPRs.)
 // JIT: the jitter read from P.jit (NH_SPLAT_JITTER=stored) instead of recomputed -- a template parameter: a runtime
 // choice between the two costs the recomputing kernel 6 % (profiles/round4_session9_10_splat_ab.txt)
-template <bool DIRECT, bool JIT = false>
+// T: workgroup threads. 256: 6-row strips, 4 phase-1 samples per thread; 512: 3-row strips, 2 samples per thread --
+// the same LDS per workgroup, half the registers per thread, so twice the waves per CU fit (NH_SPLAT_T512)
+template <bool DIRECT, bool JIT = false, int T = 256>
 __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *tab, int slot, int k0, int k1) {
+    constexpr int SR = T == 512 ? 3 : kStripRows, NS = 36 / SR, NQ = 1024 / T;
+    static_assert(SR * NS == 36 && NQ * T == 1024, "strip tiling");
     const int bid = P.blocks[slot];
     const int by = bid / P.nbx, bx = bid - by * P.nbx;
     const int ox = bx * 32, oy = by * 32;
@@ -243,38 +247,38 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
     if (threadIdx.x < 33) tab[threadIdx.x] = P.table[threadIdx.x];
     // the zero rows and column are never written again
     float2 *const W2 = reinterpret_cast<float2 *>(W);  // the pair planes, indexed like one float plane
-    for (int i = threadIdx.x; i < (kTabPlanes - kTabWX) * 40; i += 256) {
+    for (int i = threadIdx.x; i < (kTabPlanes - kTabWX) * 40; i += T) {
         const int p = kTabWX + i / 40, row = i % 40;
         W[p * kTabPlane + row * kTabRow + 32] = 0.f;
     }
-    for (int i = threadIdx.x; i < (kTabPlanes - kTabWX) * 8 * 32; i += 256) {
+    for (int i = threadIdx.x; i < (kTabPlanes - kTabWX) * 8 * 32; i += T) {
         const int p = kTabWX + (i >> 8), q = i & 255, row = q >> 5;
         W[p * kTabPlane + (row < 4 ? row : row + 32) * kTabRow + (q & 31)] = 0.f;
     }
-    for (int i = threadIdx.x; i < 2 * 40; i += 256) {  // pair planes: the zero column, then the zero rows
+    for (int i = threadIdx.x; i < 2 * 40; i += T) {  // pair planes: the zero column, then the zero rows
         const int p = i / 40, row = i % 40;
         W2[p * kTabPlane + row * kTabRow + 32] = make_float2(0.f, 0.f);
     }
-    for (int i = threadIdx.x; i < 2 * 8 * 32; i += 256) {
+    for (int i = threadIdx.x; i < 2 * 8 * 32; i += T) {
         const int p = i >> 8, q = i & 255, row = q >> 5;
         W2[p * kTabPlane + (row < 4 ? row : row + 32) * kTabRow + (q & 31)] = make_float2(0.f, 0.f);
     }
-    // phase-1 samples of this thread: (lx, ly) = (s & 31, s >> 5), s = threadIdx.x + 256 q (block rows are
+    // phase-1 samples of this thread: (lx, ly) = (s & 31, s >> 5), s = threadIdx.x + T q (block rows are
     // consecutive list entries: neighbouring lanes load neighbouring records)
-    int li[4];
-    F3 rec[4];
-    uint64_t hs[4];  // splitmix64(seed ^ pixel) of each sample's path stream: its jitter is recomputed per round
+    int li[NQ];
+    F3 rec[NQ];
+    uint64_t hs[NQ];  // splitmix64(seed ^ pixel) of each sample's path stream: its jitter is recomputed per round
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
+    for (int q = 0; q < NQ; ++q) {
+        const int s = threadIdx.x + T * q, lx = s & 31, ly = s >> 5;
         li[q] = (lx < sxb && ly < syb) ? P.pixel_map[(oy + ly) * P.width + (ox + lx)] : -1;
         hs[q] = splitmix64(P.seed ^ (uint64_t)((oy + ly) * P.width + (ox + lx)));
     }
-    float sjx[4], sjy[4];  // the round's jitter, formed with the record fetch (during the previous round's sums)
+    float sjx[NQ], sjy[NQ];  // the round's jitter, formed with the record fetch (during the previous round's sums)
     auto fetch = [&](int k) {
         const size_t rbase = (size_t)k * P.n_list;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < NQ; ++q) {
             if (li[q] >= 0) rec[q] = load_rec(P.rec, rbase + li[q]);
             if (JIT) {  // NH_SPLAT_JITTER=stored (A/B)
                 if (li[q] >= 0) {
@@ -289,10 +293,10 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
     };
     fetch(k0);
     // phase-2 strip of this thread: block-array column xt, rows yt0..yt0+5
-    const int seg = threadIdx.x / 36, xt = threadIdx.x - seg * 36, yt0 = seg * kStripRows;
+    const int seg = threadIdx.x / 36, xt = threadIdx.x - seg * 36, yt0 = seg * SR;
     const int mcols = P.width + 4, mrows = P.height + 4;
-    bool own[kStripRows];
-    float4 m[kStripRows];
+    bool own[SR];
+    float4 m[SR];
     float4 *const fb4 = reinterpret_cast<float4 *>(P.fb);
     // Pixels only this block covers (covering_blocks(..) == 1, the merge's test): inside the master and this
     // block's array, and not in the 4-pixel band a rendered neighbour's array also covers -- left / up neighbours
@@ -308,10 +312,10 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
     }
     const int cx = xt < 4 ? 0 : xt >= 32 ? 2 : 1;  // the column's band: left / none / right
 #pragma unroll
-    for (int j = 0; j < kStripRows; ++j) {
+    for (int j = 0; j < SR; ++j) {
         own[j] = false;
         m[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (DIRECT && threadIdx.x < 36 * 6) {
+        if (DIRECT && threadIdx.x < 36 * NS) {
             const int yt = yt0 + j, mx = ox + xt, my = oy + yt;  // block-array position -> master pixel
             const int cy = yt < 4 ? 0 : yt >= 32 ? 2 : 1;
             // neighbours whose array holds this pixel: the column band's, the row band's and their corner
@@ -327,8 +331,8 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
     for (int k = k0; k < k1; ++k) {
         __syncthreads();  // the previous round's phase 2 is done with W (and tab / zero rows are in place)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int s = threadIdx.x + 256 * q, lx = s & 31, ly = s >> 5;
+        for (int q = 0; q < NQ; ++q) {
+            const int s = threadIdx.x + T * q, lx = s & 31, ly = s >> 5;
             float v[3] = {0.f, 0.f, 0.f}, wx[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, wy[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
             if (li[q] >= 0 && is_valid(rec[q])) {  // invalid samples drop with their weight
                 const float spx = (float)(ox + lx) + sjx[q], spy = (float)(oy + ly) + sjy[q];
@@ -354,10 +358,10 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
         }
         __syncthreads();
         if (k + 1 < k1) fetch(k + 1);  // in flight during phase 2
-        if (threadIdx.x < 36 * 6) {
-            sf2 rg[kStripRows], bw[kStripRows];
+        if (threadIdx.x < 36 * NS) {
+            sf2 rg[SR], bw[SR];
 #pragma unroll
-            for (int j = 0; j < kStripRows; ++j) {
+            for (int j = 0; j < SR; ++j) {
                 rg[j] = sf2{0.f, 0.f};
                 bw[j] = sf2{0.f, 0.f};
             }
@@ -368,18 +372,19 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
                 const float *base = W + yt0 * kTabRow + ((unsigned)lx < 32u ? lx : 32);
                 const float2 *base2 = W2 + yt0 * kTabRow + ((unsigned)lx < 32u ? lx : 32);
 #pragma unroll
-                for (int i0 = 0; i0 < kStripRows + 4; i0 += 2) {  // sample rows i0, i0 + 1 (ly = yt0 - 4 + i)
+                for (int i0 = 0; i0 < SR + 4; i0 += 2) {  // sample rows i0, i0 + 1 (ly = yt0 - 4 + i)
                     // each row weight of the two rows as one register pair (rows i0 and i0+1 of its plane): the
                     // products take it with the half selected in the instruction (pk_mul_lo / pk_mul_hi)
                     sf2 wyp[5];
 #pragma unroll
                     for (int dy = 0; dy < 5; ++dy) {
                         const float *w = base + i0 * kTabRow + (kTabWY + dy) * kTabPlane;
-                        wyp[dy] = sf2{w[0], w[kTabRow]};
+                        wyp[dy] = sf2{w[0], i0 + 1 < SR + 4 ? w[kTabRow] : w[0]};  // (odd SR + 4: no row past)
                     }
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        const int i = i0 + h;  // sample row ly = yt0 - 4 + i (plane row yt0 + i)
+                        const int i = i0 + h;
+                        if (i >= SR + 4) continue;  // sample row ly = yt0 - 4 + i (plane row yt0 + i)
                         const float *w = base + i * kTabRow;
                         const float wx = w[(kTabWX + 4 - e) * kTabPlane];
                         const float2 prg = base2[i * kTabRow], pbw = base2[kTabPlane + i * kTabRow];
@@ -388,7 +393,7 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
 #pragma unroll
                         for (int dy = 0; dy < 5; ++dy) {  // row offset dy of the sample: strip row i - 4 + dy
                             const int j = i - 4 + dy;
-                            if (j < 0 || j >= kStripRows) continue;
+                            if (j < 0 || j >= SR) continue;
                             rg[j] += h ? pk_mul_hi(vrg, wyp[dy]) : pk_mul_lo(vrg, wyp[dy]);
                             bw[j] += h ? pk_mul_hi(vbw, wyp[dy]) : pk_mul_lo(vbw, wyp[dy]);
                         }
@@ -397,7 +402,7 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
             }
             float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(36 * stage_pitch(36));
 #pragma unroll
-            for (int j = 0; j < kStripRows; ++j) {
+            for (int j = 0; j < SR; ++j) {
                 if (DIRECT && own[j]) {  // round k of a pixel only this block covers: the master, in round order
                     m[j].x += rg[j].x;
                     m[j].y += rg[j].y;
@@ -411,22 +416,22 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
     }
     if (DIRECT)
 #pragma unroll
-        for (int j = 0; j < kStripRows; ++j)
+        for (int j = 0; j < SR; ++j)
             if (own[j]) fb4[(size_t)(oy + yt0 + j) * mcols + ox + xt] = m[j];
 }
 
-template <bool DIRECT, int ROUNDS = kTabRounds, bool JIT = false, bool PERSIST = false>
-__global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) {
+template <bool DIRECT, int ROUNDS = kTabRounds, bool JIT = false, bool PERSIST = false, int T = 256>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 128))) void nh_block_splat_tab_kernel(SplatLaunch P) {
     __shared__ float W[kTabPlanes * kTabPlane];
     __shared__ float tab[33];
     if (DIRECT) {
-        tab_body<true, JIT>(P, W, tab, blockIdx.x, 0, P.n_rounds);
+        tab_body<true, JIT, T>(P, W, tab, blockIdx.x, 0, P.n_rounds);
         return;
     }
     if (!PERSIST) {
         const int k0 = blockIdx.y * ROUNDS, k1 = min(k0 + ROUNDS, P.n_rounds);
-        if (P.direct > 0 && blockIdx.y == 0) tab_body<true, JIT>(P, W, tab, blockIdx.x, k0, k1);
-        else tab_body<false, JIT>(P, W, tab, blockIdx.x, k0, k1);
+        if (P.direct > 0 && blockIdx.y == 0) tab_body<true, JIT, T>(P, W, tab, blockIdx.x, k0, k1);
+        else tab_body<false, JIT, T>(P, W, tab, blockIdx.x, k0, k1);
         return;
     }
     // PERSIST: a grid of P.persist workgroups walks the (block, round group) items, so the splat holds the LDS of
@@ -437,8 +442,8 @@ __global__ __launch_bounds__(256) void nh_block_splat_tab_kernel(SplatLaunch P) 
         const int slot = v % P.n_blocks, grp = v / P.n_blocks;
         __syncthreads();  // the previous item's sums are done with W before it is set up again
         const int k0 = grp * ROUNDS, k1 = min(k0 + ROUNDS, P.n_rounds);
-        if (P.direct > 0 && grp == 0) tab_body<true, JIT>(P, W, tab, slot, k0, k1);
-        else tab_body<false, JIT>(P, W, tab, slot, k0, k1);
+        if (P.direct > 0 && grp == 0) tab_body<true, JIT, T>(P, W, tab, slot, k0, k1);
+        else tab_body<false, JIT, T>(P, W, tab, slot, k0, k1);
     }
 }
 
@@ -854,10 +859,15 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
         Q.persist = pw ? std::max(0, std::atoi(pw)) : 0;
         if (all_direct || tr != 8 || P.jit) Q.persist = 0;  // the persistent grid: default grouping only
         if (Q.persist) g = dim3(std::min<unsigned>((unsigned)Q.persist, g.x * g.y), 1);
+        const bool t512 = splat_knob("NH_SPLAT_T512");  // 512-thread workgroups, 3-row strips (0: 256, 6-row)
         if (P.jit) {
             if (all_direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true, 8, true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
             else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8, true>), g, dim3(256), 0, st, Q);
         }
+        else if (t512 && all_direct)
+            hipLaunchKernelGGL((nh_block_splat_tab_kernel<true, 8, false, false, 512>), dim3(P.n_blocks, 1), dim3(512), 0, st, Q);
+        else if (t512 && tr == 8 && !Q.persist)
+            hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8, false, false, 512>), g, dim3(512), 0, st, Q);
         else if (all_direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
         else if (tr == 1) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 1>), g, dim3(256), 0, st, Q);
         else if (tr == 2) hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 2>), g, dim3(256), 0, st, Q);
