@@ -783,6 +783,28 @@ __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
             }
         }
     }
+    // pixels of the 4-pixel bands (2-4 covering blocks): four rounds' loads of every block in flight, then added in
+    // the same order as the loop below (rounds in order, blocks in spiral order within a round)
+#ifndef NH_AB_MERGE_SERIAL
+    for (; nb > 1 && k + 4 <= P.n_rounds; k += 4) {
+        float4 v[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (q < nb) v[j][q] = P.staging[(size_t)(k + j) * per_round + (size_t)slot[q] * blk + off[q]];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (q < nb) {
+                    m.x += v[j][q].x;
+                    m.y += v[j][q].y;
+                    m.z += v[j][q].z;
+                    m.w += v[j][q].w;
+                }
+    }
+#endif
     for (; k < P.n_rounds; ++k) {
         const float4 *base = P.staging + (size_t)k * per_round;
         for (int q = 0; q < nb; ++q) {
