@@ -867,8 +867,10 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
     Q.direct = 0;
     Q.band = tabulated && P.border == 2 && P.reach == 2 ? 1 : 0;  // the layout the tab kernel writes
     if (tabulated && P.border == 2 && P.reach == 2) {
-        const char *d = std::getenv("NH_SPLAT_DIRECT");  // opt-in until measured
-        const bool all_direct = d && d[0] == '1';
+        // one workgroup per block takes all the chunk's rounds of the pixels only that block covers (default since
+        // round 5: with 512-thread workgroups it beats the lead split on C1 / C2 / C4, and stages only the 4-pixel
+        // bands: 0.54 vs 0.77 GB per C2 chunk); NH_SPLAT_DIRECT=0 restores the per-round-group workgroups
+        const bool all_direct = splat_knob("NH_SPLAT_DIRECT");
         const char *rv = std::getenv("NH_SPLAT_ROUNDS");  // rounds per workgroup: 1, 2, 4 or 8 (default)
         int tr = rv ? std::atoi(rv) : kTabRounds;
         if (tr != 1 && tr != 2 && tr != 4 && tr != 8) tr = kTabRounds;  // 0 / garbage: the default (no 0 divisor)

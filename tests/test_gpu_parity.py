@@ -218,9 +218,9 @@ def test_render_deterministic_and_sharded(gpu, tmp_path):
                                             ((64, 64), 3, [1, 2]), ((96, 96), 2, [4])])
 def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, spp, blocks):
     """The fused splat + merge (NH_SPLAT_FUSED=1: one workgroup per master tile, rounds in order, blocks in spiral
-    order, no staging) and the staged pair -- its first workgroup per block adding its rounds of the pixels only that
-    block covers straight into the master (default, at 1 / 4 / 8 rounds per workgroup), every workgroup staging
-    (NH_SPLAT_LEAD=0), one workgroup per block taking all rounds of those pixels (NH_SPLAT_DIRECT=1), the jitter read
+    order, no staging) and the staged pair -- one workgroup per block taking all rounds of the pixels only that block
+    covers (default), or per round group with its first workgroup adding its rounds of those pixels straight into the
+    master (NH_SPLAT_DIRECT=0, at 1 / 4 / 8 rounds per workgroup), every workgroup staging (NH_SPLAT_LEAD=0), the jitter read
     from a per-record array instead of recomputed from the path stream (NH_SPLAT_JITTER=stored), a persistent grid of
     3 workgroups walking the items (NH_SPLAT_WGS=3), 256-thread workgroups with 6-row strips instead of the default
     512 threads with 3-row strips (NH_SPLAT_T512=0, staged and all-direct) -- give the same
@@ -232,9 +232,10 @@ def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, 
     s.set_resolution(*res)
     b = nh.Bvh(s)
     out = {}
-    variants = ({"NH_SPLAT_DIRECT": "1"}, {"NH_SPLAT_LEAD": "0"}, {}, {"NH_SPLAT_ROUNDS": "4"},
-                {"NH_SPLAT_ROUNDS": "1"}, {"NH_SPLAT_FUSED": "1"}, {"NH_SPLAT_JITTER": "stored"},
-                {"NH_SPLAT_WGS": "3"}, {"NH_SPLAT_T512": "0"}, {"NH_SPLAT_T512": "0", "NH_SPLAT_DIRECT": "1"})
+    d0 = {"NH_SPLAT_DIRECT": "0"}
+    variants = ({}, d0, {**d0, "NH_SPLAT_LEAD": "0"}, {**d0, "NH_SPLAT_ROUNDS": "4"}, {**d0, "NH_SPLAT_ROUNDS": "1"},
+                {"NH_SPLAT_FUSED": "1"}, {"NH_SPLAT_JITTER": "stored"}, {**d0, "NH_SPLAT_JITTER": "stored"},
+                {**d0, "NH_SPLAT_WGS": "3"}, {"NH_SPLAT_T512": "0"}, {**d0, "NH_SPLAT_T512": "0"})
     for env in variants:
         for name in ("NH_SPLAT_DIRECT", "NH_SPLAT_LEAD", "NH_SPLAT_ROUNDS", "NH_SPLAT_FUSED", "NH_SPLAT_JITTER",
                      "NH_SPLAT_WGS", "NH_SPLAT_T512"):
