@@ -184,9 +184,10 @@ NHD bool box_test_finite(float mnx, float mny, float mnz, float mxx, float mxy, 
 
 // box_test_finite for two boxes at once: the slab products in packed FP32 (component i = box i, the
 // same IEEE operations), the min / max reductions per box as box_test_finite does them
-NHD void box_test_finite_pair(f2 mnx, f2 mny, f2 mnz, f2 mxx, f2 mxy, f2 mxz, F3 o, F3 r, float mint, float maxt,
-                              bool &hit0, bool &hit1, float &near0, float &near1) {
-    const f2 ox{o.x, o.x}, oy{o.y, o.y}, oz{o.z, o.z}, rx{r.x, r.x}, ry{r.y, r.y}, rz{r.z, r.z};
+NHD void box_test_finite_pair(f2 mnx, f2 mny, f2 mnz, f2 mxx, f2 mxy, f2 mxz, float o_x, float o_y, float o_z,
+                              float r_x, float r_y, float r_z, float mint, float maxt, bool &hit0, bool &hit1,
+                              float &near0, float &near1) {
+    const f2 ox{o_x, o_x}, oy{o_y, o_y}, oz{o_z, o_z}, rx{r_x, r_x}, ry{r_y, r_y}, rz{r_z, r_z};
     const f2 ax = (mnx - ox) * rx, bx = (mxx - ox) * rx;
     const f2 ay = (mny - oy) * ry, by = (mxy - oy) * ry;
     const f2 az = (mnz - oz) * rz, bz = (mxz - oz) * rz;
@@ -388,26 +389,34 @@ NHD bool leaf_any(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float &
     else return leaf_test<ANY, STATS, PAIRS>(tv, leaf, o, d, mint, maxt, best, found, st);
 }
 
-// Child box of an inner node: side 0 = left, 1 = right. fin: every 1/d component is finite (box_test_finite applies)
-NHD bool child_box_test(const float4 &n0, const float4 &n1, const float4 &n2, int side, F3 o, F3 d, F3 r, float mint,
-                        float maxt, float &near_t, bool fin) {
-    if (fin)
-        return side == 0 ? box_test_finite(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, r, mint, maxt, near_t)
-                         : box_test_finite(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, r, mint, maxt, near_t);
-    return side == 0 ? box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, near_t)
-                     : box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, near_t);
+// Inner-node fields read as scalars straight from the node record (float i of node n: nf[i], nf = the node's first
+// float): [0..5] the left child's box (min xyz, max xyz), [6..11] the right child's, int [12] / [13] their refs. The
+// float4 form (n0, n1, n2) let the compiler pick a child's six bounds by selecting between addresses of local float4
+// copies, which put those copies in scratch memory: a scratch store and reload in every node visit of every traversal.
+NHD const float *node_f(const Traversal &tv, int n) { return reinterpret_cast<const float *>(tv.nodes + 4 * n); }
+NHD int node_ref(const float *nf, int side) { return reinterpret_cast<const int *>(nf)[12 + side]; }
+
+// Child box of an inner node: side 0 = left, 1 = right (its six bounds read from the record at nf + 6 side). fin:
+// every 1/d component is finite (box_test_finite applies)
+NHD bool child_box_test(const float *nf, int side, F3 o, F3 d, F3 r, float mint, float maxt, float &near_t, bool fin) {
+    const float *c = nf + 6 * side;
+    const float mnx = c[0], mny = c[1], mnz = c[2], mxx = c[3], mxy = c[4], mxz = c[5];
+    if (fin) return box_test_finite(mnx, mny, mnz, mxx, mxy, mxz, o, r, mint, maxt, near_t);
+    return box_test(mnx, mny, mnz, mxx, mxy, mxz, o, d, r, mint, maxt, near_t);
 }
 
 // Both child boxes of an inner node; rays with all 1/d finite take the branch-free packed slab test (box_test_finite:
 // the same answers as the reference's branchy form for them), the others the reference's form
-NHD void node_box_tests(const float4 &n0, const float4 &n1, const float4 &n2, F3 o, F3 d, F3 r, float mint,
-                        float maxt, bool fin, bool &hl, bool &hr, float &nl, float &nr) {
+NHD void node_box_tests(const float *nf, F3 o, F3 d, F3 r, float mint, float maxt, bool fin, bool &hl, bool &hr,
+                        float &nl, float &nr) {
+    const float l0 = nf[0], l1 = nf[1], l2 = nf[2], l3 = nf[3], l4 = nf[4], l5 = nf[5];
+    const float r0 = nf[6], r1 = nf[7], r2 = nf[8], r3 = nf[9], r4 = nf[10], r5 = nf[11];
     if (fin) {
-        box_test_finite_pair(f2{n0.x, n1.z}, f2{n0.y, n1.w}, f2{n0.z, n2.x}, f2{n0.w, n2.y}, f2{n1.x, n2.z},
-                             f2{n1.y, n2.w}, o, r, mint, maxt, hl, hr, nl, nr);
+        box_test_finite_pair(f2{l0, r0}, f2{l1, r1}, f2{l2, r2}, f2{l3, r3}, f2{l4, r4}, f2{l5, r5}, o.x, o.y, o.z, r.x,
+                             r.y, r.z, mint, maxt, hl, hr, nl, nr);
     } else {
-        hl = box_test(n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, o, d, r, mint, maxt, nl);
-        hr = box_test(n1.z, n1.w, n2.x, n2.y, n2.z, n2.w, o, d, r, mint, maxt, nr);
+        hl = box_test(l0, l1, l2, l3, l4, l5, o, d, r, mint, maxt, nl);
+        hr = box_test(r0, r1, r2, r3, r4, r5, o, d, r, mint, maxt, nr);
     }
 }
 
@@ -444,22 +453,22 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
     int cur = 0;
     for (;;) {
         while (cur >= 0) {
-            const float4 n0 = tv.nodes[4 * cur], n1 = tv.nodes[4 * cur + 1], n2 = tv.nodes[4 * cur + 2];
-            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * cur + 3]);
+            const float *nf = node_f(tv, cur);
+            const int ref_l = node_ref(nf, 0), ref_r = node_ref(nf, 1);
             if (STATS && lead) { st.nodes++; st.boxes += 2; }
             float nl, nr;
             bool hl, hr;
-            node_box_tests(n0, n1, n2, o, d, r, mint, maxt, fin, hl, hr, nl, nr);
+            node_box_tests(nf, o, d, r, mint, maxt, fin, hl, hr, nl, nr);
             int next;
             if (hl && hr) {
                 const bool right_first = ORDERED && nr < nl;
                 stk[sp * stride] = ((uint32_t)cur << 1) | (right_first ? 0u : 1u);
                 ++sp;
-                next = right_first ? n3.y : n3.x;
+                next = right_first ? ref_r : ref_l;
             } else if (hl) {
-                next = n3.x;
+                next = ref_l;
             } else if (hr) {
-                next = n3.y;
+                next = ref_r;
             } else {
                 break;
             }
@@ -476,11 +485,10 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
             --sp;
             const uint32_t e = stk[sp * stride];
             const int parent = (int)(e >> 1), side = (int)(e & 1u);
-            const float4 n0 = tv.nodes[4 * parent], n1 = tv.nodes[4 * parent + 1], n2 = tv.nodes[4 * parent + 2];
+            const float *nf = node_f(tv, parent);
             if (STATS && lead) st.boxes++;
-            if (!child_box_test(n0, n1, n2, side, o, d, r, mint, maxt, near_t, fin)) continue;
-            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * parent + 3]);
-            const int ref = side ? n3.y : n3.x;
+            if (!child_box_test(nf, side, o, d, r, mint, maxt, near_t, fin)) continue;
+            const int ref = node_ref(nf, side);
             if (ref >= 0) {
                 cur = ref;
                 break;
@@ -635,22 +643,22 @@ struct Tracer {
             return;
         }
         if (cur >= 0) {  // one inner node: test both child boxes
-            const float4 n0 = tv.nodes[4 * cur], n1 = tv.nodes[4 * cur + 1], n2 = tv.nodes[4 * cur + 2];
-            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * cur + 3]);
+            const float *nf = node_f(tv, cur);
+            const int ref_l = node_ref(nf, 0), ref_r = node_ref(nf, 1);
             if (STATS) { st.nodes++; st.boxes += 2; }
             float nl, nr;
             bool hl, hr;
-            node_box_tests(n0, n1, n2, o, d, r, mint, maxt, fin, hl, hr, nl, nr);
+            node_box_tests(nf, o, d, r, mint, maxt, fin, hl, hr, nl, nr);
             int next;
             if (hl && hr) {
                 const bool right_first = ORDERED && nr < nl;
                 stk.push(sp, ((uint32_t)cur << 1) | (right_first ? 0u : 1u));
                 ++sp;
-                next = right_first ? n3.y : n3.x;
+                next = right_first ? ref_r : ref_l;
             } else if (hl) {
-                next = n3.x;
+                next = ref_l;
             } else if (hr) {
-                next = n3.y;
+                next = ref_r;
             } else {
                 cur = -1;
                 return;
@@ -662,12 +670,11 @@ struct Tracer {
             --sp;
             const uint32_t e = stk.pop(sp);
             const int parent = (int)(e >> 1), side = (int)(e & 1u);
-            const float4 n0 = tv.nodes[4 * parent], n1 = tv.nodes[4 * parent + 1], n2 = tv.nodes[4 * parent + 2];
+            const float *nf = node_f(tv, parent);
             if (STATS) st.boxes++;
             float near_t;
-            if (!child_box_test(n0, n1, n2, side, o, d, r, mint, maxt, near_t, fin)) return;
-            const int4 n3 = *reinterpret_cast<const int4 *>(&tv.nodes[4 * parent + 3]);
-            enter(tv, side ? n3.y : n3.x);
+            if (!child_box_test(nf, side, o, d, r, mint, maxt, near_t, fin)) return;
+            enter(tv, node_ref(nf, side));
             return;
         }
         done = true;
@@ -865,9 +872,11 @@ struct Tracer4 {
             if (finite_r) {
 #if NH_WIDE_PACKED_BOX
                 box_test_finite_pair(f2{mnx.x, mnx.y}, f2{mny.x, mny.y}, f2{mnz.x, mnz.y}, f2{mxx.x, mxx.y},
-                                     f2{mxy.x, mxy.y}, f2{mxz.x, mxz.y}, o, r, mint, maxt, v0, v1, n0, n1);
+                                     f2{mxy.x, mxy.y}, f2{mxz.x, mxz.y}, o.x, o.y, o.z, r.x, r.y, r.z, mint, maxt,
+                                     v0, v1, n0, n1);
                 box_test_finite_pair(f2{mnx.z, mnx.w}, f2{mny.z, mny.w}, f2{mnz.z, mnz.w}, f2{mxx.z, mxx.w},
-                                     f2{mxy.z, mxy.w}, f2{mxz.z, mxz.w}, o, r, mint, maxt, v2, v3, n2, n3);
+                                     f2{mxy.z, mxy.w}, f2{mxz.z, mxz.w}, o.x, o.y, o.z, r.x, r.y, r.z, mint, maxt,
+                                     v2, v3, n2, n3);
                 v0 &= ref.x != kWideEmpty;
                 v1 &= ref.y != kWideEmpty;
                 v2 &= ref.z != kWideEmpty;
