@@ -1330,7 +1330,9 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     // at 67M / 16.7M paths with the fused bounce (round 2): C4 3134 / 3229 / 3254 Msamples/s at
     // 262k / 64k / 32k, C2 3680 / 3717 at 262k / 64k, bumpy-1M (persistent traversal) 1404 / 1378 at
     // 262k / 64k -- an LDS-staged bounce stays efficient down to fewer paths than a deep-tree one
-    p.tail_at = p.fused ? std::min<int64_t>(std::max<int64_t>(n_paths / 256, 8192), 65536)
+    // round 5, with the scratch-free traversal: 64k / 32k / 16k / 8k -- C2 5567 / 5591 / 5577 / 5585, C1 4409 / 4408 /
+    // 4459, C4 4891 / 4906 / 4929 Msamples/s (profiles/round5_ab_tail_threshold.txt)
+    p.tail_at = p.fused ? std::min<int64_t>(std::max<int64_t>(n_paths / 1024, 8192), 16384)
                         : std::min<int64_t>(std::max<int64_t>(n_paths / 64, 8192), 262144);
     if (const char *e = std::getenv("NH_TAIL")) p.tail_at = std::atoll(e);
     // below this many live paths the pool counts as draining: the next chunk may start beside it
