@@ -562,6 +562,18 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     S.integrator = d->integrator;
     std::memcpy(S.s2c, d->camera.sample_to_camera, sizeof(S.s2c));
     std::memcpy(S.c2w, d->camera.camera_to_world, sizeof(S.c2w));
+    {  // camera_ray's origin for a (0, 0, 0) local origin (nh_shade.h): the same operations in the same order
+        float ow[4];
+        const float z = 0.0f;
+        for (int i = 0; i < 4; ++i) {
+            float acc = S.c2w[4 * i] * z;
+            acc = acc + S.c2w[4 * i + 1] * z;
+            acc = acc + S.c2w[4 * i + 2] * z;
+            acc = acc + S.c2w[4 * i + 3] * 1.0f;
+            ow[i] = acc;
+        }
+        for (int i = 0; i < 3; ++i) S.cam_o[i] = ow[i] / ow[3];
+    }
     S.inv_w = d->camera.inv_output_size[0];
     S.inv_h = d->camera.inv_output_size[1];
     S.near_clip = d->camera.near_clip;

@@ -223,6 +223,9 @@ struct DScene {
     const float4 *emit_faces;
     // camera (perspective.cpp) and filter table (block.cpp)
     float s2c[16], c2w[16];
+    // the pinhole ray origin (camera_ray with a (0, 0, 0) local origin: c2w * (0, 0, 0, 1), divided by its w), formed
+    // once at upload by the same float operations in the same order
+    float cam_o[3];
     float inv_w, inv_h, near_clip, far_clip;
     int width, height;
     // depth of field (perspective.cpp:114-130), on when lensRadius > Epsilon: lens_index[pixel] = the position of the

@@ -333,17 +333,21 @@ __device__ __forceinline__ void camera_ray(const DScene &S, float px, float py, 
     }
     const F3 dl = normalized(f3(r[0] / r[3], r[1] / r[3], r[2] / r[3]));
     F3 lo = f3(0.0f, 0.0f, 0.0f), ld = dl;  // local ray
-    if (DOF && S.dof) camera_lens(S, round, pix, dl, lo, ld);
-    float ow[4];
+    if (DOF && S.dof) {
+        camera_lens(S, round, pix, dl, lo, ld);
+        float ow[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float acc = S.c2w[4 * i] * lo.x;
-        acc = acc + S.c2w[4 * i + 1] * lo.y;
-        acc = acc + S.c2w[4 * i + 2] * lo.z;
-        acc = acc + S.c2w[4 * i + 3] * 1.0f;
-        ow[i] = acc;
+        for (int i = 0; i < 4; ++i) {
+            float acc = S.c2w[4 * i] * lo.x;
+            acc = acc + S.c2w[4 * i + 1] * lo.y;
+            acc = acc + S.c2w[4 * i + 2] * lo.z;
+            acc = acc + S.c2w[4 * i + 3] * 1.0f;
+            ow[i] = acc;
+        }
+        o = f3(ow[0] / ow[3], ow[1] / ow[3], ow[2] / ow[3]);
+    } else {
+        o = f3(S.cam_o[0], S.cam_o[1], S.cam_o[2]);  // the same expression for lo = (0, 0, 0), formed at upload
     }
-    o = f3(ow[0] / ow[3], ow[1] / ow[3], ow[2] / ow[3]);
     const float *w = S.c2w;
     d = f3(w[0] * ld.x + (w[1] * ld.y + w[2] * ld.z), w[4] * ld.x + (w[5] * ld.y + w[6] * ld.z),
            w[8] * ld.x + (w[9] * ld.y + w[10] * ld.z));

@@ -260,6 +260,31 @@ NHD bool leaf_test(const Traversal &tv, int leaf, F3 o, F3 d, float mint, float 
             f2 pt, pu, pv;
             bool ok0, ok1;
             tri_test_pair_e(p0, e1, e2, o, d, mint, pt, pu, pv, ok0, ok1);
+            const bool has1 = k + 1 < e;
+            if (!STATS && !((__float_as_int(q5.x) | (has1 ? __float_as_int(q5.y) : 0)) & kPrimSphere)) {
+                // two triangles (or the leaf's last one): the loop below's acceptance in primitive order, as selects
+                // (a hit needs t <= the running maxt; it replaces the best on t < maxt or a later record)
+                if (ANY) {
+                    if ((ok0 && pt.x <= maxt) || (has1 && ok1 && pt.y <= maxt)) return true;
+                    continue;
+                }
+                const bool h0 = ok0 && pt.x <= maxt;
+                const bool u0 = h0 && (pt.x < maxt || k > best.k);
+                maxt = u0 ? pt.x : maxt;
+                best.t = u0 ? pt.x : best.t;
+                best.u = u0 ? pu.x : best.u;
+                best.v = u0 ? pv.x : best.v;
+                best.k = u0 ? k : best.k;
+                const bool h1 = has1 && ok1 && pt.y <= maxt;
+                const bool u1 = h1 && (pt.y < maxt || k + 1 > best.k);
+                maxt = u1 ? pt.y : maxt;
+                best.t = u1 ? pt.y : best.t;
+                best.u = u1 ? pu.y : best.u;
+                best.v = u1 ? pv.y : best.v;
+                best.k = u1 ? k + 1 : best.k;
+                found = found || u0 || u1;
+                continue;
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 if (j == 1 && k + 1 >= e) break;
