@@ -1157,14 +1157,18 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     return true;
 }
 
+// threads per wf_bounce_rr workgroup (A/B builds: -DNH_BOUNCE_TB=128)
+#ifndef NH_BOUNCE_TB
+#define NH_BOUNCE_TB 256
+#endif
 template <bool ORDERED, bool STATS, bool SORT, bool FULL = true>
-__global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScene *__restrict__ Sp, Traversal tv_g,
+__global__ __launch_bounds__(NH_BOUNCE_TB, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScene *__restrict__ Sp, Traversal tv_g,
                                                                      WfLaunch L) {
-    __shared__ uint32_t stk[16 * 256];
+    __shared__ uint32_t stk[16 * NH_BOUNCE_TB];
     __shared__ unsigned s_n[kMatClasses], s_off[kMatClasses], s_base;
     extern __shared__ float4 lds_scene[];
     const QView qv = queue_view(L.cnt_in);
-    const int base = blockIdx.x * 256;
+    const int base = blockIdx.x * NH_BOUNCE_TB;
     if (base >= qv.n) return;  // whole workgroup
     if (threadIdx.x < kMatClasses) s_n[threadIdx.x] = 0u;  // visible after the staging barrier
     const DScene &S = *Sp;
@@ -1187,10 +1191,10 @@ __global__ __launch_bounds__(256, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScen
         Its its;
         bool alive = true;
         if constexpr (STATS) t_ph = clock64();
-        if (L.first) alive = first_vertex<ORDERED, STATS>(S, tv, L, s, v, h, its, my_stk, 256, st_e, q_e);
+        if (L.first) alive = first_vertex<ORDERED, STATS>(S, tv, L, s, v, h, its, my_stk, NH_BOUNCE_TB, st_e, q_e);
         else load_post_head(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
         if constexpr (STATS) c_load = clock64() - t_ph;
-        if (alive) cont = rr_step<ORDERED, STATS, STATS, 1, FULL>(S, tv, L, v, its, h, my_stk, 256, st_e, st_s, q_e,
+        if (alive) cont = rr_step<ORDERED, STATS, STATS, 1, FULL>(S, tv, L, v, its, h, my_stk, NH_BOUNCE_TB, st_e, st_s, q_e,
                                                                   q_s, &clk);
         if (cont) cls = prim_material(tv.prims[3 * h.k + 2]);  // a live path's ray has hit something
         if constexpr (STATS) t_ph = clock64();
@@ -1563,11 +1567,11 @@ void launch_wf_bounce(const DScene *S, const Traversal &tv, const WfLaunch &L, b
 #if NH_WF_HAS_PART(2)
 void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
                          bool lean, int bound, hipStream_t st) {
-    int blocks = std::max(1, (bound + 255) / 256);
+    int blocks = std::max(1, (bound + NH_BOUNCE_TB - 1) / NH_BOUNCE_TB);
     blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
     const size_t lds = 16 * (size_t)rr_lds_f4(L);
-#define NH_FB(O, T, SO) hipLaunchKernelGGL((wf_bounce_rr<O, T, SO>), dim3(blocks), dim3(256), lds, st, S, tv, L)
-#define NH_FBN(T, SO) hipLaunchKernelGGL((wf_bounce_rr<true, T, SO, false>), dim3(blocks), dim3(256), lds, st, S, tv, L)
+#define NH_FB(O, T, SO) hipLaunchKernelGGL((wf_bounce_rr<O, T, SO>), dim3(blocks), dim3(NH_BOUNCE_TB), lds, st, S, tv, L)
+#define NH_FBN(T, SO) hipLaunchKernelGGL((wf_bounce_rr<true, T, SO, false>), dim3(blocks), dim3(NH_BOUNCE_TB), lds, st, S, tv, L)
     if (ordered && lean) {  // no discrete BSDF, no texture: wf_bounce_rr<.., FULL = false>
         if (stats) { if (sort) NH_FBN(true, true); else NH_FBN(true, false); }
         else { if (sort) NH_FBN(false, true); else NH_FBN(false, false); }
