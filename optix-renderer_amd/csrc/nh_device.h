@@ -455,6 +455,11 @@ NHD int dpdf_search(const float *cdf, int n_entries, float x, int lo, int hi) {
     return index;
 }
 NHD int dpdf_sample(const float *cdf, int n_entries, float x) { return dpdf_search(cdf, n_entries, x, 0, n_entries + 1); }
+// the emitter pick of the integrators (m_emitterPDF.sample): with one emitter DiscretePDF::sample's clamp returns 0 for
+// every x, so the two dependent CDF reads of the search are skipped (the caller still draws x)
+NHD int emitter_pick(const DScene &S, float x) {
+    return S.n_emitters == 1 ? 0 : dpdf_sample(S.emitter_cdf, S.n_emitters, x);
+}
 
 // The same search bracketed by a guide table (Chen & Asau's cutpoint method), bit-identical: guide[j] is the first
 // CDF index not below j / 2^bits (nh_api.hip env_guide), and the first index not below x is monotone in x, so for

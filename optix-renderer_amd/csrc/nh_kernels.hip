@@ -57,7 +57,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
         t = divs(t, succ);
 
         // emitter sampling (path_mis.cpp:75-102)
-        const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, rng.next1d());
+        const int ei = emitter_pick(S, rng.next1d());
         const DEmitter em = S.emitters[ei];
         const float ex = rng.next1d(), ey = rng.next1d();
         ESample es;
@@ -322,7 +322,7 @@ __device__ F3 li_direct_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o
     const float n_lights = (float)S.n_emitters;
     F3 result_ems = f3(0, 0, 0), result_mats = f3(0, 0, 0);
     float w_ems = 0.f, w_mat = 0.f;
-    const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, rng.next1d());
+    const int ei = emitter_pick(S, rng.next1d());
     const DEmitter em = S.emitters[ei];
     const float ex = rng.next1d(), ey = rng.next1d();
     ESample es;

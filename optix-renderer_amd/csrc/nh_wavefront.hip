@@ -673,7 +673,7 @@ __device__ __forceinline__ void shade_body(const DScene &S, const Traversal &tv,
         F3 li_ems = f3(0, 0, 0);
         float pdfems = 0.f, pdfems_mats = 0.f;
         if (!skip_nee) {
-            const int ei = dpdf_sample(S.emitter_cdf, S.n_emitters, e0);
+            const int ei = emitter_pick(S, e0);
             const DEmitter em = S.emitters[ei];
             ESample es;
             const F3 ems_col = emitter_sample(S, em, its.p, ex, ey, es);
