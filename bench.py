@@ -835,7 +835,7 @@ def main():
     # one hardware queue per path-pool stream: the benchmark's own configuration (the GPU box exports HIP's default
     # of 4, with which two pool streams share a queue and one pool's tail blocks another's bounces: C1 -15 %,
     # profiles/round4_session3_ab.txt). Raised before torch may initialise the HIP runtime in a multi-rank run (the
-    # binding raises it the same way when imported); the line records the value.
+    # binding's nori_hip.configure_runtime() raises it the same way); the line records the value.
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
         os.environ["NH_KEEP_HW_QUEUES"] = "1"

@@ -79,6 +79,10 @@ typedef struct nh_shape {
     float bbox_max[3];
     uint32_t pdf_offset;     /* mesh area DiscretePDF: n_faces+1 CDF entries in area_cdf */
     float pdf_normalization; /* DiscretePDF::getNormalization() = 1/sum(area) */
+    uint32_t normal_map;     /* 1 + index into nh_scene_desc.textures of the shape's <texture name="normal"> child
+                                (Shape::addChild, src/shapes/shape.cpp:138-147), 0 = none. It perturbs the shading
+                                frame: meshes with normals and uvs take normalize(TBN * eval(uv)) (mesh.cpp:165-185),
+                                spheres re-derive their frame from shFrame.toWorld(eval(uv)) (sphere.cpp:115-121) */
 } nh_shape;
 
 /* One Nori BSDF (src/bsdf/{diffuse,mirror,dielectric,microfacet}.cpp). */
@@ -98,7 +102,11 @@ typedef struct nh_bsdf {
  *   NH_TEXTURE_CHECKERBOARD Checkerboard<Color3f> (src/textures/checkerboard.cpp:29-47): value1 / value2 by the
  *                           parity of the cell of uv / scale - delta
  *   NH_TEXTURE_PNG          PNGTexture (src/textures/PNGTexture.cpp:125-160): nearest texel of an sRGB-decoded RGBA
- *                           image (row 0 of the PNG first) at texel_offset in nh_scene_desc.texels */
+ *                           image (row 0 of the PNG first) at texel_offset in nh_scene_desc.texels; with
+ *                           linear = 1 (sRGB = false, the default for a texture named "normal", PNGTexture.cpp:26)
+ *                           the texels hold the normal-map decode of loadFromFile (x / 255 * 2 - 1 with every third
+ *                           float of the RGBA array normalized as a Vector3f, PNGTexture.cpp:85-95) and eval blends
+ *                           the texel by intensity and normalizes it (:155-161) */
 enum { NH_TEXTURE_CONSTANT = 0, NH_TEXTURE_CHECKERBOARD = 1, NH_TEXTURE_PNG = 2 };
 typedef struct nh_texture {
     int32_t type;            /* NH_TEXTURE_* */
@@ -113,6 +121,8 @@ typedef struct nh_texture {
     int32_t spherical;       /* png sphericalTexture */
     float rotation[9];       /* png spherical lookups: the eulerAngles rotation (PNGTexture.cpp:133-139), row-major;
                                 identity for eulerAngles = 0 */
+    int32_t linear;          /* png: sRGB = false (normal-map decode + eval's intensity blend and normalize) */
+    float intensity;         /* png, linear: PNGTexture intensity [1] */
     int32_t pad;
 } nh_texture;
 
@@ -137,7 +147,13 @@ typedef struct nh_camera {
        thin lens (perspective.cpp:114-130); camera ray k of the serial render order (round, BlockGenerator
        spiral, x-major pixels) takes draws 2k, 2k+1 of a default-state pcg32 -- the reference's static sampler */
     float lens_radius, focal_distance;
+    /* which of those two draws is the lens sample's x: Independent::next2D builds Point2f(nextFloat(), nextFloat())
+       (independent.cpp:74-78), whose argument evaluation order C++ leaves unspecified. NH_LENS_DRAWS_RTL (the
+       loader's default): x = draw 2k+1, y = draw 2k, as g++ compiles it (oracle/normalmap_probe.cpp "order");
+       NH_LENS_DRAWS_LTR: x = draw 2k, as clang compiles it */
+    int32_t lens_draw_order;
 } nh_camera;
+enum { NH_LENS_DRAWS_LTR = 0, NH_LENS_DRAWS_RTL = 1 };
 
 /* Tabulated reconstruction filter as ImageBlock::init builds it (src/utils/block.cpp:54-70). */
 typedef struct nh_filter {
@@ -346,6 +362,16 @@ int nh_scene_set_bsdf(nh_scene *scene, uint32_t shape, const nh_bsdf *bsdf);
 /* append a texture to the scene's texture table (png: texels = width*height*4 floats, copied); returns its
    index + 1 for nh_bsdf.albedo_texture, or 0 on error (nh_host_last_error) */
 uint32_t nh_scene_add_texture(nh_scene *scene, const nh_texture *tex, const float *texels);
+/* give a shape a normal map (Shape::addChild of a <texture name="normal">, src/shapes/shape.cpp:138-147):
+   texture = a value nh_scene_add_texture returned, 0 removes it */
+int nh_scene_set_normal_map(nh_scene *scene, uint32_t shape, uint32_t texture);
+/* the thin-lens sample's draw order (nh_camera.lens_draw_order): NH_LENS_DRAWS_RTL or NH_LENS_DRAWS_LTR */
+int nh_scene_set_lens_draw_order(nh_scene *scene, int32_t order);
+/* PNGTexture::loadFromFile's byte -> float loop over lodepng's RGBA8 array (PNGTexture.cpp:78-95): srgb != 0
+   InverseGammaCorrect(b / 255) per byte; srgb == 0 the normal-map decode b / 255 * 2 - 1 with every third float
+   of the array normalized as an Eigen Vector3f (the triples run over RGBA data, so they straddle pixels -- the
+   reference's behaviour, reproduced). out: n floats. */
+int nh_texture_decode(const uint8_t *rgba8, uint64_t n, int32_t srgb, float *out);
 int nh_scene_set_integrator(nh_scene *scene, int32_t integrator);
 void nh_scene_free(nh_scene *scene);
 const char *nh_host_last_error(void);

@@ -261,6 +261,72 @@ std::vector<uint32_t> serial_ray_index(int w, int h, int bs) {
     return idx;
 }
 
+// pcg32::advance (pcg32.h:131-150) as an affine map of the state: advance(x, delta) = a * x + c (mod 2^64)
+struct PcgAffine {
+    uint64_t a = 1u, c = 0u;
+};
+PcgAffine pcg_affine(uint64_t inc, uint64_t delta) {
+    uint64_t cur_mult = 0x5851f42d4c957f2dULL, cur_plus = inc;
+    PcgAffine r;
+    while (delta > 0) {
+        if (delta & 1) {
+            r.a *= cur_mult;
+            r.c = r.c * cur_mult + cur_plus;
+        }
+        cur_plus = (cur_mult + 1) * cur_plus;
+        cur_mult *= cur_mult;
+        delta /= 2;
+    }
+    return r;
+}
+// g after f: x -> g.a * (f.a * x + f.c) + g.c
+PcgAffine pcg_then(const PcgAffine &f, const PcgAffine &g) {
+    PcgAffine r;
+    r.a = g.a * f.a;
+    r.c = g.a * f.c + g.c;
+    return r;
+}
+
+// Lens-stream tables (nh_shade.h lens_uniform): camera ray k = round * W * H + pos[pixel] starts at draw 2k of the
+// default-state stream, i.e. state(2k) = A_pos * (A_lo * S_hi + C_lo) + C_pos with round = 256 h + l,
+// S_hi[h] = state(2 * 256 h * W * H), (A_lo, C_lo)[l] = advance by 2 l W H, (A_pos, C_pos) = advance by 2 pos:
+// two 64-bit multiply-adds per ray instead of pcg_advance's O(log k) loop, and the same state (the maps commute)
+constexpr uint64_t kLensDefaultState = 0x853c49e6748fea9bULL, kLensDefaultStream = 0xda3e39cb94b95bdbULL;
+struct LensTables {
+    std::vector<ulonglong2> pix, lo;
+    std::vector<uint64_t> hi;
+};
+LensTables lens_tables(int w, int h) {
+    LensTables t;
+    const std::vector<uint32_t> pos = serial_ray_index(w, h, 32);
+    const uint64_t wh = (uint64_t)w * (uint64_t)h;
+    // per pixel, in serial order: advance by 2 pos
+    std::vector<PcgAffine> by_pos(wh);
+    const PcgAffine two = pcg_affine(kLensDefaultStream, 2);
+    PcgAffine cur;
+    for (uint64_t k = 0; k < wh; ++k) {
+        by_pos[k] = cur;
+        cur = pcg_then(cur, two);
+    }
+    t.pix.resize(wh);
+    for (uint64_t i = 0; i < wh; ++i) t.pix[i] = make_ulonglong2(by_pos[pos[i]].a, by_pos[pos[i]].c);
+    const PcgAffine round1 = pcg_affine(kLensDefaultStream, 2 * wh);
+    cur = PcgAffine();
+    t.lo.resize(nhd::kLensLo);
+    for (int l = 0; l < nhd::kLensLo; ++l) {
+        t.lo[l] = make_ulonglong2(cur.a, cur.c);
+        cur = pcg_then(cur, round1);
+    }
+    const PcgAffine round_hi = pcg_affine(kLensDefaultStream, 2 * wh * (uint64_t)nhd::kLensLo);
+    uint64_t st = kLensDefaultState;
+    t.hi.resize(nhd::kLensHi);
+    for (int hh = 0; hh < nhd::kLensHi; ++hh) {
+        t.hi[hh] = st;
+        st = round_hi.a * st + round_hi.c;
+    }
+    return t;
+}
+
 }  // namespace
 
 extern "C" {
@@ -411,7 +477,12 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         o.radius = s.radius;
         o.pdf_off = (int)s.pdf_offset;
         o.pdf_norm = s.pdf_normalization;
-        o.tex_uv = d->bsdfs[s.bsdf].type == NH_BSDF_DIFFUSE && d->bsdfs[s.bsdf].albedo_texture != 0;
+        if (s.normal_map > d->n_textures || (s.normal_map && !d->textures))
+            return fail(c, "shape normal map index out of range"), NH_ERR_INVALID;
+        // bit 0: uv read (textured albedo or normal map); bits 1+: 1 + the normal map's texture index
+        o.tex_uv = ((int)s.normal_map << 1) |
+                   ((d->bsdfs[s.bsdf].type == NH_BSDF_DIFFUSE && d->bsdfs[s.bsdf].albedo_texture != 0) || s.normal_map
+                        ? 1 : 0);
         o.ef_off = -1;
     }
     // emitting meshes without vertex normals: one emit_faces record per face (vertex index triples here)
@@ -461,6 +532,8 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
         o.su = t.scale_u; o.sv = t.scale_v; o.ou = t.offset_u; o.ov = t.offset_v;
         o.off = (long long)t.texel_offset;
         std::memcpy(o.rot, t.rotation, sizeof(o.rot));
+        o.linear = t.type == NH_TEXTURE_PNG && t.linear;
+        o.intensity = t.intensity;
     }
     std::vector<DEmitter> de(d->n_emitters);
     for (uint32_t i = 0; i < d->n_emitters; ++i) {
@@ -586,11 +659,15 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     S.dof = d->camera.lens_radius > 1e-4f ? 1 : 0;
     S.lens_radius = d->camera.lens_radius;
     S.focal_distance = d->camera.focal_distance;
-    S.lens_index = nullptr;
-    std::vector<uint32_t> lens_index;
+    S.lens_rtl = d->camera.lens_draw_order == NH_LENS_DRAWS_RTL ? 1 : 0;
+    S.lens_pix = S.lens_lo = nullptr;
+    S.lens_hi = nullptr;
     if (S.dof) {
-        lens_index = serial_ray_index(S.width, S.height, 32);
-        if ((rc = upload(c, c->scene_bufs, lens_index.data(), lens_index.size(), &S.lens_index))) return rc;
+        const LensTables lt = lens_tables(S.width, S.height);
+        if ((rc = upload(c, c->scene_bufs, lt.pix.data(), lt.pix.size(), &S.lens_pix))) return rc;
+        if ((rc = upload(c, c->scene_bufs, lt.lo.data(), lt.lo.size(), &S.lens_lo))) return rc;
+        if ((rc = upload(c, c->scene_bufs, lt.hi.data(), lt.hi.size(), &S.lens_hi))) return rc;
+        HIP_TRY(c, hipStreamSynchronize(c->stream));  // (the tables are locals)
     }
     S.filter_radius = d->filter.radius;
     S.lookup = d->filter.lookup_factor;
@@ -607,8 +684,10 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     }
     c->n_bsdf_types = __builtin_popcount(types);
     c->specular = (types & ((1u << NH_BSDF_MIRROR) | (1u << NH_BSDF_DIELECTRIC))) != 0;
-    c->textured = false;  // any BSDF with an albedo texture (wf_bounce_rr's lean instantiation has no lookup)
+    // any BSDF with an albedo texture or shape with a normal map (wf_bounce_rr's lean instantiation has no lookup)
+    c->textured = false;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) c->textured = c->textured || d->bsdfs[i].albedo_texture != 0;
+    for (uint32_t i = 0; i < d->n_shapes; ++i) c->textured = c->textured || d->shapes[i].normal_map != 0;
     c->V.assign(d->V, d->V + 3 * nv);
     c->F.assign(d->F, d->F + 3 * (size_t)d->n_faces);
     c->width = d->camera.width;
@@ -1822,6 +1901,8 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
     if (!c || !q) return NH_ERR_INVALID;
     if (!c->has_scene || !c->has_bvh) return fail(c, "nh_render: scene and BVH must be uploaded"), NH_ERR_STATE;
     if (q->sample_end < q->sample_begin || q->sample_begin < 0) return fail(c, "invalid sample range"), NH_ERR_INVALID;
+    if (c->S.dof && q->sample_end > nhd::kLensLo * nhd::kLensHi)  // the lens tables' range (nh_shade.h lens_uniform)
+        return fail(c, "depth of field: sample rounds beyond 2^24"), NH_ERR_UNSUPPORTED;
     // path_mis throws it (path_mis.cpp:76-79); direct_mis would pick from an empty emitter list
     if ((c->integrator == NH_INTEGRATOR_PATH_MIS || c->integrator == NH_INTEGRATOR_DIRECT_MIS) && c->n_emitters == 0)
         return fail(c, "No Emitter in scene!"), NH_ERR_INVALID;

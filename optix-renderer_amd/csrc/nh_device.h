@@ -22,6 +22,9 @@ constexpr uint64_t kPcgMult = 0x5851f42d4c957f2dULL;
 
 #define NHD __device__ __forceinline__
 
+// lens-stream tables (DScene::lens_lo / lens_hi): rounds 256 h + l, h < kLensHi
+constexpr int kLensLo = 256, kLensHi = 65536;
+
 NHD float f_sin(float x) { return (float)sin((double)x); }
 NHD float f_cos(float x) { return (float)cos((double)x); }
 
@@ -172,7 +175,9 @@ struct alignas(16) DShape {
     float cx, cy, cz, radius;
     int pdf_off;
     float pdf_norm;
-    int tex_uv;  // its BSDF reads Intersection::uv (a textured diffuse albedo): hit_info computes uv only then
+    // bit 0: Intersection::uv is read (a textured diffuse albedo, or a normal map): hit_info computes uv only then;
+    // bits 1+: 1 + the DScene::texs index of the shape's normal map (shape.cpp:138-147), 0 = none
+    int tex_uv;
     int ef_off;  // emitting mesh without normals: its faces' first record in DScene::emit_faces, else -1
 };
 struct alignas(16) DBsdf {
@@ -192,7 +197,9 @@ struct alignas(16) DTex {
     float ou, ov;
     long long off;  // png: first texel in DScene::texels
     float rot[9];   // png spherical lookups: the eulerAngles rotation, row-major
-    float pad[3];
+    int linear;     // png with sRGB = false: normal-map texels, eval blends by intensity and normalizes
+    float intensity;
+    float pad;
 };
 struct alignas(16) DEmitter {
     int type, shape;
@@ -228,11 +235,14 @@ struct DScene {
     float cam_o[3];
     float inv_w, inv_h, near_clip, far_clip;
     int width, height;
-    // depth of field (perspective.cpp:114-130), on when lensRadius > Epsilon: lens_index[pixel] = the position of the
-    // pixel's camera ray within one sample round of the serial render order (spiral blocks, x-major pixels)
-    int dof;
+    // depth of field (perspective.cpp:114-130), on when lensRadius > Epsilon. The lens stream's state at a camera
+    // ray's first draw (nh_shade.h lens_uniform): lens_pix[pixel] = advance by 2 x (the pixel's position within one
+    // sample round of the serial render order: spiral blocks, x-major pixels) as (a, c); lens_lo[l] = advance by
+    // 2 l W H; lens_hi[h] = the state at draw 2 * 256 h * W * H. lens_rtl: x = the second draw (g++'s order)
+    int dof, lens_rtl;
     float lens_radius, focal_distance;
-    const uint32_t *lens_index;
+    const ulonglong2 *lens_pix, *lens_lo;
+    const uint64_t *lens_hi;
     float filter_radius, lookup;
     int border;
     float table[33];

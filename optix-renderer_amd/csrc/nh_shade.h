@@ -22,7 +22,11 @@ __device__ __forceinline__ Frame staged_frame(const float4 *frames, int k) {
     return f;
 }
 
-// Mesh::setHitInformation (mesh.cpp:141-196) / Sphere::setHitInformation (sphere.cpp:96-124)
+__device__ __noinline__ F3 tex_eval(const DTex *texs, const float4 *texels, int ti, float u, float v);
+
+// Mesh::setHitInformation (mesh.cpp:141-196) / Sphere::setHitInformation (sphere.cpp:96-124), with the shape's normal
+// map (DShape::tex_uv >> 1) unless NMAP = false (the lean RR-ahead bounce kernel: scenes without textures)
+template <bool NMAP = true>
 __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, const Hit &h, F3 o, F3 d, Its &its) {
     const float4 a = tv.prims[3 * h.k], b = tv.prims[3 * h.k + 1];
     const int shape = __float_as_int(b.w);
@@ -31,8 +35,8 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
     if (sh.type == SHAPE_SPHERE) {
         its.p = add(o, scl(h.t, d));
         F3 n = normalized(sub(its.p, f3(sh.cx, sh.cy, sh.cz)));
-        // uv (two fp64-evaluated transcendentals) only matters to a textured albedo (bsdf_albedo is its only
-        // reader): the specular chains that set the tail's length skip it
+        // uv (two fp64-evaluated transcendentals) only matters to a textured albedo (bsdf_albedo) and a normal map,
+        // its only readers: the specular chains that set the tail's length skip it
         its.u = its.v = 0.f;
         if (sh.tex_uv) {
             F3 mn = neg(n);
@@ -45,6 +49,14 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
         its.sh.s = t;
         its.sh.t = cross(n, t);
         its.sh.n = n;
+        if (NMAP && (sh.tex_uv >> 1)) {  // sphere.cpp:115-121: the frame re-derived from the mapped normal
+            const F3 nm = tex_eval(S.texs, S.texels, (sh.tex_uv >> 1) - 1, its.u, its.v);
+            n = normalized(to_world(its.sh, nm));
+            t = normalized(cross(f3(0, 0, 1), n));
+            its.sh.s = t;
+            its.sh.t = cross(n, t);
+            its.sh.n = n;
+        }
         return;
     }
     const float bx = 1 - (h.u + h.v), by = h.u, bz = h.v;
@@ -60,7 +72,7 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
     const int local = __float_as_int(a.w);
     const uint32_t *f = S.F + 3 * (size_t)(sh.f_off + local);
     const uint32_t i0 = sh.v_off + f[0], i1 = sh.v_off + f[1], i2 = sh.v_off + f[2];
-    if (sh.has_uv && sh.tex_uv) {  // texture coordinates, read only by a textured albedo
+    if (sh.has_uv && sh.tex_uv) {  // texture coordinates, read only by a textured albedo or a normal map
         its.u = bx * S.UV[2 * i0] + by * S.UV[2 * i1] + bz * S.UV[2 * i2];
         its.v = bx * S.UV[2 * i0 + 1] + by * S.UV[2 * i1 + 1] + bz * S.UV[2 * i2 + 1];
     }
@@ -69,6 +81,13 @@ __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, c
         if (sh.has_uv) {
             its.sh.s = normalized(add(add(scl(bx, ldv(S.T, i0)), scl(by, ldv(S.T, i1))), scl(bz, ldv(S.T, i2))));
             its.sh.t = normalized(add(add(scl(bx, ldv(S.BT, i0)), scl(by, ldv(S.BT, i1))), scl(bz, ldv(S.BT, i2))));
+            if (NMAP && (sh.tex_uv >> 1)) {  // mesh.cpp:173-183: normal = (TBN * m_normalMap->eval(uv)).normalized()
+                const F3 nm = tex_eval(S.texs, S.texels, (sh.tex_uv >> 1) - 1, its.u, its.v);
+                // TBN's columns are (tangent, bitangent, normal); Matrix3f * Vector3f per row x0*y0 + (x1*y1 + x2*y2)
+                const F3 a = its.sh.s, b = its.sh.t;
+                nrm = normalized(f3(a.x * nm.x + (b.x * nm.y + nrm.x * nm.z), a.y * nm.x + (b.y * nm.y + nrm.y * nm.z),
+                                    a.z * nm.x + (b.z * nm.y + nrm.z * nm.z)));
+            }
             its.sh.n = nrm;
         } else {
             its.sh = frame_from_n(nrm);
@@ -133,7 +152,14 @@ __device__ __noinline__ F3 tex_eval(const DTex *texs, const float4 *texels, int 
             u += t.ou;
             v += t.ov;
         }
-        return png_lookup(texels + t.off, (unsigned)t.w, (unsigned)t.h, t.su, t.sv, u, v);
+        F3 c = png_lookup(texels + t.off, (unsigned)t.w, (unsigned)t.h, t.su, t.sv, u, v);
+        if (t.linear) {  // sRGB = false, a normal map (PNGTexture.cpp:155-161): blend towards +z by intensity, normalize
+            c.x = c.x * t.intensity;
+            c.y = c.y * t.intensity;
+            c.z = c.z * t.intensity + (1.f - t.intensity);
+            c = normalized(c);
+        }
+        return c;
     }
     return f3(t.v1r, t.v1g, t.v1b);
 }
@@ -288,14 +314,20 @@ __device__ __forceinline__ F3 emitter_sample(const DScene &S, const DEmitter &e,
 // k = round * W * H + lens_index[pixel] takes draws 2k and 2k + 1, which pcg32::advance reaches directly: every
 // ray's lens sample is independent of how the rays are distributed over threads, blocks and ranks. (With several
 // threads the reference's draws race, so only its single-thread order is reproducible: DESIGN.md §7.)
+// The state at draw 2k is one affine map of the default state, composed from three table entries (nh_api.hip
+// lens_tables: pcg32::advance is x -> a x + c mod 2^64, and advances compose and commute): two 64-bit multiply-adds
+// instead of pcg_advance's O(log k) loop. Point2f(nextFloat(), nextFloat()) as g++ evaluates it (right to left,
+// S.lens_rtl): x = draw 2k + 1, y = draw 2k.
 NHD void lens_uniform(const DScene &S, int round, int pix, float &u, float &v) {
-    const uint64_t k = (uint64_t)(uint32_t)round * (uint64_t)((uint32_t)S.width * (uint32_t)S.height) +
-                       (uint64_t)S.lens_index[pix];
+    const unsigned rr = (unsigned)round;  // < kLensLo * kLensHi (nh_render checks)
+    const ulonglong2 lo = S.lens_lo[rr & (kLensLo - 1)], pa = S.lens_pix[pix];
+    const uint64_t s_round = lo.x * S.lens_hi[rr / kLensLo] + lo.y;
     Rng r;
     r.inc = kPcgDefaultStream;
-    r.state = pcg_advance(kPcgDefaultState, kPcgDefaultStream, 2 * k);
-    u = r.next1d();
-    v = r.next1d();
+    r.state = pa.x * s_round + pa.y;
+    const float a = r.next1d(), b = r.next1d();
+    u = S.lens_rtl ? b : a;
+    v = S.lens_rtl ? a : b;
 }
 
 // The thin-lens part of sampleRay (perspective.cpp:120-130): the local ray's origin on the lens and its direction

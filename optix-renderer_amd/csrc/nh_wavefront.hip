@@ -572,7 +572,9 @@ struct PathV {
 // The head of a shade step (path_mis.cpp:26-71 / path_mats.cpp:22-56): with the hit of the path's ray,
 // finish the previous bounce's MIS probe weight (w_mats, :117-140), take the escaped ray's environment term
 // or the hit's emitter term, then Russian roulette. Returns whether the path survives; its = the hit's
-// Intersection. The previous bounce's pending light sample (F_NEE) must be resolved already.
+// Intersection. The previous bounce's pending light sample (F_NEE) must be resolved already. NMAP: hit_info's normal
+// maps (false only in the lean bounce kernel, for scenes without textures).
+template <bool NMAP = true>
 __device__ __forceinline__ bool shade_head(const DScene &S, const Traversal &tv, PathV &v, const Hit &h, bool found,
                                            float pdfmat, Its &its) {
     bool have_its = false;
@@ -581,7 +583,7 @@ __device__ __forceinline__ bool shade_head(const DScene &S, const Traversal &tv,
             if (S.envmap >= 0) v.li = add(v.li, mulc(v.t, env_eval(S, v.d)));
             return false;
         }
-        hit_info(S, tv, h, v.org, v.d, its);
+        hit_info<NMAP>(S, tv, h, v.org, v.d, its);
         const DShape shape = S.shapes[its.shape];
         if (shape.emitter >= 0) {
             const F3 wi = normalized(sub(its.p, v.org));
@@ -600,7 +602,7 @@ __device__ __forceinline__ bool shade_head(const DScene &S, const Traversal &tv,
     if (!(v.flags & F_FIRST)) {  // finish the previous bounce (path_mis.cpp:115-140)
         // the MIS probe hit an emitter (:117-133): w_mats from the pdfs of both strategies
         if (!(v.flags & F_ZERO_COL) && found) {
-            hit_info(S, tv, h, v.org, v.d, its);
+            hit_info<NMAP>(S, tv, h, v.org, v.d, its);
             have_its = true;
             const int hem = S.shapes[its.shape].emitter;
             if (hem >= 0) {
@@ -615,7 +617,7 @@ __device__ __forceinline__ bool shade_head(const DScene &S, const Traversal &tv,
         if (S.envmap >= 0) v.li = add(v.li, mulc(v.t, env_eval(S, v.d)));
         return false;
     }
-    if (!have_its) hit_info(S, tv, h, v.org, v.d, its);
+    if (!have_its) hit_info<NMAP>(S, tv, h, v.org, v.d, its);
     const DShape shape = S.shapes[its.shape];
     if (shape.emitter >= 0) {  // path_mis.cpp:51-56, ref = ray origin
         const F3 wi = normalized(sub(its.p, v.org));
@@ -1039,6 +1041,7 @@ __device__ __forceinline__ void store_post_head(const WfBuf &B, int s, const Pat
     B.hit[s] = make_float4(h.t, h.u, h.v, __int_as_float(h.k));
 }
 
+template <bool NMAP = true>
 __device__ __forceinline__ void load_post_head(const DScene &S, const Traversal &tv, const WfLaunch &L, const WfBuf &B,
                                                int s, PathV &v, Hit &h, Its &its) {
     const float4 ro = B.ray_o[s], rd = B.ray_d[s], li4 = B.li[s], th4 = B.thr[s], hv = B.hit[s];
@@ -1057,11 +1060,11 @@ __device__ __forceinline__ void load_post_head(const DScene &S, const Traversal 
     h.u = hv.y;
     h.v = hv.z;
     h.k = __float_as_int(hv.w);
-    hit_info(S, tv, h, v.org, v.d, its);
+    hit_info<NMAP>(S, tv, h, v.org, v.d, its);
 }
 
 // the camera path of queue entry s at bounce 0, up to its first vertex's head
-template <bool ORDERED, bool STATS>
+template <bool ORDERED, bool STATS, bool NMAP = true>
 __device__ __forceinline__ bool first_vertex(const DScene &S, const Traversal &tv, const WfLaunch &L, int s, PathV &v,
                                              Hit &h, Its &its, uint32_t *stk, int stride, TravStats &st_e,
                                              unsigned long long &q_e) {
@@ -1080,7 +1083,7 @@ __device__ __forceinline__ bool first_vertex(const DScene &S, const Traversal &t
     const bool live = rd.w >= ro.w;
     q_e += live ? 1 : 0;
     const bool found = live && trace<16, ORDERED, false, STATS, true>(tv, S, v.org, v.d, ro.w, rd.w, h, stk, stride, st_e);
-    if (!shade_head(S, tv, v, h, found, 0.f, its)) {
+    if (!shade_head<NMAP>(S, tv, v, h, found, 0.f, its)) {
         write_radiance(L, v);
         return false;
     }
@@ -1145,7 +1148,7 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
         t0 = t1;
     }
     v = path_of(L, o);
-    const bool alive = shade_head(S, tv, v, h, found, o.pdfmat, its);
+    const bool alive = shade_head<FULL>(S, tv, v, h, found, o.pdfmat, its);
     if constexpr (CLK) {
         if (lead) cs[3] += clock64() - t0;
         if (lead) ++(G > 1 ? clk->coop_bounces : clk->bounces);
@@ -1191,8 +1194,8 @@ __global__ __launch_bounds__(NH_BOUNCE_TB, NH_BOUNCE_WAVES) void wf_bounce_rr(co
         Its its;
         bool alive = true;
         if constexpr (STATS) t_ph = clock64();
-        if (L.first) alive = first_vertex<ORDERED, STATS>(S, tv, L, s, v, h, its, my_stk, NH_BOUNCE_TB, st_e, q_e);
-        else load_post_head(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
+        if (L.first) alive = first_vertex<ORDERED, STATS, FULL>(S, tv, L, s, v, h, its, my_stk, NH_BOUNCE_TB, st_e, q_e);
+        else load_post_head<FULL>(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
         if constexpr (STATS) c_load = clock64() - t_ph;
         if (alive) cont = rr_step<ORDERED, STATS, STATS, 1, FULL>(S, tv, L, v, its, h, my_stk, NH_BOUNCE_TB, st_e, st_s, q_e,
                                                                   q_s, &clk);

@@ -47,13 +47,17 @@ bool old_decrunch(Reader &r, uint8_t (*line)[4], int first, int len, std::string
         if (r.eof) return err = "truncated scanline", false;
         if (p[0] == 1 && p[1] == 1 && p[2] == 1) {
             if (x == 0) return err = "repeat code before the first pixel of a scanline", false;
-            for (long i = (long)p[3] << rshift; i > 0; --i) {
-                if (len <= 0) return err = "repeat code past the end of a scanline", false;
+            // the count p[3] << rshift, checked against the scanline's rest before it is formed: chained repeat codes
+            // grow rshift by 8 each, and the reference's int shift overflows (undefined) from rshift 24 on
+            if (p[3] != 0 && (rshift > 24 || ((uint64_t)p[3] << rshift) > (uint64_t)len))
+                return err = "repeat code past the end of a scanline", false;
+            for (uint64_t i = p[3] == 0 ? 0 : (uint64_t)p[3] << rshift; i > 0; --i) {
                 std::memcpy(line[x], line[x - 1], 4);
                 ++x;
                 --len;
             }
             rshift += 8;
+            if (rshift > 64) rshift = 64;  // (zero-count codes may chain without bound)
         } else {
             std::memcpy(line[x], p, 4);
             ++x;

@@ -232,6 +232,8 @@ struct SceneData {
     nh_denoiser denoiser{};  // type NH_DENOISER_NONE unless the scene has a <denoiser>
     // camera parameters kept for re-projection on resize
     float fov = 30.f, near_clip = 1e-4f, far_clip = 1e4f, focal = 10.f, fstop = 0.f, lens = 0.f;
+    // Independent::next2D's argument order as g++ compiles it (nh_camera.lens_draw_order)
+    int32_t lens_draw_order = NH_LENS_DRAWS_RTL;
     M4 to_world = M4::identity();
 };
 
@@ -594,14 +596,17 @@ void camera_update(SceneData &sd) {
     c.focal_distance = sd.focal;
     // cloneAndInit: fstop/lensRadius coupling (perspective.cpp:39-42)
     c.lens_radius = sd.lens;
+    c.lens_draw_order = sd.lens_draw_order;
 }
 
 namespace {
 
-// PNGTexture::loadFromFile for sRGB images (PNGTexture.cpp:70-84): lodepng RGBA8 -> InverseGammaCorrect(v / 255)
-void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w, unsigned &h);
+// PNGTexture::loadFromFile (PNGTexture.cpp:63-117): lodepng RGBA8 -> InverseGammaCorrect(v / 255) for sRGB images,
+// the normal-map decode otherwise (decode_texels); a .hdr file's floats as they are
+void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w, unsigned &h, bool srgb = true);
 
-// A Texture<Color3f> child (src/textures/consttexture.cpp, checkerboard.cpp, PNGTexture.cpp) -> nh_texture
+// A Texture<Color3f> child (src/textures/consttexture.cpp, checkerboard.cpp, PNGTexture.cpp) -> nh_texture: a
+// diffuse albedo, or a shape's normal map (Texture<Normal3f>, the same classes)
 nh_texture make_texture(const Obj &t, const std::string &base_dir, SceneData &sd) {
     nh_texture x{};
     const PropList &p = t.props;
@@ -618,8 +623,9 @@ nh_texture make_texture(const Obj &t, const std::string &base_dir, SceneData &sd
         x.value2[0] = b.x; x.value2[1] = b.y; x.value2[2] = b.z;
     } else if (t.type == "png_texture") {  // PNGTexture (PNGTexture.cpp:23-34, 125-160)
         x.type = NH_TEXTURE_PNG;
-        if (!p.get_bool("sRGB", p.get_string("name", "") != "normal"))
-            throw SceneError("png_texture: normal-map (sRGB=false) lookups are not supported as an albedo");
+        // sRGB defaults to false for the texture named "normal" (PNGTexture.cpp:26)
+        x.linear = p.get_bool("sRGB", p.get_string("name", "") != "normal") ? 0 : 1;
+        x.intensity = p.get_float("intensity", 1.f);
         x.spherical = p.get_bool("sphericalTexture", false) ? 1 : 0;
         xf::png_rotation(to_xf(p.get_vector("eulerAngles", v3(0, 0, 0))), x.rotation);
         x.scale_u = p.get_float("scaleU", 1.f);
@@ -628,13 +634,13 @@ nh_texture make_texture(const Obj &t, const std::string &base_dir, SceneData &sd
         x.offset_v = p.get_float("offsetV", 0.f);
         unsigned w = 0, h = 0;
         std::vector<float> px;
-        load_png_texels(join_path(base_dir, p.get_string("filename")), px, w, h);
+        load_png_texels(join_path(base_dir, p.get_string("filename")), px, w, h, x.linear == 0);
         x.width = (int32_t)w;
         x.height = (int32_t)h;
         x.texel_offset = sd.texels.size() / 4;
         sd.texels.insert(sd.texels.end(), px.begin(), px.end());
     } else {
-        throw SceneError("texture \"" + t.type + "\" is not supported as a diffuse albedo");
+        throw SceneError("texture \"" + t.type + "\" is not supported as a diffuse albedo or normal map");
     }
     return x;
 }
@@ -712,7 +718,37 @@ float inverse_gamma(float x) {  // PNGTexture.cpp:442-447
     return (float)std::pow((double)((x + 0.055f) * 1.f / 1.055f), (double)2.4f);
 }
 
-void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w, unsigned &h) {
+}  // namespace
+
+// PNGTexture::loadFromFile's byte -> float loop over lodepng's RGBA8 array (PNGTexture.cpp:78-95). sRGB: every byte
+// through InverseGammaCorrect(b / 255.f). Otherwise the normal-map decode: b / 255 * 2 - 1 (float / int: 255.f, 2.f,
+// 1.f), and after every third float `Eigen::Map<Eigen::Vector3f>(data + i - 2).normalize()` -- the triples run over
+// the RGBA array, so after the first pixel they straddle pixels and take in alpha (reproduced,
+// not fixed). Eigen 3.3.8's normalize(): z = squaredNorm() = x0^2 + (x1^2 + x2^2), and if z > 0 each component is
+// divided by sqrt(z) (Dot.h:145-150). Pinned against the reference's own lodepng + Eigen (oracle/normalmap_probe.cpp).
+void decode_texels(const uint8_t *px, size_t n, bool srgb, float *out) {
+    if (srgb) {
+        for (size_t i = 0; i < n; ++i) out[i] = inverse_gamma(static_cast<float>(px[i]) / 255.f);
+        return;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        out[i] = static_cast<float>(px[i]) / 255 * 2 - 1;
+        if ((i + 1) % 3 == 0) {
+            float *v = out + i - 2;
+            const float z = v[0] * v[0] + (v[1] * v[1] + v[2] * v[2]);
+            if (z > 0.f) {
+                const float s = std::sqrt(z);
+                v[0] /= s;
+                v[1] /= s;
+                v[2] /= s;
+            }
+        }
+    }
+}
+
+namespace {
+
+void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w, unsigned &h, bool srgb) {
     const auto dot = fn.find_last_of('.');
     const std::string ext = dot == std::string::npos ? std::string() : fn.substr(dot);
     // PNGTexture::loadFromFile's order (PNGTexture.cpp:63-72): existence first, then the extension
@@ -727,7 +763,7 @@ void load_png_texels(const std::string &fn, std::vector<float> &out, unsigned &w
     std::string err;
     if (!png_decode_rgba8(fn, px, w, h, err)) throw SceneError("PNGTexture: " + err);
     out.resize(px.size());
-    for (size_t i = 0; i < px.size(); ++i) out[i] = inverse_gamma(static_cast<float>(px[i]) / 255.f);
+    decode_texels(px.data(), px.size(), srgb, out.data());
 }
 
 // static_cast<unsigned int>(float) as the reference's x86-64 build executes it: cvttss2si to 64 bits and the low
@@ -885,6 +921,12 @@ void build_scene(const Obj &scene, const std::string &base_dir, SceneData &sd) {
                     emitter = 1;
                 } else if (sc->tag == "medium") {
                     throw SceneError("participating media are out of scope for path_mis");
+                } else if (sc->tag == "texture") {  // Shape::addChild ETexture (shape.cpp:138-147)
+                    const std::string nm = sc->props.get_string("name", "");
+                    if (nm != "normal") throw SceneError("Shape does not have a texture with name: " + nm);
+                    if (sh.normal_map) throw SceneError("There is already a normal map defined!");
+                    sd.textures.push_back(make_texture(*sc, base_dir, sd));
+                    sh.normal_map = (uint32_t)sd.textures.size();
                 } else {
                     throw SceneError("shape child <" + sc->tag + "> is not supported");
                 }
@@ -1113,6 +1155,31 @@ uint32_t nh_scene_add_texture(nh_scene *scene, const nh_texture *tex, const floa
     }
     scene->data->textures.push_back(t);
     return (uint32_t)scene->data->textures.size();
+}
+
+int nh_scene_set_normal_map(nh_scene *scene, uint32_t shape, uint32_t texture) {
+    if (!scene || shape >= scene->data->shapes.size() || texture > scene->data->textures.size()) {
+        nh::set_host_error("invalid shape or texture index");
+        return NH_ERR_INVALID;
+    }
+    scene->data->shapes[shape].normal_map = texture;
+    return NH_OK;
+}
+
+int nh_scene_set_lens_draw_order(nh_scene *scene, int32_t order) {
+    if (!scene || (order != NH_LENS_DRAWS_LTR && order != NH_LENS_DRAWS_RTL)) {
+        nh::set_host_error("invalid lens draw order");
+        return NH_ERR_INVALID;
+    }
+    scene->data->lens_draw_order = order;
+    nh::camera_update(*scene->data);
+    return NH_OK;
+}
+
+int nh_texture_decode(const uint8_t *rgba8, uint64_t n, int32_t srgb, float *out) {
+    if ((!rgba8 || !out) && n) { nh::set_host_error("null argument"); return NH_ERR_INVALID; }
+    nh::decode_texels(rgba8, (size_t)n, srgb != 0, out);
+    return NH_OK;
 }
 
 int nh_scene_set_integrator(nh_scene *scene, int32_t integrator) {

@@ -21,11 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # NH_LIB_PATH: an alternative in-tree build, for A/B measurements in one GPU session
 LIB_PATH = os.environ.get("NH_LIB_PATH") or os.path.join(_HERE, "lib", "libnori_hip.so")
 
-# One hardware queue per path-pool stream (nh_env.py): raised to 8 before the library's first HIP call unless a
-# larger value is set or NH_KEEP_HW_QUEUES keeps the caller's.
 from nh_env import raise_hw_queues  # noqa: E402  (nori_hip's own directory is on sys.path)
-
-raise_hw_queues()
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"nori_hip: HIP library not built ({LIB_PATH}); run `make` or __graft_entry__.build()")
@@ -40,6 +36,7 @@ INTEGRATOR_DIRECT = 5  # the point-light `direct` integrator of scenes/pa1 (dire
 MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1
 TRAVERSAL_REFERENCE, TRAVERSAL_ORDERED, TRAVERSAL_WIDE = 0, 1, 2
 DENOISER_NONE, DENOISER_SIMPLE = 0, 1
+LENS_DRAWS_LTR, LENS_DRAWS_RTL = 0, 1
 
 _f = C.c_float
 _i32 = C.c_int32
@@ -52,7 +49,7 @@ class nh_shape(C.Structure):
     _fields_ = [("type", _i32), ("bsdf", _i32), ("emitter", _i32), ("v_offset", _u32), ("n_vertices", _u32),
                 ("f_offset", _u32), ("n_faces", _u32), ("has_normals", _i32), ("has_uvs", _i32),
                 ("center", _f * 3), ("radius", _f), ("bbox_min", _f * 3), ("bbox_max", _f * 3),
-                ("pdf_offset", _u32), ("pdf_normalization", _f)]
+                ("pdf_offset", _u32), ("pdf_normalization", _f), ("normal_map", _u32)]
 
 
 class nh_bsdf(C.Structure):
@@ -66,7 +63,8 @@ TEXTURE_CONSTANT, TEXTURE_CHECKERBOARD, TEXTURE_PNG = 0, 1, 2
 class nh_texture(C.Structure):
     _fields_ = [("type", _i32), ("value1", _f * 3), ("value2", _f * 3), ("delta", _f * 2), ("scale", _f * 2),
                 ("width", _i32), ("height", _i32), ("texel_offset", C.c_uint64), ("scale_u", _f), ("scale_v", _f),
-                ("offset_u", _f), ("offset_v", _f), ("spherical", _i32), ("rotation", _f * 9), ("pad", _i32)]
+                ("offset_u", _f), ("offset_v", _f), ("spherical", _i32), ("rotation", _f * 9), ("linear", _i32),
+                ("intensity", _f), ("pad", _i32)]
 
 
 class nh_emitter(C.Structure):
@@ -77,7 +75,7 @@ class nh_emitter(C.Structure):
 class nh_camera(C.Structure):
     _fields_ = [("width", _i32), ("height", _i32), ("sample_to_camera", _f * 16), ("camera_to_world", _f * 16),
                 ("inv_output_size", _f * 2), ("near_clip", _f), ("far_clip", _f), ("lens_radius", _f),
-                ("focal_distance", _f)]
+                ("focal_distance", _f), ("lens_draw_order", _i32)]
 
 
 class nh_filter(C.Structure):
@@ -187,6 +185,9 @@ _sig("nh_scene_set_sample_count", _i32, _vp, _i32)
 _sig("nh_scene_set_bsdf", _i32, _vp, _u32, C.POINTER(nh_bsdf))
 _sig("nh_scene_set_integrator", _i32, _vp, _i32)
 _sig("nh_scene_add_texture", _u32, _vp, C.POINTER(nh_texture), _fp)
+_sig("nh_scene_set_normal_map", _i32, _vp, _u32, _u32)
+_sig("nh_scene_set_lens_draw_order", _i32, _vp, _i32)
+_sig("nh_texture_decode", _i32, C.POINTER(C.c_uint8), C.c_uint64, _i32, _fp)
 _sig("nh_scene_free", None, _vp)
 _sig("nh_host_last_error", C.c_char_p)
 _sig("nh_debug_transform", _i32, C.c_char_p, _fp, _i32)
@@ -217,6 +218,17 @@ _sig("nh_denoise_image", _i32, _vp, _fp, _i32, _i32, _i32, C.POINTER(nh_denoiser
 _sig("nh_last_error", C.c_char_p, _vp)
 
 lib = _lib
+_hip_used = False  # set by the first call that initialises the HIP runtime (device_count, Context)
+
+
+def configure_runtime(min_hw_queues: int = 8) -> int:
+    """Process settings the HIP runtime reads once, when it initialises: GPU_MAX_HW_QUEUES raised to min_hw_queues
+    (one hardware queue per path-pool stream, nh_env.py) unless a larger value is set or NH_KEEP_HW_QUEUES keeps the
+    caller's. An explicit call, not an import side effect; it must come before the first device_count() / Context().
+    Returns the value the runtime will see."""
+    if _hip_used:
+        raise RuntimeError("configure_runtime: the HIP runtime is already initialised in this process")
+    return raise_hw_queues(min_hw_queues)
 
 
 class NoriError(RuntimeError):
@@ -280,11 +292,14 @@ class Scene:
         _host_check(_lib.nh_scene_set_bsdf(self._h, shape, C.byref(b)), "set_bsdf")
 
     def add_texture(self, type: int, value1=(0, 0, 0), value2=(1, 1, 1), delta=(0, 0), scale=(1, 1), texels=None,
-                    scale_uv=(1, 1), offset_uv=(0, 0), spherical=False) -> int:
-        """Append an albedo texture (nh_scene_add_texture); returns the nh_bsdf.albedo_texture value naming it.
-        texels: (H, W, 4) float32 RGBA for TEXTURE_PNG (already sRGB-decoded, row 0 first)."""
+                    scale_uv=(1, 1), offset_uv=(0, 0), spherical=False, linear=False, intensity=1.0) -> int:
+        """Append a texture (nh_scene_add_texture); returns the value naming it in nh_bsdf.albedo_texture or
+        nh_shape.normal_map (set_normal_map). texels: (H, W, 4) float32 RGBA for TEXTURE_PNG, already decoded
+        (texture_decode), row 0 first; linear: sRGB = false (normal-map texels, eval blends by intensity)."""
         t = nh_texture()
         t.type = type
+        t.linear = int(linear)
+        t.intensity = intensity
         for i in range(3):
             t.value1[i], t.value2[i] = value1[i], value2[i]
         t.delta[0], t.delta[1] = delta
@@ -303,6 +318,14 @@ class Scene:
         if idx == 0:
             raise NoriError(f"add_texture: {_lib.nh_host_last_error().decode()}")
         return idx
+
+    def set_lens_draw_order(self, order: int):
+        """LENS_DRAWS_RTL (default, g++'s evaluation of Point2f(nextFloat(), nextFloat())) or LENS_DRAWS_LTR."""
+        _host_check(_lib.nh_scene_set_lens_draw_order(self._h, order), "set_lens_draw_order")
+
+    def set_normal_map(self, shape: int, texture: int):
+        """Shape::addChild(<texture name="normal">): texture = an add_texture value, 0 removes the map."""
+        _host_check(_lib.nh_scene_set_normal_map(self._h, shape, texture), "set_normal_map")
 
     @property
     def width(self):
@@ -325,6 +348,15 @@ class Scene:
         d = self.desc
         b = d.filter.border
         return (d.camera.height + 2 * b, d.camera.width + 2 * b, 4)
+
+
+def texture_decode(rgba8, srgb: bool) -> np.ndarray:
+    """PNGTexture::loadFromFile's byte -> float loop (nh_texture_decode): sRGB or the normal-map decode."""
+    b = np.ascontiguousarray(rgba8, dtype=np.uint8).ravel()
+    out = np.empty(b.size, dtype=np.float32)
+    _host_check(_lib.nh_texture_decode(b.ctypes.data_as(C.POINTER(C.c_uint8)), b.size, int(srgb), _fptr(out)),
+                "texture_decode")
+    return out
 
 
 class Bvh:
@@ -367,6 +399,8 @@ def debug_transform(request: str) -> np.ndarray:
 
 
 def device_count() -> int:
+    global _hip_used
+    _hip_used = True
     n = C.c_int(0)
     _lib.nh_get_device_count(C.byref(n))
     return n.value
@@ -376,6 +410,8 @@ class Context:
     """One GPU: device scene, BVH, master framebuffer (nh_ctx)."""
 
     def __init__(self, device: int = 0):
+        global _hip_used
+        _hip_used = True
         h = _vp()
         rc = _lib.nh_create(device, C.byref(h))
         if rc != NH_OK:

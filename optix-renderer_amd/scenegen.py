@@ -19,18 +19,20 @@ _REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIXTURE = os.path.join(_REPO, "tests", "golden", "reference_scenes.json")
 TEXTURED_FIXTURE = os.path.join(_REPO, "tests", "golden", "textured_scenes.json.gz")
 PROJECT_FIXTURE = os.path.join(_REPO, "tests", "golden", "project_scenes.json.gz")
+NORMALMAP_FIXTURE = os.path.join(_REPO, "tests", "golden", "normalmap_scenes.json.gz")
 
 C2_ALBEDO = "0.725 0.71 0.68"
 
 
 def materialize(out_dir: str) -> str:
     """Write the reference scene fixtures (reference_scenes.json, the textured scenes of textured_scenes.json.gz and
-    the depth-of-field / envmap scenes of project_scenes.json.gz) under out_dir; returns out_dir."""
+    the depth-of-field / envmap scenes of project_scenes.json.gz, the normal-mapped scenes of
+    normalmap_scenes.json.gz) under out_dir; returns out_dir."""
     import base64
     import gzip
     with open(FIXTURE) as f:
         files = json.load(f)
-    for bundle in (TEXTURED_FIXTURE, PROJECT_FIXTURE):
+    for bundle in (TEXTURED_FIXTURE, PROJECT_FIXTURE, NORMALMAP_FIXTURE):
         if os.path.exists(bundle):
             with gzip.open(bundle, "rt") as f:
                 files.update(json.load(f))

@@ -28,3 +28,18 @@ if [ -d "$REF/ext/eigen/Eigen" ]; then
   g++ -O2 -std=c++17 -ffp-contract=off -I"$REF/ext/eigen" "$(dirname "$0")/eigen_xform_probe.cpp" -o "$OUT/eigen_xform_probe"
   echo "built $OUT/eigen_xform_probe"
 fi
+# Texture / normal-map probe (oracle/normalmap_probe.cpp, test infrastructure): PNGTexture's decode loops, eval's
+# normal-map blend, the mesh TBN product and the sphere re-framing, over the reference's own lodepng + Eigen 3.3.8.
+# Built twice: with g++ and with clang++, whose argument evaluation orders differ (the "order" mode reports
+# Point2f(nextFloat(), nextFloat()) as each compiler evaluates it).
+if [ -d "$REF/ext/eigen/Eigen" ] && [ -f "$REF/ext/lodepng/src/lodepng.cpp" ]; then
+  PROBE_FLAGS="-O2 -std=c++17 -ffp-contract=off -include algorithm -I$REF/ext/eigen -I$REF/ext/lodepng/include -I$REF/ext/pcg32"
+  g++ $PROBE_FLAGS "$(dirname "$0")/normalmap_probe.cpp" "$REF/ext/lodepng/src/lodepng.cpp" -o "$OUT/normalmap_probe"
+  echo "built $OUT/normalmap_probe"
+  CLANGXX=/opt/rocm/llvm/bin/clang++
+  if [ -x "$CLANGXX" ]; then
+    "$CLANGXX" $PROBE_FLAGS "$(dirname "$0")/normalmap_probe.cpp" "$REF/ext/lodepng/src/lodepng.cpp" \
+      -o "$OUT/normalmap_probe_clang"
+    echo "built $OUT/normalmap_probe_clang"
+  fi
+fi

@@ -492,6 +492,31 @@ bool sphere_intersect(const nh_shape &sh, const Ray &ray, float &t) {  // sphere
     return false;
 }
 
+V3 texture_eval(const no_scene &s, const nh_texture &t, float u, float v);
+
+// mesh.cpp:176-182: Eigen::Matrix3f TBN; TBN << aTangent, aBitangent, normal (columns);
+// normal = (TBN * m_normalMap->eval(its.uv)).normalized(), each row of the product x0*y0 + (x1*y1 + x2*y2)
+V3 tbn_normal(V3 tg, V3 bt, V3 nrm, V3 nm) {
+    return normalized(mk(tg.x * nm.x + (bt.x * nm.y + nrm.x * nm.z), tg.y * nm.x + (bt.y * nm.y + nrm.y * nm.z),
+                         tg.z * nm.x + (bt.z * nm.y + nrm.z * nm.z)));
+}
+// sphere.cpp:117-120: n = its.shFrame.toWorld(eval(uv)).normalized() (Frame::toWorld = s * x + t * y + n * z,
+// frame.h:61-63); t = (Vector3f(0,0,1).cross(n)).normalized(); b = n.cross(t)
+Frame sphere_reframe(const Frame &f, V3 nm) {
+    Frame r;
+    r.n = normalized(f.s * nm.x + f.t * nm.y + f.n * nm.z);
+    r.s = normalized(cross(mk(0, 0, 1), r.n));
+    r.t = cross(r.n, r.s);
+    return r;
+}
+// PNGTexture::eval's !sRgb branch (PNGTexture.cpp:155-161): out.matrix().normalize() after the intensity blend
+V3 normal_blend(V3 out, float intensity) {
+    out.x = out.x * intensity;
+    out.y = out.y * intensity;
+    out.z = out.z * intensity + (1.f - intensity);
+    return normalized(out);
+}
+
 void set_hit_information(const no_scene &s, uint32_t shape, uint32_t prim, const Ray &ray, Its &its) {
     const nh_shape &sh = s.shapes[shape];
     its.shape = (int)shape;
@@ -510,6 +535,8 @@ void set_hit_information(const no_scene &s, uint32_t shape, uint32_t prim, const
         its.sh.s = t;
         its.sh.t = b;
         its.sh.n = n;
+        if (sh.normal_map)  // sphere.cpp:115-121
+            its.sh = sphere_reframe(its.sh, texture_eval(s, s.textures[sh.normal_map - 1], its.u, its.v));
         return;
     }
     // mesh.cpp:141-196
@@ -529,6 +556,8 @@ void set_hit_information(const no_scene &s, uint32_t shape, uint32_t prim, const
         if (sh.has_uvs) {
             V3 tg = normalized(bx * s.T[vi[0]] + by * s.T[vi[1]] + bz * s.T[vi[2]]);
             V3 bt = normalized(bx * s.BT[vi[0]] + by * s.BT[vi[1]] + bz * s.BT[vi[2]]);
+            if (sh.normal_map)  // mesh.cpp:173-183
+                nrm = tbn_normal(tg, bt, nrm, texture_eval(s, s.textures[sh.normal_map - 1], its.u, its.v));
             its.sh.s = tg;
             its.sh.t = bt;
             its.sh.n = nrm;
@@ -713,8 +742,9 @@ V3 texture_eval(const no_scene &s, const nh_texture &t, float u, float v) {
             u += t.offset_u;
             v += t.offset_v;
         }
-        return png_lookup(s.texels.data() + 4 * (size_t)t.texel_offset, (unsigned)t.width, (unsigned)t.height,
-                          t.scale_u, t.scale_v, u, v);
+        V3 out = png_lookup(s.texels.data() + 4 * (size_t)t.texel_offset, (unsigned)t.width, (unsigned)t.height,
+                            t.scale_u, t.scale_v, u, v);
+        return t.linear ? normal_blend(out, t.intensity) : out;  // !sRgb: a normal map
     }
     return mk(t.value1[0], t.value1[1], t.value1[2]);
 }
@@ -1207,12 +1237,15 @@ std::vector<uint32_t> serial_ray_index(int w, int h, int bs) {
 
 // The lens sample of serial camera ray k (perspective.cpp:118-122): the camera's static Independent sampler is a
 // default-state pcg32 that is never prepared (pcg32.h:40), two floats per sampleRay call, so ray k reads draws
-// 2k and 2k + 1 -- pcg32::advance gets there without the k - 1 rays before it
-void lens_jump(uint64_t k, float out[2]) {
+// 2k and 2k + 1 -- pcg32::advance gets there without the k - 1 rays before it. Point2f(nextFloat(), nextFloat()) takes them as
+// (x, y) = (2k + 1, 2k) when the compiler evaluates the arguments right to left (g++: nh_camera.lens_draw_order
+// NH_LENS_DRAWS_RTL), (2k, 2k + 1) left to right (clang)
+void lens_jump(const nh_camera &c, uint64_t k, float out[2]) {
     Pcg32 r;
     r.advance((int64_t)(2 * k));
-    out[0] = r.next_float();
-    out[1] = r.next_float();
+    const float a = r.next_float(), b = r.next_float();
+    out[0] = c.lens_draw_order == NH_LENS_DRAWS_RTL ? b : a;
+    out[1] = c.lens_draw_order == NH_LENS_DRAWS_RTL ? a : b;
 }
 
 }  // namespace
@@ -1239,6 +1272,8 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
     if (d->n_texels) s->texels.assign(d->texels, d->texels + 4 * (size_t)d->n_texels);
     for (const nh_bsdf &b : s->bsdfs)
         if (b.albedo_texture > s->textures.size()) return NH_ERR_INVALID;
+    for (const nh_shape &sh : s->shapes)
+        if (sh.normal_map > s->textures.size()) return NH_ERR_INVALID;
     s->emitters.assign(d->emitters, d->emitters + d->n_emitters);
     s->emitter_cdf.assign(d->emitter_cdf, d->emitter_cdf + d->n_emitters + 1);
     for (uint32_t i = 0; i < d->n_vertices; ++i) {
@@ -1573,6 +1608,24 @@ int no_denoise_simple(float *rgbw, int32_t width, int32_t height, int32_t border
 // The oracle's restated Eigen arithmetic on the probe's cases (oracle/eigen_probe.cpp layout): the same
 // helpers the path uses (dot, normalized, max_coeff, sqnorm, norm, cross, cwise chains; camera_ray's
 // 3x3 direction product and 4x4 point product)
+int no_normal_ops(int32_t n, const float *in, float *out) {
+    for (int32_t i = 0; i < n; ++i) {
+        const float *p = in + 13 * (size_t)i;
+        const V3 sv = mk(p[0], p[1], p[2]), tv = mk(p[3], p[4], p[5]), nv = mk(p[6], p[7], p[8]), v = mk(p[9], p[10], p[11]);
+        float *o = out + 15 * (size_t)i;
+        const V3 m = tbn_normal(sv, tv, nv, v);
+        Frame f;
+        f.s = sv;
+        f.t = tv;
+        f.n = nv;
+        const Frame r = sphere_reframe(f, v);
+        const V3 bl = normal_blend(v, p[12]);
+        const float vals[15] = {m.x, m.y, m.z, r.n.x, r.n.y, r.n.z, r.s.x, r.s.y, r.s.z, r.t.x, r.t.y, r.t.z, bl.x, bl.y, bl.z};
+        std::memcpy(o, vals, sizeof(vals));
+    }
+    return NH_OK;
+}
+
 int no_eigen_ops(int32_t n, const float *in, float *out) {
     for (int32_t i = 0; i < n; ++i) {
         const float *p = in + 36 * (size_t)i;
@@ -1675,7 +1728,7 @@ int no_path_radiance(const no_scene *s, uint64_t seed, int32_t px, int32_t py, i
     if (has_dof(s->cam)) {
         const int W = s->cam.width, H = s->cam.height;
         const uint64_t pos = serial_ray_index(W, H, 32)[(size_t)py * W + px];
-        lens_jump((uint64_t)(uint32_t)sample * (uint64_t)W * (uint64_t)H + pos, lens);
+        lens_jump(s->cam, (uint64_t)(uint32_t)sample * (uint64_t)W * (uint64_t)H + pos, lens);
     }
     Ray ray = camera_ray(s->cam, spx, spy, lens);
     V3 v = li(*s, smp, ray);
@@ -1743,10 +1796,11 @@ int no_render(const no_scene *s, int32_t mode, uint64_t seed, int32_t s0, int32_
                         float spx = (float)px + jx, spy = (float)py + jy;
                         float lens[2] = {0.f, 0.f};
                         if (dof && lens_serial) {
-                            lens[0] = lens_stream.next_float();  // sampler->next2D()
-                            lens[1] = lens_stream.next_float();
+                            const float a = lens_stream.next_float(), b = lens_stream.next_float();  // next2D()
+                            lens[0] = s->cam.lens_draw_order == NH_LENS_DRAWS_RTL ? b : a;
+                            lens[1] = s->cam.lens_draw_order == NH_LENS_DRAWS_RTL ? a : b;
                         } else if (dof) {
-                            lens_jump((uint64_t)(uint32_t)smp_i * (uint64_t)W * (uint64_t)H +
+                            lens_jump(s->cam, (uint64_t)(uint32_t)smp_i * (uint64_t)W * (uint64_t)H +
                                           ray_pos[(size_t)py * W + px], lens);
                         }
                         Ray ray = camera_ray(s->cam, spx, spy, lens);
@@ -1789,7 +1843,7 @@ int no_ttest_scene(const no_scene *s, uint64_t *state, uint64_t *inc, int32_t n,
         float ax, ay;
         smp.next2d(ax, ay);
         float lens[2] = {0.f, 0.f};
-        if (has_dof(s->cam)) lens_jump((uint64_t)k, lens);  // the k-th sampleRay of this serial loop
+        if (has_dof(s->cam)) lens_jump(s->cam, (uint64_t)k, lens);  // the k-th sampleRay of this serial loop
         Ray ray = camera_ray(s->cam, spx, spy, lens);
         V3 v = li(*s, smp, ray);
         double r = (double)luminance(v);

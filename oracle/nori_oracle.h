@@ -46,6 +46,10 @@ int no_bvh_export(const no_scene *s, nh_bvh_node *nodes, uint32_t *indices);
 /* the oracle's restated Eigen arithmetic on n cases of 36 floats (oracle/eigen_probe.cpp layout) -> 28 floats
    each, for the bit-for-bit comparison with the reference's Eigen */
 int no_eigen_ops(int32_t n, const float *in, float *out);
+/* the oracle's normal-map arithmetic on n cases of 13 floats (s3 t3 n3 v3 intensity, oracle/normalmap_probe.cpp "ops"
+   layout) -> 15 floats each: normalize(TBN * v) (mesh.cpp:176-182), the sphere's re-derived frame n', t', b'
+   (sphere.cpp:117-120) and PNGTexture::eval's normal-map blend of v (PNGTexture.cpp:155-161) */
+int no_normal_ops(int32_t n, const float *in, float *out);
 
 /* SimpleDenoiser::denoise (src/denoiser/simple.cpp:29-76) in place on an (W+2b)(H+2b)x4 RGBW ImageBlock,
    serial row-major order (the reference with one thread) */

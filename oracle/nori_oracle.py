@@ -53,6 +53,7 @@ _sig("no_bsdf_pdf", C.c_float, C.POINTER(nh.nh_bsdf), _fp, _fp)
 _sig("no_texture_eval", _i32, _vp, _u32, _i32, _fp, _fp, _fp)
 _sig("no_bsdf_pdf_batch", _i32, C.POINTER(nh.nh_bsdf), _fp, _i32, _fp, _fp)
 _sig("no_eigen_ops", _i32, _i32, _fp, _fp)
+_sig("no_normal_ops", _i32, _i32, _fp, _fp)
 _sig("no_denoise_simple", _i32, _fp, _i32, _i32, _i32, C.POINTER(nh.nh_denoiser))
 _sig("no_chi2_histogram", _i32, C.POINTER(nh.nh_bsdf), _fp, _u64p, _u64p, _i32, _i32, _i32, C.POINTER(C.c_double))
 
@@ -209,6 +210,14 @@ def denoise_simple(rgbw, border: int, params) -> np.ndarray:
     h, w = out.shape[0] - 2 * border, out.shape[1] - 2 * border
     if _lib.no_denoise_simple(out.ctypes.data_as(_fp), w, h, border, C.byref(params)) != 0:
         raise RuntimeError("no_denoise_simple: invalid arguments")
+    return out
+
+
+def normal_ops(cases):
+    """The oracle's normal-map arithmetic (no_normal_ops) on (n, 13) float32 cases -> (n, 15)."""
+    cases = np.ascontiguousarray(cases, np.float32)
+    out = np.zeros((len(cases), 15), np.float32)
+    _lib.no_normal_ops(len(cases), cases.ctypes.data_as(_fp), out.ctypes.data_as(_fp))
     return out
 
 

@@ -11,6 +11,8 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    import nori_hip as nh
+    nh.configure_runtime()  # before any test touches HIP: one hardware queue per path pool (nh_env.py)
 
 
 @pytest.fixture(scope="session")

@@ -21,6 +21,10 @@ Writes (all data, no reference source):
                           table_path_mis.xml, path_mis, thin lens) with their meshes, and its envmap scene
                           scenes/project/envmap/envmap_sphere.xml with the shipped res/wooden_motel.png (binary
                           files stored as {"base64": ...})
+  normalmap_scenes.json.gz the reference's normal-mapped scenes that run an in-scope integrator
+                          (scenes/project/normalmap/normals-identity-direct.xml and normals-primitives-direct.xml,
+                          direct_mis; normals-camel.xml, direct) with their meshes and the shipped normal maps
+                          res/normal-identity.png, normal-primitives.png, normal-test.png (same form)
 """
 import base64
 import gzip
@@ -96,6 +100,20 @@ PROJECT_FILES = [
 ]
 
 
+NORMALMAP_FILES = [
+    "scenes/project/normalmap/normals-identity-direct.xml",
+    "scenes/project/normalmap/normals-primitives-direct.xml",
+    "scenes/project/normalmap/normals-camel.xml",
+    "scenes/project/meshes/plane.obj",
+    "scenes/project/meshes/cube.obj",
+    "scenes/project/meshes/cone.obj",
+    "scenes/project/meshes/camelhead.obj",
+    "scenes/project/res/normal-identity.png",
+    "scenes/project/res/normal-primitives.png",
+    "scenes/project/res/normal-test.png",
+]
+
+
 def read_fixture(ref, rel):
     data = open(os.path.join(ref, rel), "rb").read()
     try:
@@ -153,7 +171,11 @@ def main():
     project = {p: read_fixture(ref, p) for p in PROJECT_FILES}
     with open(os.path.join(HERE, "project_scenes.json.gz"), "wb") as f:
         f.write(gzip.compress(json.dumps(project, indent=0).encode(), mtime=0))
-    print("wrote pcg32_kat.json, reference_scenes.json, textured_scenes.json.gz, project_scenes.json.gz")
+    normalmap = {p: read_fixture(ref, p) for p in NORMALMAP_FILES}
+    with open(os.path.join(HERE, "normalmap_scenes.json.gz"), "wb") as f:
+        f.write(gzip.compress(json.dumps(normalmap, indent=0).encode(), mtime=0))
+    print("wrote pcg32_kat.json, reference_scenes.json, textured_scenes.json.gz, project_scenes.json.gz, "
+          "normalmap_scenes.json.gz")
 
 
 if __name__ == "__main__":

@@ -37,12 +37,14 @@ def dof_cbox(tmp_path, lens=0.08, focal=3.2):
     return path
 
 
+@pytest.mark.parametrize("order", [nh.LENS_DRAWS_RTL, nh.LENS_DRAWS_LTR])
 @pytest.mark.parametrize("mode", [no.PER_PATH, no.NORI_BLOCK])
-def test_lens_advance_equals_serial_stream(tmp_path, mode):
+def test_lens_advance_equals_serial_stream(tmp_path, mode, order):
     """70x45 (3x2 blocks, ragged right and bottom edges), 3 rounds: every ray's lens sample by advance(2k) equals
-    the literal sequential stream of the serial render loop, bit for bit."""
+    the literal sequential stream of the serial render loop, bit for bit, in both next2D argument orders."""
     s = nh.Scene(dof_cbox(tmp_path))
     s.set_resolution(70, 45)
+    s.set_lens_draw_order(order)
     orc = no.OracleScene(s)
     serial = orc.render(0, 3, seed=3, mode=mode | no.LENS_SERIAL, threads=1)
     jump = orc.render(0, 3, seed=3, mode=mode, threads=4)
@@ -101,3 +103,18 @@ def test_reference_dof_scene_oracle_crop_serial(proj_dir):
     orc = no.OracleScene(s)
     np.testing.assert_array_equal(orc.render(0, 2, seed=1, mode=no.LENS_SERIAL, threads=1),
                                   orc.render(0, 2, seed=1, threads=4))
+
+
+def test_lens_draw_order_default_and_effect(tmp_path):
+    """The loader defaults to g++'s evaluation of Point2f(nextFloat(), nextFloat()) (right to left: x = draw 2k + 1,
+    pinned by oracle/normalmap_probe "order" in test_normalmap.py); the other order gives another image."""
+    s = nh.Scene(dof_cbox(tmp_path))
+    assert s.desc.camera.lens_draw_order == nh.LENS_DRAWS_RTL
+    s.set_resolution(48, 40)
+    rtl = no.OracleScene(s).render(0, 2, seed=3)
+    s.set_lens_draw_order(nh.LENS_DRAWS_LTR)
+    assert s.desc.camera.lens_draw_order == nh.LENS_DRAWS_LTR
+    ltr = no.OracleScene(s).render(0, 2, seed=3)
+    assert not np.array_equal(rtl, ltr)
+    with pytest.raises(nh.NoriError):
+        s.set_lens_draw_order(2)

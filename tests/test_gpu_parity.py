@@ -334,7 +334,10 @@ def test_render_parity_black_envmap_mirror(gpu, tmp_path, mode):
                                   "NH_FUSED=0", "NH_SORT=0", "NH_SORT=1", "NH_FUSED=1,NH_TAIL=0",
                                   "NH_SORT_SHADE=1", "NH_FUSED=0,NH_SORT_SHADE=1", "NH_RR_AHEAD=0",
                                   "NH_RR_AHEAD=0,NH_TAIL=0", "NH_TRACE2=0", "NH_PERSISTENT=1,NH_TRACE2=0",
-                                  "NH_LDS_FRAMES=0", "NH_EMIT_FACES=0"])
+                                  "NH_LDS_FRAMES=0", "NH_EMIT_FACES=0",
+                                  # the count kernel's handoff: the runtime copy + memset fallback, alone
+                                  # and with in-place chunk ends
+                                  "NH_COUNT_KERNEL=0", "NH_COUNT_KERNEL=0,NH_TAIL=0"])
 def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
     """The traversal variants the wavefront picks per scene (persistent ray-fetching traversal for
     deep BVHs over the binary or the 4-wide tree, per-lane traversal, LDS-staged small BVHs) all give

@@ -64,6 +64,21 @@ def test_reference_dof_scene_crops(gpu, proj_dir, rel, rect, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+def test_dof_crop_clang_draw_order_and_late_rounds(gpu, proj_dir, mode):
+    """dof-val.xml with the other next2D argument order (x = draw 2k, as clang compiles Independent::next2D) over
+    rounds [300, 302) and [255, 257) (the lens tables' low / high round split at 256): GPU = oracle bit for bit."""
+    s = nh.Scene(os.path.join(proj_dir, "scenes/project/dof/dof-val.xml"))
+    s.set_lens_draw_order(nh.LENS_DRAWS_LTR)
+    d = s.desc.camera
+    blocks = blocks_of(d.width, d.height, 352, 160, 480, 256)
+    orc = no.OracleScene(s)
+    for r0 in (300, 255):
+        g = gpu_render(s, r0, r0 + 2, blocks, mode, seed=5)
+        r = orc.render(r0, r0 + 2, seed=5, blocks=blocks)
+        np.testing.assert_array_equal(g, r)
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_dof_block_split_and_round_offset(gpu, proj_dir, mode):
     """dof-val.xml: the crop's blocks split in two renders (alternate blocks, as two ranks take them) over rounds
     [3, 5): each half equals the oracle's render of the same blocks and rounds."""
@@ -107,3 +122,90 @@ def test_reference_envmap_sphere_crop(gpu, proj_dir, mode):
     print(f"envmap_sphere mode={mode}: {len(blocks)} blocks, max|d| {np.abs(g - r).max():.3e}")
     np.testing.assert_array_equal(g, r)
     assert np.abs(r[..., :3]).sum() > 0
+
+
+# ---- shape normal maps (tests/golden/normalmap_scenes.json.gz) -------------------------
+# Mesh::setHitInformation's TBN branch (mesh.cpp:173-183), Sphere::setHitInformation's re-framing (sphere.cpp:115-121)
+# and PNGTexture's normal-map decode + eval (PNGTexture.cpp:26, :85-95, :155-161); the decode and the arithmetic are
+# pinned against the reference's own lodepng + Eigen in test_normalmap.py.
+NORMALMAP_CROPS = [
+    ("scenes/project/normalmap/normals-identity-direct.xml", (224, 160, 576, 416)),    # sphere, cube, cone, plane
+    ("scenes/project/normalmap/normals-primitives-direct.xml", (224, 160, 576, 416)),
+    ("scenes/project/normalmap/normals-camel.xml", (224, 128, 544, 448)),              # the camel head (22.7k tris)
+]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("rel,rect", NORMALMAP_CROPS)
+def test_reference_normalmap_scene_crops(gpu, proj_dir, rel, rect, mode):
+    s = nh.Scene(os.path.join(proj_dir, rel))
+    d = s.desc
+    assert any(d.shapes[i].normal_map for i in range(d.n_shapes))
+    blocks = blocks_of(d.camera.width, d.camera.height, *rect)
+    g = gpu_render(s, 0, 3, blocks, mode)
+    r = no.OracleScene(s).render(0, 3, seed=7, blocks=blocks)
+    print(f"{rel} mode={mode}: {len(blocks)} blocks, max|d| {np.abs(g - r).max():.3e}")
+    np.testing.assert_array_equal(g, r)
+    assert np.abs(r[..., :3]).sum() > 0
+
+
+def normalmap_cbox(tmp_path, variant="c1", camel=False):
+    """The Cornell box (path_mis) with normal maps: both spheres (c1: mirror + dielectric) take normal-test.png, a
+    cube mesh with normals and uvs takes normal-primitives.png at intensity 0.7; camel = the camel head (normals +
+    uvs, 22.7k triangles: a BVH past the LDS-staged size) with normal-test.png in place of the cube."""
+    proj = scenegen.materialize(str(tmp_path))
+    nm = ('<texture type="png_texture" name="normal"><string name="filename" value="../../project/res/{}"/>'
+          '{}</texture>')
+    if camel:
+        mesh = ('<shape type="obj"><string name="filename" value="../../project/meshes/camelhead.obj"/>'
+                + nm.format("normal-test.png", "") +
+                '<bsdf type="diffuse"><color name="albedo" value="0.6 0.5 0.4"/></bsdf>'
+                '<transform name="toWorld"><scale value="1.4,1.4,1.4"/><translate value="0,0.55,-0.1"/></transform>'
+                '</shape>')
+    else:
+        mesh = ('<shape type="obj"><string name="filename" value="../../project/meshes/cube.obj"/>'
+                + nm.format("normal-primitives.png", '<float name="intensity" value="0.7"/>') +
+                '<bsdf type="diffuse"><color name="albedo" value="0.5 0.6 0.7"/></bsdf>'
+                '<transform name="toWorld"><scale value="0.3,0.3,0.3"/><rotate axis="0,1,0" angle="30"/>'
+                '<translate value="0.1,0.15,-0.55"/></transform></shape>')
+    xml = scenegen.cbox_xml(str(tmp_path), variant, extra_shapes=mesh, drop_spheres=camel)
+    text = open(xml).read()
+    if not camel:
+        text = text.replace('<float name="radius" value="0.3263" />',
+                            '<float name="radius" value="0.3263" />' + nm.format("normal-test.png", ""))
+        assert text.count("normal-test.png") == 2
+    path = os.path.join(os.path.dirname(xml), f"cbox_{variant}_nmap{'_camel' if camel else ''}.xml")
+    with open(path, "w") as f:
+        f.write(text)
+    return path
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("variant", ["c1", "c2"])
+def test_normalmap_cbox_path_mis(gpu, tmp_path, variant, mode):
+    """path_mis on a Cornell box whose spheres and a cube mesh carry normal maps, whole image (96x72, 6 spp) through
+    the default pipelines: GPU = oracle bit for bit (c1: mirror + dielectric spheres; c2: diffuse spheres)."""
+    s = nh.Scene(normalmap_cbox(tmp_path, variant))
+    d = s.desc
+    assert [d.shapes[i].normal_map != 0 for i in range(d.n_shapes)].count(True) == 3
+    s.set_resolution(96, 72)
+    g = gpu_render(s, 0, 6, None, mode, seed=4)
+    r = no.OracleScene(s).render(0, 6, seed=4)
+    np.testing.assert_array_equal(g, r)
+    s2 = nh.Scene(normalmap_cbox(tmp_path, variant))
+    s2.set_resolution(96, 72)
+    for i in range(s2.desc.n_shapes):
+        s2.set_normal_map(i, 0)
+    plain = no.OracleScene(s2).render(0, 6, seed=4)
+    assert not np.array_equal(plain, r)  # the maps do change the image
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_normalmap_deep_bvh_path_mis(gpu, tmp_path, mode):
+    """The camel head (normals + uvs, 22.7k triangles, a BVH the kernels traverse from HBM) with a normal map in the
+    Cornell box, path_mis, 64x64, 4 spp: GPU = oracle bit for bit."""
+    s = nh.Scene(normalmap_cbox(tmp_path, "c2", camel=True))
+    s.set_resolution(64, 64)
+    g = gpu_render(s, 0, 4, None, mode, seed=8)
+    r = no.OracleScene(s).render(0, 4, seed=8)
+    np.testing.assert_array_equal(g, r)

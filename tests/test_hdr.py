@@ -145,6 +145,15 @@ BAD_FILES = {  # name: (file, the decoder's reason)
     "repeat_first": (H + b"-Y 1 +X 2\n\x01\x01\x01\x02", "before the first pixel"),
     "repeat_past_end": (H + b"-Y 1 +X 2\n\x80\x80\x80\x80\x01\x01\x01\x05", "past the end"),
     "run_past_end": (H + b"-Y 1 +X 8\n\x02\x02\x00\x08" + b"\x89\x10" + b"\x88\x10" * 3, "run past the end"),
+    # chained repeat codes: the count n << 8k must be checked before it is formed -- after three codes in
+    # a row the reference's int shift is at 24 (n >= 128: negative), after four at 32 (undefined); both are errors,
+    # not a silently skipped repeat
+    "repeat_chain_24": (H + b"-Y 1 +X 4\n\x80\x80\x80\x80" + b"\x01\x01\x01\x00" * 3 + b"\x01\x01\x01\x80",
+                        "past the end"),
+    "repeat_chain_32": (H + b"-Y 1 +X 4\n\x80\x80\x80\x80" + b"\x01\x01\x01\x00" * 4 + b"\x01\x01\x01\x01",
+                        "past the end"),
+    "repeat_chain_64": (H + b"-Y 1 +X 4\n\x80\x80\x80\x80" + b"\x01\x01\x01\x00" * 9 + b"\x01\x01\x01\xff",
+                        "past the end"),
     "truncated_rle": (H + b"-Y 1 +X 8\n\x02\x02\x00\x08\x88\x10\x88\x10", "scanline 0: truncated"),
 }
 
@@ -169,6 +178,9 @@ def test_hdr_well_formed_minimal_files(tmp_path):
         H + b"-Y 1 +X 8\n\x02\x02\x00\x08\x88\x10\x88\x20\x88\x30\x88\x80":
             np.broadcast_to(np.uint8([16, 32, 48, 128]), (1, 8, 4)),
     }
+    # zero-count repeat codes chain without effect (each only shifts the next count), then a literal pixel resets it
+    cases[H + b"-Y 1 +X 2\n\x80\x40\x20\x81" + b"\x01\x01\x01\x00" * 6 + b"\x10\x20\x30\x82"] = \
+        np.uint8([[[128, 64, 32, 129], [16, 32, 48, 130]]])
     for raw, rgbe in cases.items():
         open(os.path.join(d, "sky_8x4.hdr"), "wb").write(raw)
         np.testing.assert_array_equal(env_texels(nh.Scene(xml)), scenegen.rgbe_decode_reference(rgbe))
