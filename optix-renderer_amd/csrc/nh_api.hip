@@ -1507,7 +1507,8 @@ static int pool_handoff(nh_ctx *c, WfPool &p, WfPool &T, int bound, hipEvent_t *
     HIP_TRY(c, hipStreamWaitEvent(T.stream, p.ev_handoff, 0));
     HIP_TRY(c, hipEventRecord(ev[1], T.stream));
     HIP_TRY(c, hipEventRecord(ev[2], T.stream));
-    nh::launch_wf_tail_rr(c->d_scene, c->tv, L, T.job.ordered, T.job.stats, bound, c->specular, T.stream);
+    nh::launch_wf_tail_rr(c->d_scene, c->tv, L, T.job.ordered, T.job.stats, bound, c->specular,
+                          !c->specular && !c->textured, T.stream);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(ev[3], T.stream));
     T.tail = true;
@@ -1570,7 +1571,9 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
         HIP_TRY(c, hipEventRecord(ev[1], p.stream));
         HIP_TRY(c, hipEventRecord(ev[2], p.stream));
         if (it > 0 && (int64_t)bound <= p.tail_at) {
-            if (p.rr) nh::launch_wf_tail_rr(c->d_scene, c->tv, L, ordered, stats, bound, c->specular, p.stream);
+            if (p.rr)
+                nh::launch_wf_tail_rr(c->d_scene, c->tv, L, ordered, stats, bound, c->specular, !c->specular && !c->textured,
+                                      p.stream);
             else nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, false, bound, c->depth, p.stream);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev[3], p.stream));

@@ -198,7 +198,7 @@ void launch_wf_bounce(const nhd::DScene *S, const nhd::Traversal &tv, const WfLa
 void launch_wf_bounce_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
                          bool lean, int bound, hipStream_t st);
 void launch_wf_tail_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
-                       bool specular, hipStream_t st);
+                       bool specular, bool lean, hipStream_t st);
 void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                     bool wide, int bound, int depth, hipStream_t st);
 // copies the live RR-ahead paths of L's input queue (at most bound) densely into dst, count into dst_counts[0]

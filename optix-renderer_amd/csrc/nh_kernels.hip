@@ -230,7 +230,7 @@ __global__ __launch_bounds__(64) void nh_trace_wide_kernel(const DScene *__restr
     const int i = blockIdx.x * 64 + threadIdx.x;
     TravStats st{0, 0, 0};
     if (i < n) {
-        RingStack2<16> stk{s_ref + threadIdx.x, s_near + threadIdx.x, 64, spill + (size_t)i * spill_depth};
+        RingStack2<16> stk{s_ref + threadIdx.x, s_near + threadIdx.x, 64, spill, (unsigned)n, (unsigned)i};
         Tracer4<ORDERED, ANY, STATS, RingStack2<16>> tr;
         tr.begin(S, tv, f3(rb.ox[i], rb.oy[i], rb.oz[i]), f3(rb.dx[i], rb.dy[i], rb.dz[i]), rb.mint[i], rb.maxt[i], st);
         while (!tr.done) tr.step(tv, stk, st);

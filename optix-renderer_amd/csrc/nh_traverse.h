@@ -751,17 +751,23 @@ constexpr int kWideEmpty = (int)0x80000000;
 #endif
 
 // Traversal stack of one lane, (ref, entry distance) pairs: the top K entries live in LDS
-// (lane-interleaved, `stride` words apart), deeper entries spill to the lane's own global area.
+// (lane-interleaved, `stride` words apart), deeper entries spill to a global area, lane-interleaved too: spill entry
+// j of lane g at glob[j * lanes + g] (glob and lanes uniform). The lane keeps only its 32-bit index g live -- a
+// per-lane 64-bit pointer into its own region was two more VGPRs, which the persistent kernels spilled to scratch at
+// their 96-VGPR budget -- and lanes that spill at the same depth write neighbouring words.
 template <int K>
 struct RingStack2 {
     static_assert((K & (K - 1)) == 0, "K must be a power of two");
     int *lds_ref;      // this lane's first LDS slot (refs)
     float *lds_near;   // this lane's first LDS slot (entry distances)
     int stride;
-    int2 *glob;        // this lane's spill area
+    int2 *glob;        // spill area (uniform)
+    unsigned lanes;    // lanes sharing it (uniform)
+    unsigned g;        // this lane's index
+    NHD int2 &spill(int j) const { return glob[(size_t)(unsigned)j * lanes + g]; }
     NHD void push(int i, int ref, float nr) {
         const int o = (i & (K - 1)) * stride;
-        if (i >= K) glob[i - K] = make_int2(lds_ref[o], __float_as_int(lds_near[o]));
+        if (i >= K) spill(i - K) = make_int2(lds_ref[o], __float_as_int(lds_near[o]));
         lds_ref[o] = ref;
         lds_near[o] = nr;
     }
@@ -773,7 +779,7 @@ struct RingStack2 {
             const int i = i0 + j;
             if (j < m && i >= K) {
                 const int o = (i & (K - 1)) * stride;
-                glob[i - K] = make_int2(lds_ref[o], __float_as_int(lds_near[o]));
+                spill(i - K) = make_int2(lds_ref[o], __float_as_int(lds_near[o]));
             }
         }
     }
@@ -787,7 +793,7 @@ struct RingStack2 {
         ref = lds_ref[o];
         nr = lds_near[o];
         if (i >= K) {
-            const int2 e = glob[i - K];
+            const int2 e = spill(i - K);
             lds_ref[o] = e.x;
             lds_near[o] = __int_as_float(e.y);
         }

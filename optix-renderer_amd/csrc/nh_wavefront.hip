@@ -322,7 +322,10 @@ struct PtStack<true> {
         s.lds_ref = reinterpret_cast<int *>(lds) + threadIdx.x;
         s.lds_near = reinterpret_cast<float *>(lds + kRingEntries / 2 * 128) + threadIdx.x;
         s.stride = 128;
-        s.glob = reinterpret_cast<int2 *>(L.trav_spill + ((size_t)blockIdx.x * 128 + threadIdx.x) * (size_t)L.spill_depth);
+        // kPersistentBlocks * 128 lanes x spill_depth / 2 entries (every WIDE grid is capped at kPersistentBlocks)
+        s.glob = reinterpret_cast<int2 *>(L.trav_spill);
+        s.lanes = (unsigned)kPersistentBlocks * 128u;
+        s.g = blockIdx.x * 128u + threadIdx.x;
         return s;
     }
 };
@@ -1248,7 +1251,8 @@ __global__ __launch_bounds__(NH_BOUNCE_TB, NH_BOUNCE_WAVES) void wf_bounce_rr(co
 // bounces that sets the tail's length then tests each leaf's primitives in one parallel step instead of one after
 // the other. Only which lanes run which operation changes; every path's operations and draws are the same.
 constexpr int kTailCoopWords = 48;  // 32-bit words of one handed-over path (PathV, Hit, Its, bounce count)
-template <bool ORDERED, bool STATS, int TB, int W>
+// FULL = false: the lean body of wf_bounce_rr<.., FULL = false> (scenes with no mirror / dielectric BSDF and no texture)
+template <bool ORDERED, bool STATS, int TB, int W, bool FULL = true>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf_tail_rr(
     const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L, int coop) {
     __shared__ uint32_t stk[16 * TB];
@@ -1268,14 +1272,14 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
     Hit h;
     Its its;
     unsigned long long nb = 0;  // bounces of this lane's path
-    if (alive) load_post_head(S, tv, L, B, queue_slot(qv.pre, L.seg_cap, q), v, h, its);
+    if (alive) load_post_head<FULL>(S, tv, L, B, queue_slot(qv.pre, L.seg_cap, q), v, h, its);
     const bool can_coop = TB == 64 && coop == 16;
     for (;;) {
         const unsigned long long m = __ballot(alive);
         if (m == 0ull || (can_coop && __popcll(m) <= 4)) break;
         if (alive) {
-            alive = rr_step<ORDERED, STATS, STATS>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s, q_e, q_s,
-                                                   &clk);
+            alive = rr_step<ORDERED, STATS, STATS, 1, FULL>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s,
+                                                            q_e, q_s, &clk);
             ++nb;
         }
     }
@@ -1305,8 +1309,8 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
             }
             while (__ballot(carry)) {
                 if (carry) {
-                    carry = rr_step<ORDERED, STATS, STATS, 16>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s, q_e,
-                                                              q_s, &clk);
+                    carry = rr_step<ORDERED, STATS, STATS, 16, FULL>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e,
+                                                                    st_s, q_e, q_s, &clk);
                     ++nb;
                 }
             }
@@ -1590,14 +1594,17 @@ void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L
 }
 
 void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
-                       bool specular, hipStream_t st) {
+                       bool specular, bool lean, hipStream_t st) {
     const char *e = std::getenv("NH_TAIL_WG");  // threads per tail workgroup: 64 (default) or 256
     const int tb = e && std::atoi(e) == 256 ? 256 : 64;
     // register budget, NH_TAIL_RR_WAVES=1|4: by default 1 wave/SIMD for scenes with mirror / dielectric BSDFs (their
     // long chains: shorter tails on C1 and C4, profiles/round4_session4_ab.txt) and 4 otherwise (a short tail that
     // leaves the next chunk's bounce kernels their occupancy: C2 +0.5 %, profiles/round4_session11_12_c2_ab.txt)
+    // (NH_TAIL_RR_WAVES=2: 256 VGPRs, an A/B point between the two). lean (NH_TAIL_LEAN=0 off): the FULL = false body
     const char *w = std::getenv("NH_TAIL_RR_WAVES");
-    const bool w1 = w ? std::atoi(w) == 1 : specular;
+    const int waves = w ? (std::atoi(w) == 1 ? 1 : std::atoi(w) == 2 ? 2 : 4) : specular ? 1 : 4;
+    const char *ln = std::getenv("NH_TAIL_LEAN");
+    if (ln && ln[0] == '0') lean = false;
     const char *cp = std::getenv("NH_TAIL_COOP");  // lanes per path once <= 4 remain in a wave: 16 (default) or 1
     const int coop = cp && std::atoi(cp) == 1 ? 1 : 16;
     // one path per lane: the grid covers the bound (tail bounds are <= kTailCap paths)
@@ -1606,7 +1613,11 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
 #define NH_TR(O, T)                                                                                         \
     do {                                                                                                    \
         if (tb == 256) hipLaunchKernelGGL((wf_tail_rr<O, T, 256, 1>), grid, dim3(256), lds, st, S, tv, L, coop); \
-        else if (w1) hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 1>), grid, dim3(64), lds, st, S, tv, L, coop);   \
+        else if (waves == 1) hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 1>), grid, dim3(64), lds, st, S, tv, L, coop); \
+        else if (lean && waves == 2)                                                                        \
+            hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 2, false>), grid, dim3(64), lds, st, S, tv, L, coop);  \
+        else if (waves == 2) hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 2>), grid, dim3(64), lds, st, S, tv, L, coop); \
+        else if (lean) hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 4, false>), grid, dim3(64), lds, st, S, tv, L, coop); \
         else hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 4>), grid, dim3(64), lds, st, S, tv, L, coop);           \
     } while (0)
     if (ordered) { if (stats) NH_TR(true, true); else NH_TR(true, false); }

@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # Interleaved A/B of environment settings on one build: scripts/ab_env.sh ROUNDS "c2 c4" "NH_X=0 NH_X=1" [bench args]
-# prints Msamples/s, ms/step, splat ms per launch and the dominant kernel's ms per launch per run
+# prints Msamples/s, ms/step, splat ms per launch, the dominant kernel's ms per launch and the serialized pass's
+# tail stage (ms per launch, launches) per run
 set -u
 n=$1; cfgs=$2; vars=$3; shift 3
 mkdir -p gpurun_out
@@ -12,7 +13,9 @@ for i in $(seq 1 $n); do
       python3 -c "
 import json
 l=json.loads([x for x in open('$log') if x.startswith('{')][0]); r=l['roofline'] or {}
-print('$cfg $v $i', l['value'], l['ms_per_step'], 'splat/launch', r.get('splat_ms_per_launch'), 'dominant', r.get('avg_launch_ms'))"
+t=(r.get('stages') or {}).get('tail') or {}
+print('$cfg $v $i', l['value'], l['ms_per_step'], 'splat/launch', r.get('splat_ms_per_launch'), 'dominant', r.get('avg_launch_ms'),
+      'tail', t.get('avg_launch_ms'), t.get('launches'))"
     done
   done
 done
