@@ -1375,8 +1375,7 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     p.persistent = c->depth > 20;
     if (const char *e = std::getenv("NH_PERSISTENT")) p.persistent = e[0] == '1';
     // the persistent kernels generate pinhole camera rays only (camera_ray<false>: the lens arithmetic spilled their
-    // refill code): thin-lens scenes trace with one ray per lane
-    if (c->S.dof) p.persistent = false;
+    // refill code): for a thin-lens scene wf_camera_rays writes bounce 0's rays first (WfLaunch::cam_rays)
     // the persistent kernels walk the 4-wide collapse of the tree (half the dependent node fetches)
     // unless the reference's own visit order was asked for
     p.wide = p.persistent && j.ordered && c->tv.wnodes != nullptr;
@@ -1549,6 +1548,7 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
     unsigned *slot[2] = {p.wf.counts, p.wf.counts + kCountSlot};
     L.in_q = in;
     L.first = it == 0;
+    L.cam_rays = it == 0 && p.persistent && c->S.dof ? 1 : 0;
     L.cnt_in = slot[in];
     L.cnt_out = slot[in ^ 1];
     while ((size_t)(it + 1) * 4 > p.events.size()) {
@@ -1591,6 +1591,10 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
         if (it == 0) p.it = 1;
         else p.state = WfPool::COUNTS;
         return NH_OK;
+    }
+    if (it == 0 && L.cam_rays) {
+        nh::launch_wf_camera_rays(c->d_scene, L, bound, p.stream);
+        HIP_TRY(c, hipGetLastError());
     }
     if (p.trace2) {  // both queries in one launch: its time counts as the extend stage's, the shadow stage's is 0
         nh::launch_wf_trace2(c->d_scene, c->tv, L, ordered, stats, it == 0 ? bound : 2 * bound, p.stream);

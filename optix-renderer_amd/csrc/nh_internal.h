@@ -164,6 +164,9 @@ struct WfLaunch {
     float2 *jit;            // NH_SPLAT_JITTER=stored only: the jitter per record, written at the first vertex
     int in_q;               // buffer (and count slot) read by this bounce
     int first;              // bounce 0: paths come from the camera, not from a buffer
+    int cam_rays;           // bounce 0 of a thin-lens scene on the persistent kernels: the camera rays were written raw
+                            // into buf[in_q].ray_o / ray_d by wf_camera_rays (the persistent refill builds pinhole
+                            // rays only)
     unsigned *cnt_in;       // count slot of this bounce's input queues
     unsigned *cnt_out;      // count slot the shade kernel appends into
     int seg_cap;            // entries per shard segment of every queue / buffer
@@ -188,6 +191,9 @@ void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLau
 // closest-hit + any-hit queries of a bounce in one persistent launch (4-wide tree); bound = both queues' sum
 void launch_wf_trace2(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                       int bound, hipStream_t st);
+// bounce 0 of a thin-lens scene on the persistent kernels: every camera ray (camera_ray with its lens sample) into
+// buf[in_q].ray_o / ray_d, (origin, mint) / (direction, maxt), for the persistent refill to read (WfLaunch::cam_rays)
+void launch_wf_camera_rays(const nhd::DScene *S, const WfLaunch &L, int bound, hipStream_t st);
 void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool sort, int bound,
                      hipStream_t st);
 // fused shade + any-hit + closest-hit bounce for LDS-staged BVHs; sort = material-sorted output queue

@@ -411,8 +411,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
                 if (ANY) {
                     ro = L.st.sh_o[slot];
                     rd = L.st.sh_d[slot];
+                } else if (L.first && L.cam_rays) {  // thin-lens camera rays, precomputed (wf_camera_rays)
+                    ro = B.ray_o[slot];
+                    rd = B.ray_d[slot];
                 } else {
-                    load_ray<false>(S, L, B, q, slot, ro, rd);  // (never a DOF scene, nh_api.hip)
+                    load_ray<false>(S, L, B, q, slot, ro, rd);  // (pinhole camera rays only)
                 }
                 // a zero BSDF direction (maxt = -inf) misses every primitive without a traversal
                 if (STATS && (ANY || rd.w >= ro.w)) ++queries;
@@ -500,7 +503,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
                     if (STATS) ++q_s;
                 } else {
                     slot = queue_slot(qe.pre, L.seg_cap, q);
-                    load_ray<false>(S, L, B, q, slot, ro, rd);  // (never a DOF scene, nh_api.hip)
+                    if (L.first && L.cam_rays) {  // thin-lens camera rays, precomputed (wf_camera_rays)
+                        ro = B.ray_o[slot];
+                        rd = B.ray_d[slot];
+                    } else {
+                        load_ray<false>(S, L, B, q, slot, ro, rd);  // (pinhole camera rays only)
+                    }
                     // a zero BSDF direction (maxt = -inf) misses every primitive without a traversal
                     if (STATS && rd.w >= ro.w) ++q_e;
                 }
@@ -1358,6 +1366,22 @@ __global__ __launch_bounds__(256) void wf_counts_kernel(const unsigned *src, uns
 }
 #endif
 #if !defined(NH_WF_PART) || NH_WF_PART == 1  // a non-template kernel: defined in one part only
+// bounce 0's camera rays of a thin-lens scene, for the persistent traversal kernels, whose refill code builds pinhole
+// rays only (camera_ray<false>: the lens arithmetic spilled it): the same camera_sample as every other kernel, stored
+// raw -- (origin, mint), (direction, maxt) -- in the input buffer's ray words, which bounce 0 does not use otherwise
+__global__ __launch_bounds__(256) void wf_camera_rays(const DScene *__restrict__ Sp, WfLaunch L) {
+    const DScene &S = *Sp;
+    const QView qv = queue_view(L.cnt_in);
+    const WfBuf &B = L.st.buf[L.in_q];
+    for (int q = blockIdx.x * 256 + threadIdx.x; q < qv.n; q += gridDim.x * 256) {
+        const int s = queue_slot(qv.pre, L.seg_cap, q);
+        float4 ro, rd;
+        load_ray<true>(S, L, B, q, s, ro, rd);  // L.first: the camera ray of path q
+        B.ray_o[s] = ro;
+        B.ray_d[s] = rd;
+    }
+}
+
 __global__ __launch_bounds__(256) void wf_pack_rr(WfLaunch L, WfBuf dst, unsigned *dst_counts) {
     const QView qv = queue_view(L.cnt_in);
     const int q = blockIdx.x * 256 + threadIdx.x;
@@ -1597,12 +1621,12 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
                        bool specular, bool lean, hipStream_t st) {
     const char *e = std::getenv("NH_TAIL_WG");  // threads per tail workgroup: 64 (default) or 256
     const int tb = e && std::atoi(e) == 256 ? 256 : 64;
-    // register budget, NH_TAIL_RR_WAVES=1|4: by default 1 wave/SIMD for scenes with mirror / dielectric BSDFs (their
-    // long chains: shorter tails on C1 and C4, profiles/round4_session4_ab.txt) and 4 otherwise (a short tail that
-    // leaves the next chunk's bounce kernels their occupancy: C2 +0.5 %, profiles/round4_session11_12_c2_ab.txt)
-    // (NH_TAIL_RR_WAVES=2: 256 VGPRs, an A/B point between the two). lean (NH_TAIL_LEAN=0 off): the FULL = false body
+    // register budget, NH_TAIL_RR_WAVES=1|2|4: by default 1 wave/SIMD for scenes with mirror / dielectric BSDFs (their
+    // long chains: shorter tails on C1 and C4, profiles/round4_session4_ab.txt) and 2 otherwise: spill-free (the
+    // 4-wave budget spilled 448 B per lane inside the bounce loop), the tail 4-6 % shorter, the C2 step level with 4
+    // waves (profiles/round6_ab_tail_waves.txt). lean (NH_TAIL_LEAN=0 off): the FULL = false body
     const char *w = std::getenv("NH_TAIL_RR_WAVES");
-    const int waves = w ? (std::atoi(w) == 1 ? 1 : std::atoi(w) == 2 ? 2 : 4) : specular ? 1 : 4;
+    const int waves = w ? (std::atoi(w) == 1 ? 1 : std::atoi(w) == 2 ? 2 : 4) : specular ? 1 : 2;
     const char *ln = std::getenv("NH_TAIL_LEAN");
     if (ln && ln[0] == '0') lean = false;
     const char *cp = std::getenv("NH_TAIL_COOP");  // lanes per path once <= 4 remain in a wave: 16 (default) or 1
@@ -1625,6 +1649,13 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
 #undef NH_TR
 }
 
+#endif
+
+#if NH_WF_HAS_PART(1)
+void launch_wf_camera_rays(const DScene *S, const WfLaunch &L, int bound, hipStream_t st) {
+    const int blocks = std::min(std::max(1, (bound + 255) / 256), kTraceBlocksMax);
+    hipLaunchKernelGGL(wf_camera_rays, dim3(blocks), dim3(256), 0, st, S, L);
+}
 #endif
 
 #if NH_WF_HAS_PART(1)

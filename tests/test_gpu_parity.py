@@ -374,15 +374,20 @@ def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
             assert ref.stats()[k] == ctx.stats()[k], (xml, k)
 
 
-@pytest.mark.parametrize("tail,coop,waves", [("4096", "16", "4"), ("4096", "1", "4"), ("200000", "16", "1"),
-                                             ("64", "16", "4")])
-def test_cooperative_tail_matches_oracle(gpu, tmp_path, monkeypatch, tail, coop, waves):
+@pytest.mark.parametrize("variant,tail,coop,waves", [("c1", "4096", "16", "4"), ("c1", "4096", "1", "4"),
+                                                     ("c1", "200000", "16", "1"), ("c1", "64", "16", "4"),
+                                                     ("c1", "4096", "16", "2"),
+                                                     # C2 (diffuse only): the lean tail body (FULL = false)
+                                                     ("c2", "4096", "16", "2"), ("c2", "4096", "1", "4"),
+                                                     ("c2", "200000", "16", "2")])
+def test_cooperative_tail_matches_oracle(gpu, tmp_path, monkeypatch, variant, tail, coop, waves):
     """The RR-ahead tail kernel's cooperative finish (NH_TAIL_COOP=16: once a tail wave carries <= 4 paths, each is
     carried by a 16-lane group that tests a leaf's primitives in one parallel step and reduces to the smallest t,
     ties to the later primitive) on the mirror + dielectric Cornell box (long specular chains), forced early by a
     small tail threshold, and the per-lane tail (NH_TAIL_COOP=1), at both register budgets: framebuffer and traversal
-    counters equal the megakernel's, the framebuffer equals the oracle's."""
-    xml = scenegen.cbox_xml(str(tmp_path), "c1")
+    counters equal the megakernel's, the framebuffer equals the oracle's. c2: the diffuse-only box, whose tail runs
+    the lean body (no discrete-BSDF skip, texture lookup or isolated-sphere test compiled in) at 2 or 4 waves/SIMD."""
+    xml = scenegen.cbox_xml(str(tmp_path), variant)
     s = nh.Scene(xml)
     s.set_resolution(64, 48)
     b = nh.Bvh(s)

@@ -109,6 +109,29 @@ def test_dof_cbox_full_image_wavefront(gpu, tmp_path):
     np.testing.assert_array_equal(g, r)
 
 
+@pytest.mark.parametrize("knobs", [{"NH_PERSISTENT": "1", "NH_LDS_SCENE": "0"},
+                                   {"NH_PERSISTENT": "1", "NH_LDS_SCENE": "0", "NH_TRACE2": "0"},
+                                   {"NH_PERSISTENT": "1", "NH_LDS_SCENE": "0", "NH_WIDE": "0"}])
+def test_dof_persistent_camera_rays(gpu, tmp_path, monkeypatch, knobs):
+    """Thin-lens scenes on the persistent traversal kernels: bounce 0's camera rays (with their lens samples) are
+    written by wf_camera_rays and read by the persistent refill (4-wide both-queries launch, 4-wide split launches,
+    binary tree). A thin-lens Cornell box forced off the LDS-staged path, 96x64, 4 spp: GPU = oracle bit for bit."""
+    xml = scenegen.cbox_xml(str(tmp_path), "c1")
+    text = open(xml).read().replace('<camera type="perspective">',
+                                    '<camera type="perspective"><float name="lensRadius" value="0.1"/>'
+                                    '<float name="focalDistance" value="4.5"/>', 1)
+    path = os.path.join(os.path.dirname(xml), "cbox_c1_dof_pt.xml")
+    with open(path, "w") as f:
+        f.write(text)
+    s = nh.Scene(path)
+    s.set_resolution(96, 64)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    g = gpu_render(s, 0, 4, None, nh.MODE_WAVEFRONT, seed=6)
+    r = no.OracleScene(s).render(0, 4, seed=6)
+    np.testing.assert_array_equal(g, r)
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_reference_envmap_sphere_crop(gpu, proj_dir, mode):
     """envmap_sphere.xml (800x800, path_mis, the shipped wooden_motel.png envmap rotated by eulerAngles 180,180,0
