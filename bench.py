@@ -274,12 +274,13 @@ def roofline(args, calib, st, W, H, R):
             r["measured_source"] = f"profiles/pmc_traffic.json[{args.config}_{W}x{H}_r{R}_{args.traversal}_{args.mode}/{k}]"
         report[k] = r
     dom = max(report, key=lambda k: report[k]["ms"])
-    wide = node_b == 128  # deep trees: the persistent 4-wide traversal kernel runs both queries
+    wide = node_b in (128, 256)  # deep trees: the persistent 4-wide (8-wide: NH_WIDE8=1) traversal kernels
+    ww = node_b // 32
     rr = os.environ.get("NH_RR_AHEAD", "1") != "0"
     kernel = {"shade": "wf_shade",
-              "trace": "wf_trace_pt2 (persistent 4-wide closest hit + any hit, one launch per bounce)",
-              "extend": "wf_trace_pt (persistent 4-wide closest hit)" if wide else "wf_extend",
-              "shadow": "wf_trace_pt (persistent 4-wide any hit)" if wide else "wf_shadow",
+              "trace": f"wf_trace_pt2 (persistent {ww}-wide closest hit + any hit, one launch per bounce)",
+              "extend": f"wf_trace_pt (persistent {ww}-wide closest hit)" if wide else "wf_extend",
+              "shadow": f"wf_trace_pt (persistent {ww}-wide any hit)" if wide else "wf_shadow",
               "tail": "wf_tail_rr" if fused and rr else "wf_tail", "path": "nh_path_kernel",
               "bounce": ("wf_bounce_rr (shade body + any-hit + closest-hit + the next vertex's roulette, fused)" if rr
                          else "wf_bounce (shade + any-hit + closest-hit, fused)")}[dom]
@@ -644,9 +645,9 @@ def traversal_1m(nh, args, local):
     traffic, source = pmc_traffic(key1m)
     rec1m = pmc_record(key1m)
     out = {"workload": r["desc"], "msamples_s": round(r["samples"] / r["elapsed"] / 1e6, 3),
-           "kernel": ({"trace": "wf_trace_pt2 (persistent 4-wide closest-hit + any-hit traversal, one launch per bounce)",
-                       "extend": "wf_trace_pt (persistent 4-wide closest-hit traversal)"}[stage]
-                      if roof["node_bytes"] == 128 else "wf_extend"),
+           "kernel": ({"trace": "wf_trace_pt2 (persistent %d-wide closest-hit + any-hit traversal, one launch per bounce)",
+                       "extend": "wf_trace_pt (persistent %d-wide closest-hit traversal)"}[stage] % (roof["node_bytes"] // 32)
+                      if roof["node_bytes"] in (128, 256) else "wf_extend"),
            "avg_launch_ms": e["avg_launch_ms"], "algorithmic_bytes_per_launch": e["global_bytes_per_launch"],
            "achieved_gbs": e["global_gbs"], "frac": round(e["global_gbs"] / HBM_PEAK_GBS, 4), "target_frac": 0.40,
            "nodes_per_query": e.get("nodes_per_query"), "prims_per_query": e.get("prims_per_query"),

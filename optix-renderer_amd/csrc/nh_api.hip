@@ -134,7 +134,8 @@ struct nh_ctx {
     std::vector<void *> scene_bufs, bvh_bufs;
     bool has_scene = false, has_bvh = false;
     int depth = 0;
-    int depth_wide = 0;  // stack bound of the 4-wide traversal
+    int depth_wide = 0;  // stack bound of the wide traversal
+    int wide_w = 4;      // children per wide node of tv.wnodes: 4, or 8 (NH_WIDE8=1)
     int n_node_f4 = 0, n_leaves = 0, n_prim_f4 = 0;  // GPU BVH sizes (float4 / int2 entries)
     std::vector<uint32_t> bvh_indices, shape_offset;
     std::vector<int> shape_bsdf_type;  // BSDF type of each shape (material key of the sorted queues)
@@ -841,12 +842,13 @@ static int mark_isolated_spheres(std::vector<float4> &prims, const std::vector<f
     return marked;
 }
 
-// 4-wide collapse of the GPU binary tree (nh_traverse.h Tracer4): every wide node takes the two
-// children of a binary node and, while it has fewer than 4, replaces its largest-area inner child
-// by that child's two children in place (left-first DFS order of the slots is kept). Wide nodes
-// are numbered depth first, the first child next to its parent. Boxes are the binary tree's own.
+// W-wide collapse (W = 4 or 8) of the GPU binary tree (nh_traverse.h Tracer4 / Tracer8): every wide node takes
+// the two children of a binary node and, while it has fewer than W, replaces its largest-area inner child by that
+// child's two children in place (left-first DFS order of the slots is kept). Wide nodes are numbered depth first,
+// the first child next to its parent. Boxes are the binary tree's own. An 8-wide node is two 4-wide lines
+// (children 0-3, 4-7), each in the 4-wide layout.
 static std::vector<float4> collapse_wide(const std::vector<float4> &nodes, const std::vector<int2> &leaves,
-                                         int &depth_out) {
+                                         int &depth_out, int W = 4) {
     struct Child {
         float mn[3], mx[3];
         int ref;  // binary: >= 0 inner node, < 0 leaf ~index
@@ -868,12 +870,13 @@ static std::vector<float4> collapse_wide(const std::vector<float4> &nodes, const
     std::vector<float4> wide;
     depth_out = 0;
     if (nodes.empty()) return wide;
+    const int lines = W / 4, nf4 = lines * nhd::kWideF4;
     std::function<int(int, int)> make = [&](int g, int depth) -> int {
         depth_out = std::max(depth_out, depth);
-        const int idx = (int)(wide.size() / nhd::kWideF4);
-        wide.resize(wide.size() + nhd::kWideF4);
+        const int idx = (int)(wide.size() / nf4);
+        wide.resize(wide.size() + nf4);
         std::vector<Child> ch{child(g, 0), child(g, 1)};
-        while (ch.size() < 4) {
+        while ((int)ch.size() < W) {
             int best = -1;
             float best_a = -1.f;
             for (int i = 0; i < (int)ch.size(); ++i)
@@ -883,10 +886,12 @@ static std::vector<float4> collapse_wide(const std::vector<float4> &nodes, const
             ch[best] = child(gi, 1);
             ch.insert(ch.begin() + best, child(gi, 0));
         }
-        int refs[4] = {nhd::kWideEmpty, nhd::kWideEmpty, nhd::kWideEmpty, nhd::kWideEmpty};
-        float box[6][4];
-        for (int j = 0; j < 4; ++j)
+        int refs[8];
+        float box[6][8];
+        for (int j = 0; j < 8; ++j) {
+            refs[j] = nhd::kWideEmpty;
             for (int a = 0; a < 3; ++a) { box[a][j] = 0.f; box[3 + a][j] = 0.f; }
+        }
         for (int j = 0; j < (int)ch.size(); ++j) {
             for (int a = 0; a < 3; ++a) { box[a][j] = ch[j].mn[a]; box[3 + a][j] = ch[j].mx[a]; }
             if (ch[j].ref >= 0) {
@@ -896,10 +901,13 @@ static std::vector<float4> collapse_wide(const std::vector<float4> &nodes, const
                 refs[j] = lf.y > 0 ? ~lf.x : nhd::kWideEmpty;  // an empty leaf holds nothing to hit
             }
         }
-        float4 *n = &wide[(size_t)idx * nhd::kWideF4];
-        for (int a = 0; a < 6; ++a) n[a] = make_float4(box[a][0], box[a][1], box[a][2], box[a][3]);
-        std::memcpy(&n[6], refs, 16);
-        n[7] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int h = 0; h < lines; ++h) {
+            float4 *n = &wide[(size_t)idx * nf4 + (size_t)h * nhd::kWideF4];
+            for (int a = 0; a < 6; ++a)
+                n[a] = make_float4(box[a][4 * h], box[a][4 * h + 1], box[a][4 * h + 2], box[a][4 * h + 3]);
+            std::memcpy(&n[6], refs + 4 * h, 16);
+            n[7] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         return idx;
     };
     make(0, 1);
@@ -910,8 +918,10 @@ static std::vector<float4> collapse_wide(const std::vector<float4> &nodes, const
 // connected top of the tree grown from the root by the largest child-box surface area (a ray's chance
 // of entering a box grows with its area). The other nodes keep their depth-first order. Renumbering
 // moves no box and changes no visit order: every answer is unchanged. Returns the top's size.
-static int number_top_first(std::vector<float4> &wide, const float root_min[3], const float root_max[3], int K) {
-    const int n = (int)(wide.size() / nhd::kWideF4);
+static int number_top_first(std::vector<float4> &wide, const float root_min[3], const float root_max[3], int K,
+                            int W = 4) {
+    const int lines = W / 4, nf4 = lines * nhd::kWideF4;
+    const int n = (int)(wide.size() / nf4);
     if (n == 0 || K <= 0) return 0;
     auto area = [](const float *mn, const float *mx) {
         const float x = mx[0] - mn[0], y = mx[1] - mn[1], z = mx[2] - mn[2];
@@ -926,14 +936,16 @@ static int number_top_first(std::vector<float4> &wide, const float root_min[3], 
         heap.pop_back();
         order.push_back(g);
         in_top[g] = 1;
-        const float *f = reinterpret_cast<const float *>(&wide[(size_t)g * nhd::kWideF4]);
-        int refs[4];
-        std::memcpy(refs, f + 24, 16);
-        for (int j = 0; j < 4; ++j) {
-            if (refs[j] < 0) continue;  // a leaf or an empty slot
-            const float mn[3] = {f[j], f[4 + j], f[8 + j]}, mx[3] = {f[12 + j], f[16 + j], f[20 + j]};
-            heap.push_back({area(mn, mx), refs[j]});
-            std::push_heap(heap.begin(), heap.end());
+        for (int h = 0; h < lines; ++h) {
+            const float *f = reinterpret_cast<const float *>(&wide[(size_t)g * nf4 + (size_t)h * nhd::kWideF4]);
+            int refs[4];
+            std::memcpy(refs, f + 24, 16);
+            for (int j = 0; j < 4; ++j) {
+                if (refs[j] < 0) continue;  // a leaf or an empty slot
+                const float mn[3] = {f[j], f[4 + j], f[8 + j]}, mx[3] = {f[12 + j], f[16 + j], f[20 + j]};
+                heap.push_back({area(mn, mx), refs[j]});
+                std::push_heap(heap.begin(), heap.end());
+            }
         }
     }
     std::vector<int> perm(n);  // old -> new
@@ -943,13 +955,15 @@ static int number_top_first(std::vector<float4> &wide, const float root_min[3], 
         if (!in_top[g]) perm[g] = next++;
     std::vector<float4> out(wide.size());
     for (int g = 0; g < n; ++g) {
-        float4 *dst = &out[(size_t)perm[g] * nhd::kWideF4];
-        std::memcpy(dst, &wide[(size_t)g * nhd::kWideF4], nhd::kWideF4 * sizeof(float4));
-        int refs[4];
-        std::memcpy(refs, &dst[6], 16);
-        for (int j = 0; j < 4; ++j)
-            if (refs[j] >= 0) refs[j] = perm[refs[j]];
-        std::memcpy(&dst[6], refs, 16);
+        float4 *dst = &out[(size_t)perm[g] * nf4];
+        std::memcpy(dst, &wide[(size_t)g * nf4], nf4 * sizeof(float4));
+        for (int h = 0; h < lines; ++h) {
+            int refs[4];
+            std::memcpy(refs, &dst[h * nhd::kWideF4 + 6], 16);
+            for (int j = 0; j < 4; ++j)
+                if (refs[j] >= 0) refs[j] = perm[refs[j]];
+            std::memcpy(&dst[h * nhd::kWideF4 + 6], refs, 16);
+        }
     }
     wide.swap(out);
     return (int)order.size();
@@ -1070,12 +1084,15 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     // children of one root-to-leaf path; the reference keeps 64, bvh.cpp:403)
     if (tree_depth + 2 > (uint32_t)kMaxStack)
         return fail(c, "BVH deeper than " + std::to_string(kMaxStack - 2) + " levels is not supported"), NH_ERR_UNSUPPORTED;
+    // the wide tree of the persistent kernels: 4-wide, or 8-wide with NH_WIDE8=1 (A/B)
+    c->wide_w = std::getenv("NH_WIDE8") && std::getenv("NH_WIDE8")[0] == '1' ? 8 : 4;
     int depth4 = 0;
-    std::vector<float4> wide = collapse_wide(nodes, leaves, depth4);
-    // the top of the tree the persistent kernels stage in LDS (NH_TREE_TOP: its size, 0 = none)
-    int top_k = nh::tree_top_nodes();
+    std::vector<float4> wide = collapse_wide(nodes, leaves, depth4, c->wide_w);
+    // the top of the tree the persistent kernels stage in LDS (NH_TREE_TOP: its size, 0 = none): the same bytes for
+    // both widths
+    int top_k = nh::tree_top_nodes() * 4 / c->wide_w;
     if (const char *e = std::getenv("NH_TREE_TOP")) top_k = std::min(std::max(0, std::atoi(e)), top_k);
-    c->tv.n_top = S.root_kind == 1 ? number_top_first(wide, S.root_min, S.root_max, top_k) : 0;
+    c->tv.n_top = S.root_kind == 1 ? number_top_first(wide, S.root_min, S.root_max, top_k, c->wide_w) : 0;
     int rc;
     c->n_node_f4 = (int)nodes.size();
     c->n_leaves = (int)leaves.size();
@@ -1088,8 +1105,8 @@ int nh_upload_bvh(nh_ctx *c, const nh_bvh_desc *b) {
     if ((rc = upload(c, c->bvh_bufs, prims.data(), prims.size(), &c->tv.prims))) return rc;
     c->tv.wnodes = nullptr;
     if (!wide.empty() && (rc = upload(c, c->bvh_bufs, wide.data(), wide.size(), &c->tv.wnodes))) return rc;
-    // deferred entries: at most 3 per wide level (+1 slack)
-    c->depth_wide = 3 * depth4 + 1;
+    // deferred entries: at most W - 1 per wide level (+1 slack)
+    c->depth_wide = (c->wide_w - 1) * depth4 + 1;
     S.nodes = c->tv.nodes;
     S.prims = c->tv.prims;
     c->bvh_indices.assign(b->indices, b->indices + b->n_indices);
@@ -1127,7 +1144,7 @@ int nh_trace_rays(nh_ctx *c, const nh_ray_soa *r, int32_t n, int32_t any_hit, in
         HIP_TRY(c, hipMalloc(&p, nn * (size_t)c->depth_wide * sizeof(int2)));
         tmp.push_back(p);
         nh::launch_trace_wide(c->d_scene, c->tv, rb, hb, n, any_hit != 0, true, false, (int2 *)p, c->depth_wide,
-                              c->counters, c->stream);
+                              c->counters, c->stream, c->wide_w);
     } else {
         nh::launch_trace(c->d_scene, c->tv, rb, hb, n, any_hit != 0, traversal != NH_TRAVERSAL_REFERENCE, false,
                          c->depth, c->counters, c->stream);
@@ -1410,7 +1427,7 @@ static int pool_start(nh_ctx *c, WfPool &p, const WfJob &job) {
     if (const char *e = std::getenv("NH_SORT_SHADE")) p.shade_sorted = !p.fused && e[0] == '1';
     if (const char *e = std::getenv("NH_SORT")) p.sorted = p.fused && e[0] == '1';
     c->stats.fused_bounce = p.fused ? 1 : 0;
-    c->stats.node_bytes = p.wide ? 16 * nhd::kWideF4 : 64;
+    c->stats.node_bytes = p.wide ? 16 * nhd::kWideF4 * (c->wide_w / 4) : 64;
     c->stats.lds_scene = small && !p.persistent && c->depth <= 16 ? 1 : 0;  // the SMALL instantiations (DEPTH 16)
     L.trav_spill = p.spill;
     L.spill_depth = p.spill_words;
@@ -1597,20 +1614,20 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
         HIP_TRY(c, hipGetLastError());
     }
     if (p.trace2) {  // both queries in one launch: its time counts as the extend stage's, the shadow stage's is 0
-        nh::launch_wf_trace2(c->d_scene, c->tv, L, ordered, stats, it == 0 ? bound : 2 * bound, p.stream);
+        nh::launch_wf_trace2(c->d_scene, c->tv, L, ordered, stats, c->wide_w, it == 0 ? bound : 2 * bound, p.stream);
         HIP_TRY(c, hipEventRecord(ev[1], p.stream));
         HIP_TRY(c, hipEventRecord(ev[2], p.stream));
     } else {
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, p.persistent, p.wide, bound, c->depth,
-                            p.stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, false, p.persistent, p.wide ? c->wide_w : 0, bound,
+                            c->depth, p.stream);
         HIP_TRY(c, hipEventRecord(ev[1], p.stream));
         // bounce 0 has no shadow rays (the launch still runs: the kernels read the count on the device)
-        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, p.persistent, p.wide, it == 0 ? 0 : bound,
-                            c->depth, p.stream);
+        nh::launch_wf_trace(c->d_scene, c->tv, L, ordered, stats, true, p.persistent, p.wide ? c->wide_w : 0,
+                            it == 0 ? 0 : bound, c->depth, p.stream);
         HIP_TRY(c, hipEventRecord(ev[2], p.stream));
     }
     if (it > 0 && (int64_t)bound <= p.tail_at) {
-        nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, p.wide, bound, c->depth, p.stream);
+        nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, p.wide ? c->wide_w : 0, bound, c->depth, p.stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], p.stream));
         p.tail = true;

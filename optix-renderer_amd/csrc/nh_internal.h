@@ -106,7 +106,7 @@ void launch_trace(const nhd::DScene *S, const nhd::Traversal &tv, const RayBatch
                   bool any, bool ordered, bool stats, int depth, unsigned long long *ctr, hipStream_t st);
 void launch_trace_wide(const nhd::DScene *S, const nhd::Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n,
                        bool any, bool ordered, bool stats, int2 *spill, int spill_depth, unsigned long long *ctr,
-                       hipStream_t st);
+                       hipStream_t st, int wide = 4);
 void launch_path(const nhd::DScene *S, const nhd::Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
                  int depth, hipStream_t st);
 void launch_splat(const SplatLaunch &P, hipStream_t st);
@@ -186,11 +186,11 @@ constexpr size_t kSmallSceneBytes = 16384;
 constexpr int kSmallFramesMaxPrims = 256;  // frames staged (48 B per record) only for scenes this small
 namespace nh {
 void launch_wf_trace(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                     bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st);
+                     bool shadow, bool persistent, int wide, int bound, int depth, hipStream_t st);
 // sort: entries shaded in the order of their hit's BSDF type within each workgroup (material-sorted shading)
 // closest-hit + any-hit queries of a bounce in one persistent launch (4-wide tree); bound = both queues' sum
 void launch_wf_trace2(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                      int bound, hipStream_t st);
+                      int wide, int bound, hipStream_t st);
 // bounce 0 of a thin-lens scene on the persistent kernels: every camera ray (camera_ray with its lens sample) into
 // buf[in_q].ray_o / ray_d, (origin, mint) / (direction, maxt), for the persistent refill to read (WfLaunch::cam_rays)
 void launch_wf_camera_rays(const nhd::DScene *S, const WfLaunch &L, int bound, hipStream_t st);
@@ -206,7 +206,7 @@ void launch_wf_bounce_rr(const nhd::DScene *S, const nhd::Traversal &tv, const W
 void launch_wf_tail_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
                        bool specular, bool lean, hipStream_t st);
 void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                    bool wide, int bound, int depth, hipStream_t st);
+                    int wide, int bound, int depth, hipStream_t st);
 // copies the live RR-ahead paths of L's input queue (at most bound) densely into dst, count into dst_counts[0]
 void launch_wf_pack_rr(const WfLaunch &L, const WfBuf &dst, unsigned *dst_counts, int bound, hipStream_t st);
 // n_copy count words src -> host_dst (pinned, device-visible), then n_zero words of zero cleared (wf_counts_kernel)

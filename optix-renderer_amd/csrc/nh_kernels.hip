@@ -7,6 +7,7 @@
 //                     path_mats.cpp:16-78), writing (radiance, jitter) sample records
 //   (the ImageBlock stage -- splat and merge of the sample records -- is in nh_splat.hip)
 #include <cstdlib>
+#include <type_traits>
 
 #include "nh_internal.h"
 
@@ -218,9 +219,9 @@ __global__ __launch_bounds__(BLOCK) void nh_trace_kernel(const DScene *__restric
     if (STATS) flush_stats(st, i < n ? 1u : 0u, stat_shard(counters));
 }
 
-// The same entry point over the 4-wide collapse (nh_traverse.h Tracer4), run to completion per
-// lane: LDS window of 16 (ref, distance) entries, deeper entries in the lane's `spill` area.
-template <bool ORDERED, bool ANY, bool STATS>
+// The same entry point over the 4-wide (or 8-wide, W = 8) collapse (nh_traverse.h Tracer4 / Tracer8), run to
+// completion per lane: LDS window of 16 (ref, distance) entries, deeper entries in the lane's `spill` area.
+template <bool ORDERED, bool ANY, bool STATS, int W = 4>
 __global__ __launch_bounds__(64) void nh_trace_wide_kernel(const DScene *__restrict__ Sp, Traversal tv, RayBatch rb,
                                                            HitBatch hb, int n, int2 *spill, int spill_depth,
                                                            unsigned long long *counters) {
@@ -231,7 +232,8 @@ __global__ __launch_bounds__(64) void nh_trace_wide_kernel(const DScene *__restr
     TravStats st{0, 0, 0};
     if (i < n) {
         RingStack2<16> stk{s_ref + threadIdx.x, s_near + threadIdx.x, 64, spill, (unsigned)n, (unsigned)i};
-        Tracer4<ORDERED, ANY, STATS, RingStack2<16>> tr;
+        typename std::conditional<W == 8, Tracer8<ORDERED, ANY, STATS, RingStack2<16>>,
+                                  Tracer4<ORDERED, ANY, STATS, RingStack2<16>>>::type tr;
         tr.begin(S, tv, f3(rb.ox[i], rb.oy[i], rb.oz[i]), f3(rb.dx[i], rb.dy[i], rb.dz[i]), rb.mint[i], rb.maxt[i], st);
         while (!tr.done) tr.step(tv, stk, st);
         hb.hit[i] = tr.found ? 1 : 0;
@@ -475,11 +477,16 @@ void launch_trace(const DScene *S, const Traversal &tv, const RayBatch &rb, cons
 
 void launch_trace_wide(const DScene *S, const Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n, bool any,
                        bool ordered, bool stats, int2 *spill, int spill_depth, unsigned long long *ctr,
-                       hipStream_t st) {
+                       hipStream_t st, int wide) {
     if (n <= 0) return;
     dim3 grid((n + 63) / 64);
-#define NH_TW(O, A, T) \
-    hipLaunchKernelGGL((nh_trace_wide_kernel<O, A, T>), grid, dim3(64), 0, st, S, tv, rb, hb, n, spill, spill_depth, ctr)
+#define NH_TW(O, A, T)                                                                                              \
+    do {                                                                                                           \
+        if (wide == 8) hipLaunchKernelGGL((nh_trace_wide_kernel<O, A, T, 8>), grid, dim3(64), 0, st, S, tv, rb, hb, n, \
+                                          spill, spill_depth, ctr);                                                \
+        else hipLaunchKernelGGL((nh_trace_wide_kernel<O, A, T>), grid, dim3(64), 0, st, S, tv, rb, hb, n, spill,      \
+                                spill_depth, ctr);                                                                 \
+    } while (0)
     if (ordered) {
         if (any) { if (stats) NH_TW(true, true, true); else NH_TW(true, true, false); }
         else { if (stats) NH_TW(true, false, true); else NH_TW(true, false, false); }

@@ -771,11 +771,13 @@ struct RingStack2 {
         lds_ref[o] = ref;
         lds_near[o] = nr;
     }
-    // entries i0 .. i0+m-1 (m <= 3 < K) are about to be written with put(): spill the entries
-    // K below them that still occupy their ring slots
+    // entries i0 .. i0+m-1 (m <= M < K; M = 3 for 4-wide nodes, 7 for 8-wide ones) are about to be written with
+    // put(): spill the entries K below them that still occupy their ring slots
+    template <int M = 3>
     NHD void reserve(int i0, int m) {
+        static_assert(M < K, "a node's deferred children must fit the LDS window");
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
+        for (int j = 0; j < M; ++j) {
             const int i = i0 + j;
             if (j < m && i >= K) {
                 const int o = (i & (K - 1)) * stride;
@@ -981,6 +983,190 @@ struct Tracer4 {
 
     // record k (a, c; for a triangle its pair-test results t, u, v, ok) against the current maxt, then
     // advance k; true when an any-hit query is answered
+    NHD bool prim(const float4 &a, const float4 &c, float t, float u, float v, bool ok, TravStats &st) {
+        if (STATS) st.prims++;
+        bool hit;
+        if (prim_is_tri(c)) {
+            hit = ok & (t <= maxt);
+        } else {
+            u = v = 0.f;
+            hit = sphere_test(a, o, d, mint, maxt, t);
+        }
+        if (hit) {
+            if (is_any()) {
+                found = true;
+                done = true;
+                return true;
+            }
+            if (t < maxt || k > best.k) {
+                found = true;
+                maxt = t;
+                best.t = t;
+                best.u = u;
+                best.v = v;
+                best.k = k;
+            }
+        }
+        k = (__float_as_int(c.w) & kPrimLeafEnd) ? -1 : k + 1;
+        return false;
+    }
+
+    NHD void enter(int ref) {
+        if (ref >= 0) {
+            cur = ref;
+        } else {
+            k = ~ref;
+            cur = -1;
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// 8-wide traversal of the same tree (A/B against the 4-wide one, NH_WIDE8): nh_api.hip collapses the binary tree
+// to 8 children per node by the same rule (the largest-area inner child replaced by its two children, slots in
+// left-first DFS order, the descendants' own boxes -- no new boxes; the argument of Tracer4 carries over). A node
+// is two 128-B lines, each laid out as a 4-wide node: children 0-3 in float4 [0..7], 4-7 in [8..15]. Both lines
+// are loaded before either is tested, so one dependent fetch covers twice the children and a query takes about
+// two thirds of the 4-wide dependent steps. Same answers as Tracer4 (smallest t, ties to the largest leaf-order
+// position k); only the visit order of deferred children changes, which no answer depends on.
+constexpr int kWide8F4 = 2 * kWideF4;
+
+template <bool ORDERED, bool ANY, bool STATS, class Stack, bool RT = false>
+struct Tracer8 {
+    F3 o, d, r;
+    float mint, maxt;
+    int cur;  // wide node to visit next, or -1
+    int k;    // primitive under test, or -1
+    int sp;
+    bool found, done;
+    bool finite_r;
+    bool any_q;  // RT: this lane's query is an any-hit query
+    Hit best;
+
+    NHD bool is_any() const { return RT ? any_q : ANY; }
+
+    NHD void begin(const DScene &S, const Traversal &tv, F3 o_, F3 d_, float mint_, float maxt_, TravStats &st) {
+        o = o_;
+        d = d_;
+        mint = mint_;
+        maxt = maxt_;
+        if (mint == kEps) mint = e_max(mint, mint * e_max(fabsf(o.x), e_max(fabsf(o.y), fabsf(o.z))));  // bvh.cpp:407-410
+        best.k = -1;
+        best.t = INFINITY;
+        found = false;
+        done = true;
+        sp = 0;
+        cur = -1;
+        k = -1;
+        if (S.root_kind == 0 || maxt < mint) return;
+        r = f3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        finite_r = fabsf(r.x) < INFINITY && fabsf(r.y) < INFINITY && fabsf(r.z) < INFINITY;
+        float near_t;
+        if (STATS) st.boxes++;
+        if (!box_test(S.root_min[0], S.root_min[1], S.root_min[2], S.root_max[0], S.root_max[1], S.root_max[2], o, d,
+                      r, mint, maxt, near_t))
+            return;
+        done = false;
+        if (S.root_kind == 2) k = tv.leaves[0].x;
+        else cur = 0;
+    }
+
+    // the four children of one line: validity and entry distance
+    NHD void line_tests(const float4 *n, bool *v, float *nn, int *ref) const {
+        const float4 mnx = n[0], mny = n[1], mnz = n[2], mxx = n[3], mxy = n[4], mxz = n[5];
+        const int4 rf = *reinterpret_cast<const int4 *>(&n[6]);
+        ref[0] = rf.x; ref[1] = rf.y; ref[2] = rf.z; ref[3] = rf.w;
+        nn[0] = nn[1] = nn[2] = nn[3] = 0.f;
+        if (finite_r) {
+            v[0] = box_test_finite(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, r, mint, maxt, nn[0]) & (rf.x != kWideEmpty);
+            v[1] = box_test_finite(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, r, mint, maxt, nn[1]) & (rf.y != kWideEmpty);
+            v[2] = box_test_finite(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, r, mint, maxt, nn[2]) & (rf.z != kWideEmpty);
+            v[3] = box_test_finite(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, r, mint, maxt, nn[3]) & (rf.w != kWideEmpty);
+        } else {
+            v[0] = rf.x != kWideEmpty && box_test(mnx.x, mny.x, mnz.x, mxx.x, mxy.x, mxz.x, o, d, r, mint, maxt, nn[0]);
+            v[1] = rf.y != kWideEmpty && box_test(mnx.y, mny.y, mnz.y, mxx.y, mxy.y, mxz.y, o, d, r, mint, maxt, nn[1]);
+            v[2] = rf.z != kWideEmpty && box_test(mnx.z, mny.z, mnz.z, mxx.z, mxy.z, mxz.z, o, d, r, mint, maxt, nn[2]);
+            v[3] = rf.w != kWideEmpty && box_test(mnx.w, mny.w, mnz.w, mxx.w, mxy.w, mxz.w, o, d, r, mint, maxt, nn[3]);
+        }
+    }
+
+    NHD void step(const Traversal &tv, Stack &stk, TravStats &st) { step(tv, stk, st, nullptr, 0); }
+    // top / n_top: an LDS copy of the first n_top 8-wide nodes (0: every node from tv.wnodes)
+    NHD void step(const Traversal &tv, Stack &stk, TravStats &st, const float4 *top, int n_top) {
+        if (k < 0 && cur < 0) {  // deferred children: the visit-time test against the current maxt
+            while (sp > 0) {
+                int ref;
+                float nr;
+                stk.pop(--sp, ref, nr);
+                if (STATS) st.boxes++;
+                if (nr <= maxt) {
+                    enter(ref);
+                    break;
+                }
+            }
+            if (k < 0 && cur < 0) {
+                done = true;
+                return;
+            }
+        }
+        if (cur >= 0) {  // one 8-wide node: both lines fetched, then the eight child boxes tested
+            const float4 *n = cur < n_top ? top + kWide8F4 * cur : tv.wnodes + (size_t)kWide8F4 * cur;
+            bool v[8];
+            float nn[8];
+            int ref[8];
+            line_tests(n, v, nn, ref);
+            line_tests(n + kWideF4, v + 4, nn + 4, ref + 4);
+            if (STATS) {
+                st.nodes++;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) st.boxes += ref[i] != kWideEmpty;
+            }
+            // rank_i = number of valid children before child i (wide_first per pair: nearer first, slot order on ties)
+            int rk[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) rk[i] = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = i + 1; j < 8; ++j) {
+                    const int c = wide_first<ORDERED>(v[i], nn[i], v[j], nn[j]);
+                    rk[j] += c;
+                    rk[i] += 1 - c;
+                }
+            int nv = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) nv += (int)v[i];
+            if (nv == 0) {
+                cur = -1;
+            } else {
+                // the nearest child is entered; the child of rank r >= 1 is deferred at depth sp + nv-1-r
+                stk.template reserve<7>(sp, nv - 1);
+                const int top_i = sp + nv - 1;
+                int first = ref[7];
+#pragma unroll
+                for (int i = 7; i >= 0; --i) {
+                    if (v[i] && rk[i]) stk.put(top_i - rk[i], ref[i], nn[i]);
+                    if (v[i] && !rk[i]) first = ref[i];
+                }
+                sp = top_i;
+                enter(first);
+            }
+        }
+        if (k >= 0) {  // up to two primitives of the current leaf: records fetched together, tested as a pair
+            const float4 a0 = tv.prims[3 * k], b0 = tv.prims[3 * k + 1], c0 = tv.prims[3 * k + 2];
+            const float4 a1 = tv.prims[3 * k + 3], b1 = tv.prims[3 * k + 4], c1 = tv.prims[3 * k + 5];
+            f2 pt, pu, pv;
+            bool ok0, ok1;
+            tri_test_pair(a0, b0, c0, a1, b1, c1, o, d, mint, pt, pu, pv, ok0, ok1);
+            if (prim(a0, c0, pt.x, pu.x, pv.x, ok0, st)) return;
+            if (k >= 0) {
+                if (prim(a1, c1, pt.y, pu.y, pv.y, ok1, st)) return;
+            }
+        }
+        if (k < 0 && cur < 0 && sp == 0) done = true;
+    }
+
+    // record k against the current maxt, then advance k; true when an any-hit query is answered (as Tracer4::prim)
     NHD bool prim(const float4 &a, const float4 &c, float t, float u, float v, bool ok, TravStats &st) {
         if (STATS) st.prims++;
         bool hit;

@@ -302,20 +302,10 @@ constexpr int kRingEntries = NH_RING_ENTRIES;
 #endif
 constexpr int kTopNodes = NH_TOP_NODES;  // wide nodes per LDS copy of the top of the tree (kTopNodes * 128 B)
 //
-// WIDE: the 4-wide collapse of the tree (Tracer4), LDS window of 8 (ref, distance) pairs per lane.
-template <bool WIDE>
+// WIDE: 0 the binary tree (Tracer), 4 / 8 the 4- / 8-wide collapse of the tree (Tracer4 / Tracer8), LDS window of 8
+// (ref, distance) pairs per lane.
+template <int WIDE>
 struct PtStack {
-    using type = RingStack<kRingEntries>;
-    static __device__ __forceinline__ type make(uint32_t *lds, const WfLaunch &L) {
-        type s;
-        s.lds = lds + threadIdx.x;
-        s.stride = 128;
-        s.glob = L.trav_spill + ((size_t)blockIdx.x * 128 + threadIdx.x) * (size_t)L.spill_depth;
-        return s;
-    }
-};
-template <>
-struct PtStack<true> {
     using type = RingStack2<kRingEntries / 2>;
     static __device__ __forceinline__ type make(uint32_t *lds, const WfLaunch &L) {
         type s;
@@ -329,20 +319,36 @@ struct PtStack<true> {
         return s;
     }
 };
-template <bool WIDE, bool ORDERED, bool ANY, bool STATS, class Stk>
+template <>
+struct PtStack<0> {
+    using type = RingStack<kRingEntries>;
+    static __device__ __forceinline__ type make(uint32_t *lds, const WfLaunch &L) {
+        type s;
+        s.lds = lds + threadIdx.x;
+        s.stride = 128;
+        s.glob = L.trav_spill + ((size_t)blockIdx.x * 128 + threadIdx.x) * (size_t)L.spill_depth;
+        return s;
+    }
+};
+template <int WIDE, bool ORDERED, bool ANY, bool STATS, class Stk, bool RT = false>
 struct PtTracer { using type = Tracer<ORDERED, ANY, STATS, Stk>; };
-template <bool ORDERED, bool ANY, bool STATS, class Stk>
-struct PtTracer<true, ORDERED, ANY, STATS, Stk> { using type = Tracer4<ORDERED, ANY, STATS, Stk>; };
+template <bool ORDERED, bool ANY, bool STATS, class Stk, bool RT>
+struct PtTracer<4, ORDERED, ANY, STATS, Stk, RT> { using type = Tracer4<ORDERED, ANY, STATS, Stk, RT>; };
+template <bool ORDERED, bool ANY, bool STATS, class Stk, bool RT>
+struct PtTracer<8, ORDERED, ANY, STATS, Stk, RT> { using type = Tracer8<ORDERED, ANY, STATS, Stk, RT>; };
+// float4 per wide node, and the wide nodes of the LDS copy of the top of the tree (the same bytes for both widths)
+template <int WIDE>
+constexpr int wide_f4() { return WIDE == 8 ? kWide8F4 : kWideF4; }
 
 // one traversal run to completion by this lane (tail kernel): binary tree with the whole stack in
 // LDS (stk: DEPTH x 128 words), or the 4-wide tree with the persistent kernels' LDS window + spill
-template <bool WIDE, int DEPTH, bool ORDERED, bool ANY, bool STATS>
+template <int WIDE, int DEPTH, bool ORDERED, bool ANY, bool STATS>
 __device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S, const WfLaunch &L, F3 o, F3 d,
                                            float mint, float maxt, Hit &h, uint32_t *stk, TravStats &st) {
-    if constexpr (WIDE) {
-        using Stk = typename PtStack<true>::type;
-        Stk s = PtStack<true>::make(stk, L);
-        Tracer4<ORDERED, ANY, STATS, Stk> tr;
+    if constexpr (WIDE > 0) {
+        using Stk = typename PtStack<WIDE>::type;
+        Stk s = PtStack<WIDE>::make(stk, L);
+        typename PtTracer<WIDE, ORDERED, ANY, STATS, Stk>::type tr;
         tr.begin(S, tv, o, d, mint, maxt, st);
 #pragma unroll 1
         while (!tr.done) tr.step(tv, s, st);
@@ -359,14 +365,14 @@ __device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S,
 #ifndef NH_PT_WAVES
 #define NH_PT_WAVES 5
 #endif
-template <int DEPTH, bool ORDERED, bool ANY, bool STATS, bool WIDE>
+template <int DEPTH, bool ORDERED, bool ANY, bool STATS, int WIDE>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES))) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[kRingEntries * 128];
-    __shared__ float4 s_top[WIDE ? kTopNodes * kWideF4 : 1];  // the top of the 4-wide tree (nodes 0 .. n_top-1)
+    __shared__ float4 s_top[WIDE ? kTopNodes * kWideF4 : 1];  // the top of the wide tree (nodes 0 .. n_top-1)
     const DScene &S = *Sp;
-    const int n_top = WIDE ? min(tv.n_top, kTopNodes) : 0;
-    if constexpr (WIDE) {
-        for (int i = threadIdx.x; i < n_top * kWideF4; i += 128) s_top[i] = tv.wnodes[i];
+    const int n_top = WIDE ? min(tv.n_top, kTopNodes * kWideF4 / wide_f4<WIDE>()) : 0;
+    if constexpr (WIDE > 0) {
+        for (int i = threadIdx.x; i < n_top * wide_f4<WIDE>(); i += 128) s_top[i] = tv.wnodes[i];
         __syncthreads();
     }
     const QView qv = queue_view(L.cnt_in + (ANY ? kCountGroup : 0));
@@ -425,7 +431,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
         }
         if (!__any(slot >= 0)) break;
         if (slot >= 0) {
-            if constexpr (WIDE) {
+            if constexpr (WIDE > 0) {
                 if (!tr.done) tr.step(tv, my_stk, st, s_top, n_top);
             } else {
                 if (!tr.done) tr.step(tv, my_stk, st);
@@ -449,26 +455,26 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES
 // ray changes. A wave takes batches from the closest-hit segments first (the longer queries) and then from the
 // any-hit segments, so the launch has one tail (its slowest rays) where two launches had two, and an XCD whose
 // closest-hit work is done moves on to shadow rays while others finish.
-template <bool ORDERED, bool STATS>
+template <bool ORDERED, bool STATS, int WIDE = 4>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES))) void wf_trace_pt2(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[kRingEntries * 128];
-    __shared__ float4 s_top[kTopNodes * kWideF4];  // the top of the 4-wide tree (nodes 0 .. n_top-1)
+    __shared__ float4 s_top[kTopNodes * kWideF4];  // the top of the wide tree (nodes 0 .. n_top-1)
     const DScene &S = *Sp;
-    const int n_top = min(tv.n_top, kTopNodes);
-    for (int i = threadIdx.x; i < n_top * kWideF4; i += 128) s_top[i] = tv.wnodes[i];
+    const int n_top = min(tv.n_top, kTopNodes * kWideF4 / wide_f4<WIDE>());
+    for (int i = threadIdx.x; i < n_top * wide_f4<WIDE>(); i += 128) s_top[i] = tv.wnodes[i];
     __syncthreads();
     const QView qe = queue_view(L.cnt_in), qs = queue_view(L.cnt_in + kCountGroup);
     unsigned *fetch_e = L.cnt_in + 2 * kCountGroup, *fetch_s = L.cnt_in + 3 * kCountGroup;
     const WfBuf &B = L.st.buf[L.in_q];
     const int lane = threadIdx.x & 63;
-    using Stk = typename PtStack<true>::type;
-    Stk my_stk = PtStack<true>::make(stk, L);
+    using Stk = typename PtStack<WIDE>::type;
+    Stk my_stk = PtStack<WIDE>::make(stk, L);
     // segments 0-7: closest-hit queue, 8-15: any-hit queue; a wave starts on its XCD's segment of each
     int seg = blockIdx.x & (kQueueShards - 1), tried = 0;
     int batch_next = 0, batch_end = 0;  // wave-uniform
     bool batch_any = false;             // wave-uniform: the queue of the current batch
     int slot = -1;                      // this lane's ray (queue slot), -1 = idle
-    Tracer4<ORDERED, false, STATS, Stk, true> tr;
+    typename PtTracer<WIDE, ORDERED, false, STATS, Stk, true>::type tr;
     TravStats st_e{0, 0, 0}, st_s{0, 0, 0};
     unsigned long long q_e = 0, q_s = 0;
     for (;;) {
@@ -1403,7 +1409,7 @@ __global__ __launch_bounds__(256) void wf_pack_rr(WfLaunch L, WfBuf dst, unsigne
 // of a bounce whose extend / any-hit traversals are done and finishes every path in place, one
 // thread per path: shade, then its next closest-hit and shadow traversals, until it terminates --
 // the same operations in the same order as further wavefront bounces.
-template <int DEPTH, bool ORDERED, bool STATS, bool SMALL, bool WIDE>
+template <int DEPTH, bool ORDERED, bool STATS, bool SMALL, int WIDE>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_TAIL_WAVES))) void wf_tail(const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L) {
     __shared__ uint32_t stk[DEPTH * 128];
     extern __shared__ float4 lds_scene[];
@@ -1483,7 +1489,7 @@ static void launch_persistent(int want, hipStream_t st, const DScene *S, const T
 #if NH_WF_HAS_PART(0) || NH_WF_HAS_PART(3)
 template <int DEPTH>
 static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                              bool shadow, bool persistent, bool wide, int bound, hipStream_t st) {
+                              bool shadow, bool persistent, int wide, int bound, hipStream_t st) {
     // the queue length is only known on the device: size the grid from the host's upper bound
     // (the kernels stride over whatever the device count says)
     const int want = std::max(1, (bound + 127) / 128);
@@ -1491,8 +1497,9 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
     if (persistent) {
 #define NH_PT(A, O, T)                                                                               \
     do {                                                                                             \
-        if (wide) launch_persistent<wf_trace_pt<DEPTH, O, A, T, true>>(want, st, S, tv, L);              \
-        else launch_persistent<wf_trace_pt<DEPTH, O, A, T, false>>(want, st, S, tv, L);                  \
+        if (wide == 8) { if constexpr (O) launch_persistent<wf_trace_pt<DEPTH, O, A, T, 8>>(want, st, S, tv, L); } \
+        else if (wide) launch_persistent<wf_trace_pt<DEPTH, O, A, T, 4>>(want, st, S, tv, L);              \
+        else launch_persistent<wf_trace_pt<DEPTH, O, A, T, 0>>(want, st, S, tv, L);                  \
     } while (0)
         if (shadow) {
             if (ordered) { if (stats) NH_PT(true, true, true); else NH_PT(true, true, false); }
@@ -1523,10 +1530,10 @@ static void launch_wf_trace_d(const DScene *S, const Traversal &tv, const WfLaun
 #endif
 
 void launch_wf_trace_deep(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                          bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st);
+                          bool shadow, bool persistent, int wide, int bound, int depth, hipStream_t st);
 #if NH_WF_HAS_PART(0)
 void launch_wf_trace(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool shadow,
-                     bool persistent, bool wide, int bound, int depth, hipStream_t st) {
+                     bool persistent, int wide, int bound, int depth, hipStream_t st) {
     if (depth <= 16) launch_wf_trace_d<16>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
     else if (depth <= 32) launch_wf_trace_d<32>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
     else launch_wf_trace_deep(S, tv, L, ordered, stats, shadow, persistent, wide, bound, depth, st);
@@ -1534,7 +1541,7 @@ void launch_wf_trace(const DScene *S, const Traversal &tv, const WfLaunch &L, bo
 #endif
 #if NH_WF_HAS_PART(3)
 void launch_wf_trace_deep(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                          bool shadow, bool persistent, bool wide, int bound, int depth, hipStream_t st) {
+                          bool shadow, bool persistent, int wide, int bound, int depth, hipStream_t st) {
     if (depth <= 64) launch_wf_trace_d<64>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
     else launch_wf_trace_d<128>(S, tv, L, ordered, stats, shadow, persistent, wide, bound, st);
 }
@@ -1543,32 +1550,38 @@ void launch_wf_trace_deep(const DScene *S, const Traversal &tv, const WfLaunch &
 #if NH_WF_HAS_PART(1)
 template <int DEPTH>
 static void launch_wf_tail_d(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
-                             bool wide, int bound, hipStream_t st) {
+                             int wide, int bound, hipStream_t st) {
     // grid-stride; the wide variant's lanes own spill areas of the persistent grid's size
     const dim3 grid(std::min(std::max(1, (bound + 127) / 128), wide ? kPersistentBlocks : kTraceBlocksMax));
     const bool small = DEPTH == 16 && L.small_nodes + L.small_prims > 0;
     const size_t lds = small ? 16 * (size_t)(L.small_nodes + L.small_prims) + 8 * (size_t)L.small_leaves : 0;
 #define NH_TL2(O, T, SM, W) hipLaunchKernelGGL((wf_tail<DEPTH, O, T, SM, W>), grid, dim3(128), lds, st, S, tv, L)
-#define NH_TL(O, T) { if constexpr (DEPTH == 16) { if (small) NH_TL2(O, T, true, false); \
-                                                   else if (wide) NH_TL2(O, T, false, true); \
-                                                   else NH_TL2(O, T, false, false); } \
-                      else { if (wide) NH_TL2(O, T, false, true); else NH_TL2(O, T, false, false); } }
+#define NH_TLW(O, T) { if (wide == 8) { if constexpr (O) NH_TL2(O, T, false, 8); } \
+                       else if (wide) NH_TL2(O, T, false, 4); else NH_TL2(O, T, false, 0); }
+#define NH_TL(O, T) { if constexpr (DEPTH == 16) { if (small) NH_TL2(O, T, true, 0); else NH_TLW(O, T) } \
+                      else NH_TLW(O, T) }
     if (ordered) { if (stats) NH_TL(true, true) else NH_TL(true, false) }
     else { if (stats) NH_TL(false, true) else NH_TL(false, false) }
 #undef NH_TL2
+#undef NH_TLW
 #undef NH_TL
 }
 
-void launch_wf_trace2(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
-                      hipStream_t st) {
-    // the 4-wide tree is walked near-first only (nh_api.hip uses it for ordered traversals)
+void launch_wf_trace2(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int wide,
+                      int bound, hipStream_t st) {
+    // the wide trees are walked near-first only (nh_api.hip uses them for ordered traversals)
     (void)ordered;
     const int want = std::max(1, (bound + 127) / 128);
+    if (wide == 8) {
+        if (stats) launch_persistent<wf_trace_pt2<true, true, 8>>(want, st, S, tv, L);
+        else launch_persistent<wf_trace_pt2<true, false, 8>>(want, st, S, tv, L);
+        return;
+    }
     if (stats) launch_persistent<wf_trace_pt2<true, true>>(want, st, S, tv, L);
     else launch_persistent<wf_trace_pt2<true, false>>(want, st, S, tv, L);
 }
 
-void launch_wf_tail(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool wide,
+void launch_wf_tail(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int wide,
                     int bound, int depth, hipStream_t st) {
     if (depth <= 16) launch_wf_tail_d<16>(S, tv, L, ordered, stats, wide, bound, st);
     else if (depth <= 32) launch_wf_tail_d<32>(S, tv, L, ordered, stats, wide, bound, st);

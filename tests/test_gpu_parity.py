@@ -96,10 +96,13 @@ def test_trace_parity_cbox(gpu, scene_dir, traversal):
     compare_trace(ctx, orc, *secondary_rays(orc, 20000, 11), traversal)
 
 
-@pytest.mark.parametrize("traversal", TRAVERSALS)
-def test_trace_parity_bumpy_mesh(gpu, tmp_path, traversal):
+@pytest.mark.parametrize("traversal", TRAVERSALS + [pytest.param("wide8", id="wide8")])
+def test_trace_parity_bumpy_mesh(gpu, tmp_path, monkeypatch, traversal):
     xml, ntri = scenegen.bumpy_cbox_xml(str(tmp_path), 200, 100)
     assert ntri > 30000
+    if traversal == "wide8":  # the 8-wide collapse (NH_WIDE8=1, read when the BVH is uploaded)
+        monkeypatch.setenv("NH_WIDE8", "1")
+        traversal = nh.TRAVERSAL_WIDE
     s, b, ctx = setup(xml)
     orc = no.OracleScene(s)
     compare_trace(ctx, orc, *random_rays(20000, -0.6, 1.2, 3), traversal)
@@ -337,7 +340,9 @@ def test_render_parity_black_envmap_mirror(gpu, tmp_path, mode):
                                   "NH_LDS_FRAMES=0", "NH_EMIT_FACES=0",
                                   # the count kernel's handoff: the runtime copy + memset fallback, alone
                                   # and with in-place chunk ends
-                                  "NH_COUNT_KERNEL=0", "NH_COUNT_KERNEL=0,NH_TAIL=0"])
+                                  "NH_COUNT_KERNEL=0", "NH_COUNT_KERNEL=0,NH_TAIL=0",
+                                  # the 8-wide collapse: both-queries launch, split launches, tails
+                                  "NH_WIDE8=1", "NH_WIDE8=1,NH_TRACE2=0", "NH_WIDE8=1,NH_PERSISTENT=1,NH_TAIL=1000000"])
 def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
     """The traversal variants the wavefront picks per scene (persistent ray-fetching traversal for
     deep BVHs over the binary or the 4-wide tree, per-lane traversal, LDS-staged small BVHs) all give
@@ -362,7 +367,9 @@ def test_wavefront_variants_match(gpu, tmp_path, monkeypatch, knob):
         for name, _ in knobs:
             monkeypatch.delenv(name)
         np.testing.assert_array_equal(ref.framebuffer(), ctx.framebuffer())
-        wide = ctx.stats()["node_bytes"] == 128
+        wide = ctx.stats()["node_bytes"] in (128, 256)
+        if wide:
+            assert (ctx.stats()["node_bytes"] == 256) == (dict(knobs).get("NH_WIDE8") == "1")
         env = dict(knobs)
         # the fused bounce kernel runs exactly when the BVH is traversed from LDS, unless NH_FUSED=0
         assert ctx.stats()["fused_bounce"] == int(ctx.stats()["lds_scene"] == 1 and env.get("NH_FUSED") != "0"), xml
@@ -544,10 +551,13 @@ def test_persistent_traversal_deep_tree_spills(gpu, tmp_path, monkeypatch):
         assert out[0][1][k] == out[1][1][k], k
 
 
-def test_wide_traversal_deep_tree(gpu, tmp_path, monkeypatch):
-    """The 4-wide collapse on a deep tree (stack deeper than its 8-entry LDS window, so entries
-    spill): closest and any hit bit-exact against the oracle's binary traversal, and the persistent
+@pytest.mark.parametrize("width", [4, 8])
+def test_wide_traversal_deep_tree(gpu, tmp_path, monkeypatch, width):
+    """The 4-wide (and 8-wide, NH_WIDE8=1) collapse on a deep tree (stack deeper than its 8-entry LDS window, so
+    entries spill): closest and any hit bit-exact against the oracle's binary traversal, and the persistent
     wavefront render over it equals the megakernel's image bit for bit."""
+    if width == 8:
+        monkeypatch.setenv("NH_WIDE8", "1")
     xml, ntri = scenegen.bumpy_cbox_xml(str(tmp_path), 700, 250)
     s = nh.Scene(xml)
     s.set_resolution(40, 32)
@@ -562,7 +572,7 @@ def test_wide_traversal_deep_tree(gpu, tmp_path, monkeypatch):
     monkeypatch.setenv("NH_PERSISTENT", "1")
     ctx.reset_stats()
     ctx.render(0, 4, seed=21, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT, stats=True)
-    assert ctx.stats()["node_bytes"] == 128
+    assert ctx.stats()["node_bytes"] == 32 * width
     assert ctx.stats()["ray_queries"] == q
     np.testing.assert_array_equal(ref, ctx.framebuffer())
 
