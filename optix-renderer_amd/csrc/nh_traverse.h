@@ -25,12 +25,6 @@
 #pragma once
 #include "nh_device.h"
 
-// any-hit queries walk the children farthest first (A/B build -DNH_SHADOW_FAR=1): an occlusion answer does not depend
-// on the visit order, and a shadow ray runs from the light towards the receiver, near which occluders cluster
-#ifndef NH_SHADOW_FAR
-#define NH_SHADOW_FAR 0
-#endif
-
 namespace nhd {
 
 struct Hit {
@@ -492,7 +486,7 @@ NHD bool trace(const Traversal &tv, const DScene &S, F3 o, F3 d, float mint, flo
             node_box_tests(nf, o, d, r, mint, maxt, fin, hl, hr, nl, nr);
             int next;
             if (hl && hr) {
-                const bool right_first = ORDERED && ((ANY && NH_SHADOW_FAR) ? nl < nr : nr < nl);
+                const bool right_first = ORDERED && nr < nl;
                 stk[sp * stride] = ((uint32_t)cur << 1) | (right_first ? 0u : 1u);
                 ++sp;
                 next = right_first ? ref_r : ref_l;
@@ -824,11 +818,6 @@ NHD int wide_first(bool va, float na, bool vb, float nb) {
     return (va & (!vb | !ORDERED | (na <= nb))) ? 1 : 0;
 }
 
-template <bool ORDERED>
-NHD int wide_first_q(bool far, bool va, float na, bool vb, float nb) {
-    return (va & (!vb | !ORDERED | (far ? (na >= nb) : (na <= nb)))) ? 1 : 0;
-}
-
 // Resumable 4-wide traversal (same step protocol as Tracer: one wide node, one primitive or one
 // stack pop per step). Answers: smallest t, ties to the largest leaf-order position k.
 // RT: the query kind is a run-time property of the lane (any_q, set before begin()), so one persistent launch
@@ -944,16 +933,9 @@ struct Tracer4 {
             // Order of the hit children without moving them: rank_i = number of children before i
             // (wide_before: nearer first / slot order on ties, or slot order alone). cIJ (I < J) says
             // child I comes before child J; for two valid children exactly one of the two holds.
-#if NH_SHADOW_FAR
-            const bool far = is_any();
-            const int c01 = wide_first_q<ORDERED>(far, v0, n0, v1, n1), c02 = wide_first_q<ORDERED>(far, v0, n0, v2, n2);
-            const int c03 = wide_first_q<ORDERED>(far, v0, n0, v3, n3), c12 = wide_first_q<ORDERED>(far, v1, n1, v2, n2);
-            const int c13 = wide_first_q<ORDERED>(far, v1, n1, v3, n3), c23 = wide_first_q<ORDERED>(far, v2, n2, v3, n3);
-#else
             const int c01 = wide_first<ORDERED>(v0, n0, v1, n1), c02 = wide_first<ORDERED>(v0, n0, v2, n2);
             const int c03 = wide_first<ORDERED>(v0, n0, v3, n3), c12 = wide_first<ORDERED>(v1, n1, v2, n2);
             const int c13 = wide_first<ORDERED>(v1, n1, v3, n3), c23 = wide_first<ORDERED>(v2, n2, v3, n3);
-#endif
             const int rk0 = 3 - c01 - c02 - c03;
             const int rk1 = c01 + 2 - c12 - c13;
             const int rk2 = c02 + c12 + 1 - c23;
