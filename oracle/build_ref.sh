@@ -43,3 +43,9 @@ if [ -d "$REF/ext/eigen/Eigen" ] && [ -f "$REF/ext/lodepng/src/lodepng.cpp" ]; t
     echo "built $OUT/normalmap_probe_clang"
   fi
 fi
+# Radiance .hdr probe (oracle/hdr_probe.cpp, test infrastructure): the reference's own HDRLoader.h, a self-contained
+# header, on the test's synthetic files
+if [ -f "$REF/include/nori/HDRLoader.h" ]; then
+  g++ -O2 -std=c++17 -ffp-contract=off -I"$REF/include" "$(dirname "$0")/hdr_probe.cpp" -o "$OUT/hdr_probe"
+  echo "built $OUT/hdr_probe"
+fi

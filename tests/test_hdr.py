@@ -5,8 +5,11 @@ HDRLoader.h:28-46) on synthetic files in all three scanline encodings the reader
 (HDRLoader.h:98-131), flat RGBE pixels and the old (1, 1, 1, n) repeat codes with the chained << 8 count
 (HDRLoader.h:49-83) -- including widths outside [8, 0x7fff], where every scanline is read the old way (:89-90), and a
 flat scanline whose first pixel starts with byte 2 but is not a run-length header (:103-108). Rows land in file order
-(:196-203). No reference output exists for these files (no .hdr ships with the reference), so parity is the
-restatement's: unpinned beyond it. Malformed files the reference reads into undefined memory are errors here.
+(:196-203). No .hdr ships with the reference; the reference's own decoder (include/nori/HDRLoader.h, a
+self-contained header) is compiled here into oracle/_ref/hdr_probe (oracle/build_ref.sh), and
+test_hdr_texels_match_reference_hdrloader pins the loader against it bit for bit on well-formed files of every
+encoding (this container only: the GPU box has no reference checkout). Malformed files the reference reads into
+undefined memory are errors here.
 """
 import os
 
@@ -184,3 +187,28 @@ def test_hdr_well_formed_minimal_files(tmp_path):
     for raw, rgbe in cases.items():
         open(os.path.join(d, "sky_8x4.hdr"), "wb").write(raw)
         np.testing.assert_array_equal(env_texels(nh.Scene(xml)), scenegen.rgbe_decode_reference(rgbe))
+
+
+HDR_PROBE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "hdr_probe")
+
+
+@pytest.mark.skipif(not os.path.exists(HDR_PROBE), reason="oracle/_ref/hdr_probe not built (needs /root/reference)")
+@pytest.mark.parametrize("mode", ["rle", "flat", "old"])
+@pytest.mark.parametrize("w,h", [(37, 9), (300, 3), (5, 4), (1, 2), (40000, 2)])
+def test_hdr_texels_match_reference_hdrloader(tmp_path, mode, w, h):
+    """The reference's HDRLoader::load (its own header, compiled into oracle/_ref/hdr_probe) and the product loader
+    give the same texels bit for bit -- every encoding, widths inside and outside [8, 0x7fff] (40000: every scanline
+    read the old way), every exponent."""
+    import subprocess
+    if mode == "rle" and not 8 <= w <= 0x7FFF:
+        pytest.skip("run-length scanlines need 8 <= width <= 0x7fff")
+    rgbe = random_rgbe(h, w, seed=w * 31 + h)
+    xml = envmap_scene(tmp_path, rgbe, mode)
+    mine = env_texels(nh.Scene(xml))
+    out = tmp_path / "ref.bin"
+    subprocess.run([HDR_PROBE, str(tmp_path / "sky.hdr"), str(out)], check=True, timeout=60)
+    raw = np.fromfile(out, np.uint8)
+    W, H = raw[:8].view(np.int32)
+    assert (W, H) == (w, h)
+    ref = raw[8:].view(np.float32).reshape(h, w, 4)
+    np.testing.assert_array_equal(mine.view(np.uint32), ref.view(np.uint32))
