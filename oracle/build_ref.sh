@@ -49,3 +49,8 @@ if [ -f "$REF/include/nori/HDRLoader.h" ]; then
   g++ -O2 -std=c++17 -ffp-contract=off -I"$REF/include" "$(dirname "$0")/hdr_probe.cpp" -o "$OUT/hdr_probe"
   echo "built $OUT/hdr_probe"
 fi
+# The reference's statistical tests (oracle/hypothesis_probe.cpp, test infrastructure): ext/hypothesis/hypothesis.h
+if [ -f "$REF/ext/hypothesis/hypothesis.h" ]; then
+  g++ -O2 -std=c++17 -I"$REF/ext/hypothesis" "$(dirname "$0")/hypothesis_probe.cpp" -o "$OUT/hypothesis_probe"
+  echo "built $OUT/hypothesis_probe"
+fi

@@ -8,6 +8,8 @@
   - microfacet BSDF: scenes/pa3/tests/ttest-microfacet.xml (ttest.cpp:147-190) and
     chi2test-microfacet.xml (src/utils/chi2test.cpp:121-230: 10x20 cos(theta)/phi table,
     5000 samples per cell, pooled cells below 5 expected, Sidak-corrected chi^2 test).
+Where the reference checkout is present, every verdict is also taken from the reference's own test procedures
+(ext/hypothesis/hypothesis.h compiled into oracle/_ref/hypothesis_probe) on the same estimates, and must agree.
 """
 import json
 import math
@@ -78,6 +80,32 @@ def test_per_path_seeding_contract(seed, pixel, sample):
 
 
 # ---------------------------------------------------------------------------------------
+HYP_PROBE = os.path.join(os.path.dirname(no.__file__), "_ref", "hypothesis_probe")
+
+
+def reference_verdicts(requests, tmp_dir):
+    """The reference's hypothesis::students_t_test / chi2_test (oracle/_ref/hypothesis_probe) on the given requests:
+    ("t", mean, var, ref, n, alpha, k) or ("chi2", obs, exp, n, min_exp, alpha, k). None without the probe."""
+    import subprocess
+    import tempfile
+    if not os.path.exists(HYP_PROBE):
+        return None
+    d = tempfile.mkdtemp(dir=tmp_dir)
+    lines = []
+    for i, r in enumerate(requests):
+        if r[0] == "t":
+            lines.append("t " + " ".join(repr(float(x)) if j < 3 or j == 4 else str(int(x)) for j, x in enumerate(r[1:])))
+        else:
+            _, obs, exp, n, min_exp, alpha, k = r
+            f = os.path.join(d, f"c{i}.bin")
+            np.concatenate([np.asarray(obs, np.float64), np.asarray(exp, np.float64)]).tofile(f)
+            lines.append(f"chi2 {f} {len(obs)} {int(n)} {float(min_exp)!r} {float(alpha)!r} {int(k)}")
+    inp, out = os.path.join(d, "in.txt"), os.path.join(d, "out.txt")
+    open(inp, "w").write("\n".join(lines) + "\n")
+    subprocess.run([HYP_PROBE, inp, out], check=True, timeout=120)
+    return [x.strip() == "1" for x in open(out)]
+
+
 def students_t_test(mean, variance, reference, n, alpha, num_tests):
     """hypothesis::students_t_test (ext/hypothesis/hypothesis.h:314-346)."""
     t = abs(mean - reference) * math.sqrt(n / max(variance, 1e-5))
@@ -89,7 +117,7 @@ def students_t_test(mean, variance, reference, n, alpha, num_tests):
 @pytest.mark.parametrize("name", ["pa4/tests/test-furnace.xml", "pa4/tests/test-direct.xml",
                                   "pa3/tests/test-mesh.xml", "pa3/tests/test-mesh-furnace.xml",
                                   "pa1/test-direct.xml"])
-def test_scene_ttests(scene_dir, name):
+def test_scene_ttests(scene_dir, tmp_path, name):
     """pa4: path_mats / path_mis; pa3: direct_ems / direct_mats / direct_mis (5 + 2 scenes each);
     pa1: the point-light `direct` integrator (4 scenes: visible, visible, hidden, all three lights)."""
     path = os.path.join(scene_dir, "scenes", name)
@@ -100,8 +128,11 @@ def test_scene_ttests(scene_dir, name):
         s = nh.Scene(path, i)
         mean, var = no.OracleScene(s).ttest(rng, 100000)
         ok, p = students_t_test(mean, var, ref, 100000, 0.01, len(refs))
-        results.append((i, mean, ref, p, ok))
-    assert all(r[-1] for r in results), results
+        results.append((i, mean, ref, p, ok, var))
+    assert all(r[4] for r in results), results
+    theirs = reference_verdicts([("t", m, v, r, 100000, 0.01, len(refs)) for _, m, r, _, _, v in results], tmp_path)
+    if theirs is not None:  # the reference's own hypothesis.h agrees
+        assert theirs == [r[4] for r in results], (theirs, results)
 
 
 def microfacet_from_xml(node):
@@ -120,18 +151,23 @@ def microfacet_from_xml(node):
     return b
 
 
-def test_microfacet_ttest(scene_dir):
+def test_microfacet_ttest(scene_dir, tmp_path):
     root = ET.parse(os.path.join(scene_dir, "scenes/pa3/tests/ttest-microfacet.xml")).getroot()
     strings = {s.get("name"): s.get("value") for s in root.findall("string")}
     angles = [float(x) for x in strings["angles"].replace(",", " ").split()]
     refs = [float(x) for x in strings["references"].replace(",", " ").split()]
     rng = no.Pcg32()
+    reqs = []
     for bnode in root.findall("bsdf"):
         b = microfacet_from_xml(bnode)
         for angle, ref in zip(angles, refs):
             mean, var = no.ttest_bsdf(b, angle, rng, 100000)
             ok, p = students_t_test(mean, var, ref, 100000, 0.01, len(refs))
             assert ok, (angle, mean, ref, p)
+            reqs.append(("t", mean, var, ref, 100000, 0.01, len(refs)))
+    theirs = reference_verdicts(reqs, tmp_path)
+    if theirs is not None:
+        assert all(theirs), theirs
 
 
 def chi2_test(obs, exp, n, min_exp, alpha, num_tests):
@@ -179,13 +215,14 @@ def expected_frequencies(b, wi, res_t, res_p, n, quad=48):
     return exp
 
 
-def test_microfacet_chi2(scene_dir):
+def test_microfacet_chi2(scene_dir, tmp_path):
     root = ET.parse(os.path.join(scene_dir, "scenes/pa3/tests/chi2test-microfacet.xml")).getroot()
     res_t, res_p, tests_per_bsdf = 10, 20, 5
     n = res_t * res_p * 5000
     bsdfs = [microfacet_from_xml(b) for b in root.findall("bsdf")]
     rng = no.Pcg32()
     passed = 0
+    reqs = []
     for b in bsdfs:
         for _ in range(tests_per_bsdf):
             cos_t = rng.next_float()
@@ -195,7 +232,11 @@ def test_microfacet_chi2(scene_dir):
             obs = no.chi2_histogram(b, wi, rng, n, res_t, res_p)
             exp = expected_frequencies(b, wi, res_t, res_p, n)
             passed += chi2_test(obs, exp, n, 5, 0.01, tests_per_bsdf * len(bsdfs))
+            reqs.append(("chi2", obs, exp, n, 5, 0.01, tests_per_bsdf * len(bsdfs)))
     assert passed == tests_per_bsdf * len(bsdfs), passed
+    theirs = reference_verdicts(reqs, tmp_path)
+    if theirs is not None:
+        assert all(theirs), theirs
 
 
 def test_oracle_arithmetic_matches_reference_eigen(tmp_path):
