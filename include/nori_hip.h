@@ -56,10 +56,12 @@ enum { NH_SHAPE_MESH = 0, NH_SHAPE_SPHERE = 1 };
 enum { NH_BSDF_DIFFUSE = 0, NH_BSDF_MIRROR = 1, NH_BSDF_DIELECTRIC = 2, NH_BSDF_MICROFACET = 3 };
 enum { NH_EMITTER_AREA = 0, NH_EMITTER_POINT = 1, NH_EMITTER_ENVMAP = 2 };
 /* path_mis (src/integrators/path_mis.cpp), path_mats (path_mats.cpp), the single-bounce
- * direct_ems / direct_mats / direct_mis (direct_ems.cpp, direct_mats.cpp, direct_mis.cpp) and the
- * point-light `direct` integrator (direct.cpp, scenes/pa1) */
+ * direct_ems / direct_mats / direct_mis (direct_ems.cpp, direct_mats.cpp, direct_mis.cpp), the
+ * point-light `direct` integrator (direct.cpp, scenes/pa1) and the `normals` integrator of the normal-map scenes
+ * (normals.cpp: |shFrame.toWorld(direction)|, the envmap on a miss) */
 enum { NH_INTEGRATOR_PATH_MIS = 0, NH_INTEGRATOR_PATH_MATS = 1, NH_INTEGRATOR_DIRECT_EMS = 2,
-       NH_INTEGRATOR_DIRECT_MATS = 3, NH_INTEGRATOR_DIRECT_MIS = 4, NH_INTEGRATOR_DIRECT = 5 };
+       NH_INTEGRATOR_DIRECT_MATS = 3, NH_INTEGRATOR_DIRECT_MIS = 4, NH_INTEGRATOR_DIRECT = 5,
+       NH_INTEGRATOR_NORMALS = 6 };
 
 /* One Nori Shape (src/shapes/mesh.cpp, src/shapes/sphere.cpp). Mesh data lives in
  * the scene-wide concatenated arrays at the given offsets. */
@@ -221,6 +223,7 @@ typedef struct nh_scene_desc {
     const nh_texture *textures;
     uint64_t n_texels;            /* RGBA texels of every png texture, 4 floats each */
     const float *texels;
+    float normals_direction[3];   /* NH_INTEGRATOR_NORMALS: its `direction` point [0, 0, 1] (normals.cpp:10-12) */
 } nh_scene_desc;
 
 /* ---- BVH in the reference's own layout (include/nori/bvh.h:127-165) ---- */

@@ -631,9 +631,10 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     }
     S.n_emitters = (int)d->n_emitters;
     S.nee_finite = nee_finite(d) ? 1 : 0;
-    if (d->integrator < NH_INTEGRATOR_PATH_MIS || d->integrator > NH_INTEGRATOR_DIRECT)
+    if (d->integrator < NH_INTEGRATOR_PATH_MIS || d->integrator > NH_INTEGRATOR_NORMALS)
         return fail(c, "unknown integrator"), NH_ERR_INVALID;
     S.integrator = d->integrator;
+    for (int i = 0; i < 3; ++i) S.ndir[i] = d->normals_direction[i];
     std::memcpy(S.s2c, d->camera.sample_to_camera, sizeof(S.s2c));
     std::memcpy(S.c2w, d->camera.camera_to_world, sizeof(S.c2w));
     {  // camera_ray's origin for a (0, 0, 0) local origin (nh_shade.h): the same operations in the same order

@@ -220,7 +220,8 @@ struct DScene {
     const DEmitter *emitters;
     const float *emitter_cdf;
     int n_emitters;
-    int integrator;  // 0 path_mis, 1 path_mats
+    int integrator;  // 0 path_mis, 1 path_mats, 2-5 the direct integrators, 6 normals
+    float ndir[3];   // normals: its `direction`
     const float *V, *N, *UV, *T, *BT;
     const uint32_t *F;
     const float *area_cdf;

@@ -408,6 +408,21 @@ __device__ F3 li_direct_simple(const DScene &S, const Traversal &tv, Rng &rng, F
     return result;
 }
 
+// NormalIntegrator::Li (src/integrators/normals.cpp:15-33): the shading frame of the first hit, as
+// |shFrame.toWorld(direction)| (Frame::toWorld = s x + t y + n z); a miss sees the envmap (EnvMap::eval, wi = ray.d)
+template <int DEPTH, bool ORDERED, bool STATS>
+__device__ F3 li_normals(const DScene &S, const Traversal &tv, F3 o, F3 d, float mint, float maxt, uint32_t *stk,
+                         int stride, TravStats &st, uint32_t &queries) {
+    Hit h;
+    if (STATS) queries++;
+    if (!trace<DEPTH, ORDERED, false, STATS>(tv, S, o, d, mint, maxt, h, stk, stride, st))
+        return S.envmap >= 0 ? env_eval(S, d) : f3(0, 0, 0);
+    Its its;
+    hit_info(S, tv, h, o, d, its);
+    const F3 n = to_world(its.sh, f3(S.ndir[0], S.ndir[1], S.ndir[2]));
+    return f3(fabsf(n.x), fabsf(n.y), fabsf(n.z));
+}
+
 template <int BLOCK, int DEPTH, bool ORDERED, bool STATS, int MINW>
 __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__restrict__ Sp, Traversal tv, PathLaunch L) {
     __shared__ uint32_t stk[DEPTH * BLOCK];
@@ -436,6 +451,7 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
             case 3: li = li_direct_mats<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
             case 4: li = li_direct_mis<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
             case 5: li = li_direct_simple<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
+            case 6: li = li_normals<DEPTH, ORDERED, STATS>(S, tv, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
             default: li = li_path_mis<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
         }
         const size_t r = (size_t)k * L.n_list + i;

@@ -1177,6 +1177,10 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     return true;
 }
 
+// survivors of an unsorted bounce appended per wave instead of per workgroup (A/B build -DNH_BOUNCE_WAVE_APPEND=1)
+#ifndef NH_BOUNCE_WAVE_APPEND
+#define NH_BOUNCE_WAVE_APPEND 0
+#endif
 // threads per wf_bounce_rr workgroup (A/B builds: -DNH_BOUNCE_TB=128)
 #ifndef NH_BOUNCE_TB
 #define NH_BOUNCE_TB 256
@@ -1220,6 +1224,26 @@ __global__ __launch_bounds__(NH_BOUNCE_TB, NH_BOUNCE_WAVES) void wf_bounce_rr(co
         if constexpr (STATS) t_ph = clock64();
     }
     int rank = 0;  // survivors ranked by the material class of their hit (sorted queue) or in lane order
+#if NH_BOUNCE_WAVE_APPEND
+    if constexpr (!SORT) {
+        // unsorted queue: each wave appends its survivors to the shard counter itself -- no workgroup barrier, so a
+        // wave whose paths are done stores and retires without waiting for the workgroup's slowest wave
+        rank = wave_append(&L.cnt_out[shard * kCountStride], cont);
+        if (cont) store_post_head(L.st.buf[1 - L.in_q], shard * L.seg_cap + rank, v, h);
+        if (STATS) {
+            if (q < qv.n) c_store = clock64() - t_ph;
+            flush_trav_stats(stat_shard(L.counters), q_e, st_e);
+            flush_trav_stats(stat_shard(L.counters) + kStatAny, q_s, st_s);
+            unsigned long long *dst = stat_shard(L.counters) + kStatBounceClk;
+            for (int j = 0; j < 7; ++j) {
+                unsigned long long x = j == 0 ? c_load : j < 5 ? clk.c[j - 1] : j == 5 ? c_store : clk.bounces;
+                for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+                if ((threadIdx.x & 63) == 0) atomicAdd(&dst[j], x);
+            }
+        }
+        return;
+    }
+#endif
     if (SORT) {
 #pragma unroll
         for (int c = 0; c < kMatClasses; ++c) {

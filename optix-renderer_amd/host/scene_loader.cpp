@@ -216,6 +216,7 @@ struct SceneData {
     nh_camera camera{};
     nh_filter filter{};
     int32_t integrator = NH_INTEGRATOR_PATH_MIS;
+    float normals_dir[3] = {0.f, 0.f, 1.f};  // NormalIntegrator's `direction`
     int32_t sample_count = 1;
     std::vector<nh_shape> shapes;
     std::vector<nh_bsdf> bsdfs;
@@ -867,6 +868,11 @@ void build_scene(const Obj &scene, const std::string &base_dir, SceneData &sd) {
             else if (ch.type == "direct_mats") sd.integrator = NH_INTEGRATOR_DIRECT_MATS;
             else if (ch.type == "direct_mis") sd.integrator = NH_INTEGRATOR_DIRECT_MIS;
             else if (ch.type == "direct") sd.integrator = NH_INTEGRATOR_DIRECT;
+            else if (ch.type == "normals") {  // NormalIntegrator (normals.cpp:10-12)
+                sd.integrator = NH_INTEGRATOR_NORMALS;
+                const V3 dir = ch.props.get_point("direction", v3(0, 0, 1));
+                sd.normals_dir[0] = dir.x; sd.normals_dir[1] = dir.y; sd.normals_dir[2] = dir.z;
+            }
             else throw SceneError("integrator \"" + ch.type + "\" is not supported by the HIP path");
         } else if (ch.tag == "camera") {
             if (have_camera) throw SceneError("there can only be one camera per scene");
@@ -1079,6 +1085,7 @@ void fill_desc(const SceneData &sd, nh_scene_desc *d) {
     d->textures = sd.textures.data();
     d->n_texels = sd.texels.size() / 4;
     d->texels = sd.texels.data();
+    for (int i = 0; i < 3; ++i) d->normals_direction[i] = sd.normals_dir[i];
     if (sd.envmap >= 0) {
         d->env = sd.env;
         d->env.rgba = sd.env_rgba.data();
@@ -1183,7 +1190,7 @@ int nh_texture_decode(const uint8_t *rgba8, uint64_t n, int32_t srgb, float *out
 }
 
 int nh_scene_set_integrator(nh_scene *scene, int32_t integrator) {
-    if (!scene || integrator < NH_INTEGRATOR_PATH_MIS || integrator > NH_INTEGRATOR_DIRECT) {
+    if (!scene || integrator < NH_INTEGRATOR_PATH_MIS || integrator > NH_INTEGRATOR_NORMALS) {
         nh::set_host_error("invalid integrator");
         return NH_ERR_INVALID;
     }

@@ -33,6 +33,7 @@ BSDF_DIFFUSE, BSDF_MIRROR, BSDF_DIELECTRIC, BSDF_MICROFACET = 0, 1, 2, 3
 EMITTER_AREA, EMITTER_POINT, EMITTER_ENVMAP = 0, 1, 2
 INTEGRATOR_PATH_MIS, INTEGRATOR_PATH_MATS, INTEGRATOR_DIRECT_EMS, INTEGRATOR_DIRECT_MATS, INTEGRATOR_DIRECT_MIS = 0, 1, 2, 3, 4
 INTEGRATOR_DIRECT = 5  # the point-light `direct` integrator of scenes/pa1 (direct.cpp)
+INTEGRATOR_NORMALS = 6  # the `normals` integrator of the normal-map scenes (normals.cpp)
 MODE_MEGAKERNEL, MODE_WAVEFRONT = 0, 1
 TRAVERSAL_REFERENCE, TRAVERSAL_ORDERED, TRAVERSAL_WIDE = 0, 1, 2
 DENOISER_NONE, DENOISER_SIMPLE = 0, 1
@@ -116,7 +117,8 @@ class nh_scene_desc(C.Structure):
                 ("emitter_cdf", _fp), ("envmap", _i32), ("n_vertices", _u32), ("V", _fp), ("N", _fp),
                 ("UV", _fp), ("T", _fp), ("BT", _fp), ("n_faces", _u32), ("F", _u32p), ("n_area_cdf", _u32),
                 ("area_cdf", _fp), ("env", nh_envmap), ("denoiser", nh_denoiser), ("n_textures", _u32),
-                ("textures", C.POINTER(nh_texture)), ("n_texels", C.c_uint64), ("texels", _fp)]
+                ("textures", C.POINTER(nh_texture)), ("n_texels", C.c_uint64), ("texels", _fp),
+                ("normals_direction", _f * 3)]
 
 
 class nh_bvh_node(C.Structure):

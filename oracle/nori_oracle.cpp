@@ -418,6 +418,7 @@ struct no_scene {
     nh_camera cam;
     nh_filter filter;
     int integrator;
+    float normals_dir[3];
     std::vector<nh_shape> shapes;
     std::vector<nh_bsdf> bsdfs;
     std::vector<nh_emitter> emitters;
@@ -1106,6 +1107,14 @@ V3 li_direct(const no_scene &s, Sampler &smp, const Ray &ray) {
     return result;
 }
 
+// NormalIntegrator::Li (normals.cpp:15-33): |shFrame.toWorld(direction)| at the first hit, the envmap on a miss
+V3 li_normals(const no_scene &s, const Ray &ray) {
+    Its its;
+    if (!bvh_intersect(s, ray, its, false)) return s.envmap >= 0 ? env_eval(s, ray.d) : mk(0, 0, 0);
+    const V3 n = its.sh.to_world(mk(s.normals_dir[0], s.normals_dir[1], s.normals_dir[2]));
+    return mk(std::fabs(n.x), std::fabs(n.y), std::fabs(n.z));
+}
+
 inline bool has_dof(const nh_camera &c) { return c.lens_radius > kEps; }  // perspective.cpp:114
 
 // PerspectiveCamera::sampleRay (perspective.cpp:97-141). lens: the two floats the static camera sampler returns
@@ -1161,6 +1170,7 @@ V3 li(const no_scene &s, Sampler &smp, const Ray &r) {
         case NH_INTEGRATOR_DIRECT_MATS: return li_direct_mats(s, smp, r);
         case NH_INTEGRATOR_DIRECT_MIS: return li_direct_mis(s, smp, r);
         case NH_INTEGRATOR_DIRECT: return li_direct(s, smp, r);
+        case NH_INTEGRATOR_NORMALS: return li_normals(s, r);
         default: return li_path_mis(s, smp, r);
     }
 }
@@ -1266,6 +1276,7 @@ int no_scene_create(const nh_scene_desc *d, no_scene **out) {
     s->cam = d->camera;
     s->filter = d->filter;
     s->integrator = d->integrator;
+    for (int i = 0; i < 3; ++i) s->normals_dir[i] = d->normals_direction[i];
     s->shapes.assign(d->shapes, d->shapes + d->n_shapes);
     s->bsdfs.assign(d->bsdfs, d->bsdfs + d->n_bsdfs);
     if (d->n_textures) s->textures.assign(d->textures, d->textures + d->n_textures);

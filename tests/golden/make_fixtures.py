@@ -21,10 +21,11 @@ Writes (all data, no reference source):
                           table_path_mis.xml, path_mis, thin lens) with their meshes, and its envmap scene
                           scenes/project/envmap/envmap_sphere.xml with the shipped res/wooden_motel.png (binary
                           files stored as {"base64": ...})
-  normalmap_scenes.json.gz the reference's normal-mapped scenes that run an in-scope integrator
-                          (scenes/project/normalmap/normals-identity-direct.xml and normals-primitives-direct.xml,
-                          direct_mis; normals-camel.xml, direct) with their meshes and the shipped normal maps
-                          res/normal-identity.png, normal-primitives.png, normal-test.png (same form)
+  normalmap_scenes.json.gz the reference's normal-mapped scenes (scenes/project/normalmap/: the direct_mis / direct
+                          ones, normals-identity-direct.xml, normals-primitives-direct.xml, normals-camel.xml, and
+                          the `normals` integrator's normals-identity{,-x,-y,-ref}.xml, normals-primitives.xml) with
+                          their meshes and the shipped normal maps res/normal-identity{,-x,-y}.png,
+                          normal-primitives.png, normal-test.png (same form)
 """
 import base64
 import gzip
@@ -104,6 +105,15 @@ NORMALMAP_FILES = [
     "scenes/project/normalmap/normals-identity-direct.xml",
     "scenes/project/normalmap/normals-primitives-direct.xml",
     "scenes/project/normalmap/normals-camel.xml",
+    # the `normals` integrator's views of the same maps (normals.cpp)
+    "scenes/project/normalmap/normals-identity.xml",
+    "scenes/project/normalmap/normals-identity-x.xml",
+    "scenes/project/normalmap/normals-identity-y.xml",
+    "scenes/project/normalmap/normals-identity-ref.xml",
+    "scenes/project/normalmap/normals-primitives.xml",
+    "scenes/project/meshes/sphere.obj",
+    "scenes/project/res/normal-identity-x.png",
+    "scenes/project/res/normal-identity-y.png",
     "scenes/project/meshes/plane.obj",
     "scenes/project/meshes/cube.obj",
     "scenes/project/meshes/cone.obj",

@@ -155,6 +155,12 @@ NORMALMAP_CROPS = [
     ("scenes/project/normalmap/normals-identity-direct.xml", (224, 160, 576, 416)),    # sphere, cube, cone, plane
     ("scenes/project/normalmap/normals-primitives-direct.xml", (224, 160, 576, 416)),
     ("scenes/project/normalmap/normals-camel.xml", (224, 128, 544, 448)),              # the camel head (22.7k tris)
+    # the `normals` integrator (normals.cpp): |shFrame.n| itself, the most direct view of the mapped frames
+    ("scenes/project/normalmap/normals-identity.xml", (224, 160, 576, 416)),
+    ("scenes/project/normalmap/normals-identity-x.xml", (224, 160, 576, 416)),
+    ("scenes/project/normalmap/normals-identity-y.xml", (224, 160, 576, 416)),
+    ("scenes/project/normalmap/normals-primitives.xml", (224, 160, 576, 416)),
+    ("scenes/project/normalmap/normals-identity-ref.xml", (224, 160, 576, 416)),  # no maps: the reference view
 ]
 
 
@@ -163,7 +169,7 @@ NORMALMAP_CROPS = [
 def test_reference_normalmap_scene_crops(gpu, proj_dir, rel, rect, mode):
     s = nh.Scene(os.path.join(proj_dir, rel))
     d = s.desc
-    assert any(d.shapes[i].normal_map for i in range(d.n_shapes))
+    assert any(d.shapes[i].normal_map for i in range(d.n_shapes)) or rel.endswith("-ref.xml")
     blocks = blocks_of(d.camera.width, d.camera.height, *rect)
     g = gpu_render(s, 0, 3, blocks, mode)
     r = no.OracleScene(s).render(0, 3, seed=7, blocks=blocks)

@@ -31,7 +31,11 @@ PROBE = os.path.join(os.path.dirname(no.__file__), "_ref", "normalmap_probe")
 PROBE_CLANG = PROBE + "_clang"
 NORMALMAP_SCENES = ["scenes/project/normalmap/normals-identity-direct.xml",
                     "scenes/project/normalmap/normals-primitives-direct.xml",
-                    "scenes/project/normalmap/normals-camel.xml"]
+                    "scenes/project/normalmap/normals-camel.xml",
+                    "scenes/project/normalmap/normals-identity.xml",
+                    "scenes/project/normalmap/normals-identity-x.xml",
+                    "scenes/project/normalmap/normals-identity-y.xml",
+                    "scenes/project/normalmap/normals-primitives.xml"]
 
 
 @pytest.fixture(scope="module")
@@ -139,7 +143,11 @@ def test_reference_normalmap_scenes_load(proj_dir):
     `<texture name="normal">` becomes a linear (sRGB = false) png texture of intensity 1 on its shape."""
     expect = {"normals-identity-direct.xml": ([1, 2, 3, 4], nh.INTEGRATOR_DIRECT_MIS, (1024, 1024)),
               "normals-primitives-direct.xml": ([1, 0, 2, 0], nh.INTEGRATOR_DIRECT_MIS, (1024, 1024)),
-              "normals-camel.xml": ([1, 0], nh.INTEGRATOR_DIRECT, (200, 200))}
+              "normals-camel.xml": ([1, 0], nh.INTEGRATOR_DIRECT, (200, 200)),
+              "normals-identity.xml": ([1, 2, 3, 4], nh.INTEGRATOR_NORMALS, (1024, 1024)),
+              "normals-identity-x.xml": ([1, 2, 3, 4], nh.INTEGRATOR_NORMALS, (1024, 1024)),
+              "normals-identity-y.xml": ([1, 2, 3, 4], nh.INTEGRATOR_NORMALS, (1024, 1024)),
+              "normals-primitives.xml": ([1, 0, 2, 0], nh.INTEGRATOR_NORMALS, (1024, 1024))}
     for rel in NORMALMAP_SCENES:
         s = nh.Scene(os.path.join(proj_dir, rel))
         d = s.desc
@@ -287,3 +295,17 @@ def test_next2d_argument_order_is_compiler_dependent(tmp_path):
         run_probe(PROBE_CLANG, "order", tmp_path / "c.bin")
         c = np.fromfile(tmp_path / "c.bin", np.float32)
         assert (c[0], c[1]) == (np.float32(a), np.float32(b))
+
+
+def test_normals_integrator_shows_the_mapped_frames(proj_dir):
+    """The `normals` integrator (normals.cpp:15-33) renders |shFrame.toWorld((0, 0, 1))|: the identity map and the
+    x- and y-tilted maps of the reference's scenes give finite images that differ visibly from one another."""
+    def render(name):
+        s = nh.Scene(os.path.join(proj_dir, "scenes/project/normalmap", name))
+        assert s.desc.integrator == nh.INTEGRATOR_NORMALS
+        s.set_resolution(96, 72)
+        return no.OracleScene(s).render(0, 1, seed=2)
+    ident, x, y = render("normals-identity.xml"), render("normals-identity-x.xml"), render("normals-identity-y.xml")
+    for img in (ident, x, y):
+        assert np.isfinite(img).all() and img[..., 3].sum() > 0
+    assert np.abs(x - ident).max() > 0.05 and np.abs(y - ident).max() > 0.05 and np.abs(x - y).max() > 0.05
