@@ -365,8 +365,12 @@ __device__ __forceinline__ bool trace_lane(const Traversal &tv, const DScene &S,
 #ifndef NH_PT_WAVES
 #define NH_PT_WAVES 5
 #endif
+// waves per SIMD of the any-hit instantiations (A/B: -DNH_PT_WAVES_ANY=6)
+#ifndef NH_PT_WAVES_ANY
+#define NH_PT_WAVES_ANY NH_PT_WAVES
+#endif
 template <int DEPTH, bool ORDERED, bool ANY, bool STATS, int WIDE>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(NH_PT_WAVES))) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(ANY ? NH_PT_WAVES_ANY : NH_PT_WAVES))) void wf_trace_pt(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ uint32_t stk[kRingEntries * 128];
     __shared__ float4 s_top[WIDE ? kTopNodes * kWideF4 : 1];  // the top of the wide tree (nodes 0 .. n_top-1)
     const DScene &S = *Sp;
@@ -1177,14 +1181,30 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
     return true;
 }
 
-// survivors of an unsorted bounce appended per wave instead of per workgroup (A/B build -DNH_BOUNCE_WAVE_APPEND=1)
-#ifndef NH_BOUNCE_WAVE_APPEND
-#define NH_BOUNCE_WAVE_APPEND 0
-#endif
 // threads per wf_bounce_rr workgroup (A/B builds: -DNH_BOUNCE_TB=128)
 #ifndef NH_BOUNCE_TB
 #define NH_BOUNCE_TB 256
 #endif
+
+// one queue entry of a RR-ahead bounce: load its path (or, at bounce 0, its camera ray and first hit) and run
+// rr_step; true when the path lives on (v, h: its state to store)
+template <bool ORDERED, bool STATS, bool FULL>
+__device__ __forceinline__ bool bounce_path(const DScene &S, const Traversal &tv, const WfLaunch &L, const QView &qv,
+                                            int q, uint32_t *my_stk, PathV &v, Hit &h, TravStats &st_e,
+                                            TravStats &st_s, unsigned long long &q_e, unsigned long long &q_s,
+                                            TailClocks &clk, unsigned long long &c_load) {
+    const int s = queue_slot(qv.pre, L.seg_cap, q);
+    Its its;
+    bool alive = true;
+    unsigned long long t_ph = 0;
+    if constexpr (STATS) t_ph = clock64();
+    if (L.first) alive = first_vertex<ORDERED, STATS, FULL>(S, tv, L, s, v, h, its, my_stk, NH_BOUNCE_TB, st_e, q_e);
+    else load_post_head<FULL>(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
+    if constexpr (STATS) c_load += clock64() - t_ph;
+    return alive && rr_step<ORDERED, STATS, STATS, 1, FULL>(S, tv, L, v, its, h, my_stk, NH_BOUNCE_TB, st_e, st_s, q_e,
+                                                            q_s, &clk);
+}
+
 template <bool ORDERED, bool STATS, bool SORT, bool FULL = true>
 __global__ __launch_bounds__(NH_BOUNCE_TB, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScene *__restrict__ Sp, Traversal tv_g,
                                                                      WfLaunch L) {
@@ -1211,39 +1231,11 @@ __global__ __launch_bounds__(NH_BOUNCE_TB, NH_BOUNCE_WAVES) void wf_bounce_rr(co
     TailClocks clk;
     unsigned long long c_load = 0, c_store = 0, t_ph = 0;
     if (q < qv.n) {
-        const int s = queue_slot(qv.pre, L.seg_cap, q);
-        Its its;
-        bool alive = true;
-        if constexpr (STATS) t_ph = clock64();
-        if (L.first) alive = first_vertex<ORDERED, STATS, FULL>(S, tv, L, s, v, h, its, my_stk, NH_BOUNCE_TB, st_e, q_e);
-        else load_post_head<FULL>(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
-        if constexpr (STATS) c_load = clock64() - t_ph;
-        if (alive) cont = rr_step<ORDERED, STATS, STATS, 1, FULL>(S, tv, L, v, its, h, my_stk, NH_BOUNCE_TB, st_e, st_s, q_e,
-                                                                  q_s, &clk);
+        cont = bounce_path<ORDERED, STATS, FULL>(S, tv, L, qv, q, my_stk, v, h, st_e, st_s, q_e, q_s, clk, c_load);
         if (cont) cls = prim_material(tv.prims[3 * h.k + 2]);  // a live path's ray has hit something
         if constexpr (STATS) t_ph = clock64();
     }
     int rank = 0;  // survivors ranked by the material class of their hit (sorted queue) or in lane order
-#if NH_BOUNCE_WAVE_APPEND
-    if constexpr (!SORT) {
-        // unsorted queue: each wave appends its survivors to the shard counter itself -- no workgroup barrier, so a
-        // wave whose paths are done stores and retires without waiting for the workgroup's slowest wave
-        rank = wave_append(&L.cnt_out[shard * kCountStride], cont);
-        if (cont) store_post_head(L.st.buf[1 - L.in_q], shard * L.seg_cap + rank, v, h);
-        if (STATS) {
-            if (q < qv.n) c_store = clock64() - t_ph;
-            flush_trav_stats(stat_shard(L.counters), q_e, st_e);
-            flush_trav_stats(stat_shard(L.counters) + kStatAny, q_s, st_s);
-            unsigned long long *dst = stat_shard(L.counters) + kStatBounceClk;
-            for (int j = 0; j < 7; ++j) {
-                unsigned long long x = j == 0 ? c_load : j < 5 ? clk.c[j - 1] : j == 5 ? c_store : clk.bounces;
-                for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-                if ((threadIdx.x & 63) == 0) atomicAdd(&dst[j], x);
-            }
-        }
-        return;
-    }
-#endif
     if (SORT) {
 #pragma unroll
         for (int c = 0; c < kMatClasses; ++c) {
