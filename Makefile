@@ -30,6 +30,11 @@ WF_PARTS := 0 1 2 3
 HIP_OBJ  := $(patsubst $(PKG)/csrc/%.hip,$(OBJDIR)/hip_%.o,$(HIP_SRC)) \
             $(foreach k,$(WF_PARTS),$(OBJDIR)/hip_nh_wavefront_p$(k).o)
 HIP_DEPS := $(wildcard $(PKG)/csrc/*.h) include/nori_hip.h
+# The wavefront kernels build without LLVM's machine-level LICM: it hoists loop invariants out of the traversal, bounce
+# and tail loops into registers for the loop's whole length, which then spill (wf_tail_rr at 4 waves/SIMD: 448 ->
+# 28 B/lane of scratch; wf_tail 256 -> 157 VGPRs; the persistent traversals 96 -> 88). C5 +3.6 %, other configs
+# level; the splat TU keeps it (1 % faster with it). profiles/round6_ab_machine_licm.txt
+WF_FLAGS := -mllvm -disable-machine-licm
 
 LIB      := $(LIBDIR)/libnori_hip.so
 HOSTLIB  := $(LIBDIR)/libnori_host.so
@@ -66,7 +71,7 @@ $(OBJDIR)/host_%.o: $(PKG)/host/%.cpp $(wildcard $(PKG)/host/*.h) include/nori_h
 
 $(OBJDIR)/hip_nh_wavefront_p%.o: $(PKG)/csrc/nh_wavefront.hip $(HIP_DEPS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIP_FLAGS) -DNH_WF_PART=$* -c $< -o $@
+	$(HIPCC) $(HIP_FLAGS) $(WF_FLAGS) -DNH_WF_PART=$* -c $< -o $@
 
 $(OBJDIR)/hip_%.o: $(PKG)/csrc/%.hip $(HIP_DEPS)
 	@mkdir -p $(OBJDIR)
