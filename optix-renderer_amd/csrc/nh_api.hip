@@ -148,7 +148,8 @@ struct nh_ctx {
     size_t rec_cap = 0;  // entries
     int *pixel_list = nullptr, *pixel_map = nullptr, *block_rank = nullptr;
     int *block_ids = nullptr, *block_slot = nullptr;
-    int n_blocks = 0;
+    int *color_slots = nullptr;  // slots of the (bx + by) even blocks, then the odd ones (the pair splat's two launches)
+    int n_blocks = 0, n_color0 = 0;
     float4 *staging = nullptr;
     size_t staging_cap = 0;  // float4 entries
     int n_list = 0, nbx = 0, nby = 0;
@@ -377,6 +378,7 @@ void nh_destroy(nh_ctx *c) {
     (void)hipFree(c->block_rank);
     (void)hipFree(c->block_ids);
     (void)hipFree(c->block_slot);
+    (void)hipFree(c->color_slots);
     (void)hipFree(c->staging);
     (void)hipFree(c->counters);
     (void)hipFree(c->d_scene);
@@ -1301,6 +1303,8 @@ static SplatLaunch make_splat(const nh_ctx *c, const float *rec, uint64_t seed, 
     P.blocks = c->block_ids;
     P.block_slot = c->block_slot;
     P.n_blocks = c->n_blocks;
+    P.color_slots = c->color_slots;
+    P.n_color0 = c->n_color0;
     P.staging = staging;
     return P;
 }
@@ -1903,7 +1907,17 @@ static int ensure_pixel_list(nh_ctx *c, const nh_render_req *q) {
     (void)hipFree(c->pixel_map);
     (void)hipFree(c->block_ids);
     (void)hipFree(c->block_slot);
-    c->pixel_list = c->pixel_map = c->block_ids = c->block_slot = nullptr;
+    (void)hipFree(c->color_slots);
+    c->pixel_list = c->pixel_map = c->block_ids = c->block_slot = c->color_slots = nullptr;
+    std::vector<int> color_slots;
+    for (int col = 0; col < 2; ++col)
+        for (size_t i = 0; i < blocks.size(); ++i)
+            if (((blocks[i] % c->nbx + blocks[i] / c->nbx) & 1) == col) color_slots.push_back((int)i);
+    c->n_color0 = 0;
+    for (int32_t bid : blocks) c->n_color0 += ((bid % c->nbx + bid / c->nbx) & 1) == 0;
+    HIP_TRY(c, hipMalloc(&c->color_slots, std::max<size_t>(color_slots.size(), 1) * sizeof(int)));
+    if (!color_slots.empty())
+        HIP_TRY(c, hipMemcpyAsync(c->color_slots, color_slots.data(), color_slots.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMalloc(&c->block_ids, std::max<size_t>(blocks.size(), 1) * sizeof(int)));
     HIP_TRY(c, hipMalloc(&c->block_slot, slot_map.size() * sizeof(int)));
     if (!blocks.empty())

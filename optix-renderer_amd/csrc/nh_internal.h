@@ -66,6 +66,8 @@ struct SplatLaunch {
     int direct;             // rounds the tab splat added to fb for pixels one block covers (the merge starts them there)
     int persist;            // tab splat: a grid of this many workgroups walks the items (0: one workgroup per item)
     int band;               // staging offsets: stage_off(.., band, ..) (1: the tabulated splat's core + band layout)
+    const int *color_slots; // slots of the blocks with (bx + by) even, then odd: the pair splat's two launches
+    int n_color0;           // how many are even
     int debug;              // timing experiments only (NH_SPLAT_DEBUG, images wrong): bits skip the fused splat's
                             // phase 1 (1), phase 2 (2), record fetch (4), master-border strips (8)
 };

@@ -235,7 +235,13 @@ constexpr int kTabRG = 0, kTabBW = 2, kTabWX = 4, kTabWY = 9, kTabPlanes = 14;
 // choice between the two costs the recomputing kernel 6 % (profiles/round4_session9_10_splat_ab.txt)
 // T: workgroup threads. 256: 6-row strips, 4 phase-1 samples per thread; 512: 3-row strips, 2 samples per thread --
 // the same LDS per workgroup, half the registers per thread, so twice the waves per CU fit (NH_SPLAT_T512)
-template <bool DIRECT, bool JIT = false, int T = 256>
+// PAIR (with DIRECT, all rounds): the pair splat (launch_splat, NH_SPLAT_PAIR). The blocks run in two launches, those
+// with (bx + by) even first. A master pixel two side-by-side blocks cover (the 4-pixel seams) is staged by the even
+// block only; the odd block's workgroup reads that value back per round and adds both blocks' values to the master in
+// spiral order itself, like a pixel only it covers. Pixels of the 4x4 corner squares with three or four covering blocks
+// (or two diagonal ones) are staged by every covering block and finished by nh_corner_merge_kernel. The per-pixel
+// summation order is the merge's: rounds in order, blocks in spiral order within a round.
+template <bool DIRECT, bool JIT = false, int T = 256, bool PAIR = false>
 __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *tab, int slot, int k0, int k1) {
     constexpr int SR = T == 512 ? 3 : kStripRows, NS = 36 / SR, NQ = 1024 / T;
     static_assert(SR * NS == 36 && NQ * T == 1024, "strip tiling");
@@ -311,11 +317,35 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
         }
     }
     const int cx = xt < 4 ? 0 : xt >= 32 ? 2 : 1;  // the column's band: left / none / right
+    // PAIR: the seam pixels this (odd) block finishes: the partner's staged value of round 0 at pof[j] (-1: none), and
+    // whether the partner comes first in spiral order (bit j of pfirst)
+    int pof[SR];
+    unsigned pfirst = 0;
+    const size_t per_round = (size_t)P.n_blocks * (size_t)(36 * stage_pitch(36));
 #pragma unroll
     for (int j = 0; j < SR; ++j) {
         own[j] = false;
+        pof[j] = -1;
         m[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (DIRECT && threadIdx.x < 36 * NS) {
+        if (PAIR && threadIdx.x < 36 * NS) {
+            const int yt = yt0 + j, mx = ox + xt, my = oy + yt;
+            if (mx < mcols && my < mrows && xt < sxb + 4 && yt < syb + 4) {
+                int sl[4];
+                const int nb = covering_blocks(P, mx, my, sl);
+                if (nb == 1) {
+                    own[j] = true;
+                } else if (nb == 2) {
+                    const int ps = sl[0] == slot ? sl[1] : sl[0], pb = P.blocks[ps];
+                    const int pby = pb / P.nbx, pbx = pb - pby * P.nbx;
+                    if (((bx + by) & 1) == 1 && ((pbx + pby) & 1) == 0) {  // a seam, and this block is its odd one
+                        own[j] = true;
+                        pof[j] = ps * (36 * stage_pitch(36)) + stage_off(36, 1, mx - pbx * 32, my - pby * 32);
+                        if (sl[0] == ps) pfirst |= 1u << j;
+                    }
+                }
+                if (own[j]) m[j] = fb4[(size_t)my * mcols + mx];
+            }
+        } else if (DIRECT && threadIdx.x < 36 * NS) {
             const int yt = yt0 + j, mx = ox + xt, my = oy + yt;  // block-array position -> master pixel
             const int cy = yt < 4 ? 0 : yt >= 32 ? 2 : 1;
             // neighbours whose array holds this pixel: the column band's, the row band's and their corner
@@ -358,6 +388,11 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
         }
         __syncthreads();
         if (k + 1 < k1) fetch(k + 1);  // in flight during phase 2
+        float4 pv[SR];  // PAIR: the partner blocks' staged values of round k, in flight during phase 2
+        if (PAIR)
+#pragma unroll
+            for (int j = 0; j < SR; ++j)
+                if (pof[j] >= 0) pv[j] = P.staging[(size_t)k * per_round + pof[j]];
         if (threadIdx.x < 36 * NS) {
             sf2 rg[SR], bw[SR];
 #pragma unroll
@@ -403,11 +438,23 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
             float4 *out = P.staging + ((size_t)k * P.n_blocks + slot) * (size_t)(36 * stage_pitch(36));
 #pragma unroll
             for (int j = 0; j < SR; ++j) {
+                if (PAIR && pof[j] >= 0 && ((pfirst >> j) & 1u)) {  // the partner's value first (spiral order)
+                    m[j].x += pv[j].x;
+                    m[j].y += pv[j].y;
+                    m[j].z += pv[j].z;
+                    m[j].w += pv[j].w;
+                }
                 if (DIRECT && own[j]) {  // round k of a pixel only this block covers: the master, in round order
                     m[j].x += rg[j].x;
                     m[j].y += rg[j].y;
                     m[j].z += bw[j].x;
                     m[j].w += bw[j].y;
+                    if (PAIR && pof[j] >= 0 && !((pfirst >> j) & 1u)) {  // the partner's value second
+                        m[j].x += pv[j].x;
+                        m[j].y += pv[j].y;
+                        m[j].z += pv[j].z;
+                        m[j].w += pv[j].w;
+                    }
                 } else {
                     out[stage_off(36, 1, xt, yt0 + j)] = make_float4(rg[j].x, rg[j].y, bw[j].x, bw[j].y);
                 }
@@ -420,10 +467,20 @@ __device__ __forceinline__ void tab_body(const SplatLaunch &P, float *W, float *
             if (own[j]) fb4[(size_t)(oy + yt0 + j) * mcols + ox + xt] = m[j];
 }
 
-template <bool DIRECT, int ROUNDS = kTabRounds, bool JIT = false, bool PERSIST = false, int T = 256>
+// PAIR: the pair splat's launch of the even blocks (1: their pixels classified as in the one-launch splat -- only they
+// cover it, or staged) or of the odd blocks (2)
+template <bool DIRECT, int ROUNDS = kTabRounds, bool JIT = false, bool PERSIST = false, int T = 256, int PAIR = 0>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 128))) void nh_block_splat_tab_kernel(SplatLaunch P) {
     __shared__ float W[kTabPlanes * kTabPlane];
     __shared__ float tab[33];
+    if (PAIR == 1) {
+        tab_body<true, false, T, false>(P, W, tab, P.color_slots[blockIdx.x], 0, P.n_rounds);
+        return;
+    }
+    if (PAIR == 2) {
+        tab_body<true, false, T, true>(P, W, tab, P.color_slots[P.n_color0 + blockIdx.x], 0, P.n_rounds);
+        return;
+    }
     if (DIRECT) {
         tab_body<true, JIT, T>(P, W, tab, blockIdx.x, 0, P.n_rounds);
         return;
@@ -818,6 +875,61 @@ __global__ __launch_bounds__(256) void nh_merge_kernel(SplatLaunch P) {
     *mp = m;
 }
 
+// The pair splat's last step: master pixels of the interior 4x4 corner squares whose covering blocks are not one
+// side-by-side pair (three or four blocks, or two diagonal ones: every one of them staged its value), summed like
+// nh_merge_kernel's band pixels -- rounds in order, blocks in spiral order within a round. 4 corners per 64-thread
+// workgroup (a few hundred workgroups spread over the CUs), one pixel per thread, eight rounds' loads in flight.
+__global__ __launch_bounds__(64) void nh_corner_merge_kernel(SplatLaunch P) {
+    const int nby = (P.height + 31) >> 5, ncx = P.nbx - 1;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 4);
+    if (c >= ncx * (nby - 1)) return;
+    const int cy = c / ncx + 1, cx = c - (cy - 1) * ncx + 1;
+    const int mx = 32 * cx + (threadIdx.x & 3), my = 32 * cy + ((threadIdx.x >> 2) & 3);
+    int slot[4];
+    const int nb = covering_blocks(P, mx, my, slot);
+    if (nb < 2) return;
+    int off[4], par = 0;
+    for (int q = 0; q < nb; ++q) {
+        const int bid = P.blocks[slot[q]];
+        const int by = bid / P.nbx, bx = bid - by * P.nbx;
+        off[q] = slot[q] * (36 * stage_pitch(36)) + stage_off(36, 1, mx - bx * 32, my - by * 32);
+        par += (bx + by) & 1;
+    }
+    if (nb == 2 && par == 1) return;  // a side-by-side pair: the odd block's workgroup finished it
+    const int mcols = P.width + 4;
+    float4 *mp = reinterpret_cast<float4 *>(P.fb) + (size_t)my * mcols + mx;
+    float4 m = *mp;
+    const size_t per_round = (size_t)P.n_blocks * (size_t)(36 * stage_pitch(36));
+    int k = 0;
+    for (; k + 8 <= P.n_rounds; k += 8) {
+        float4 v[8][4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (q < nb) v[j][q] = P.staging[(size_t)(k + j) * per_round + off[q]];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (q < nb) {
+                    m.x += v[j][q].x;
+                    m.y += v[j][q].y;
+                    m.z += v[j][q].z;
+                    m.w += v[j][q].w;
+                }
+    }
+    for (; k < P.n_rounds; ++k)
+        for (int q = 0; q < nb; ++q) {
+            const float4 v = P.staging[(size_t)k * per_round + off[q]];
+            m.x += v.x;
+            m.y += v.y;
+            m.z += v.z;
+            m.w += v.w;
+        }
+    *mp = m;
+}
+
 // invalid-sample count (ImageBlock::put drops, block.cpp:94-99)
 __global__ __launch_bounds__(256) void nh_count_invalid_kernel(const float *rec, size_t n, unsigned long long *out) {
     size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -884,6 +996,17 @@ void launch_splat(const SplatLaunch &P, hipStream_t st) {
         if (all_direct || tr != 8 || P.jit) Q.persist = 0;  // the persistent grid: default grouping only
         if (Q.persist) g = dim3(std::min<unsigned>((unsigned)Q.persist, g.x * g.y), 1);
         const bool t512 = splat_knob("NH_SPLAT_T512");  // 512-thread workgroups, 3-row strips (0: 256, 6-row)
+        if (t512 && all_direct && !P.jit && splat_knob("NH_SPLAT_PAIR")) {
+            // the pair splat: the even blocks, then the odd ones (which finish the seams), then the corner squares
+            if (P.n_color0 > 0)
+                hipLaunchKernelGGL((nh_block_splat_tab_kernel<true, 8, false, false, 512, 1>), dim3(P.n_color0), dim3(512), 0, st, Q);
+            if (P.n_blocks > P.n_color0)
+                hipLaunchKernelGGL((nh_block_splat_tab_kernel<true, 8, false, false, 512, 2>), dim3(P.n_blocks - P.n_color0),
+                                   dim3(512), 0, st, Q);
+            const int n_corners = (P.nbx - 1) * ((P.height + 31) / 32 - 1);
+            if (n_corners > 0) hipLaunchKernelGGL(nh_corner_merge_kernel, dim3((n_corners + 3) / 4), dim3(64), 0, st, Q);
+            return;
+        }
         if (P.jit) {
             if (all_direct) hipLaunchKernelGGL((nh_block_splat_tab_kernel<true, 8, true>), dim3(P.n_blocks, 1), dim3(256), 0, st, Q);
             else hipLaunchKernelGGL((nh_block_splat_tab_kernel<false, 8, true>), g, dim3(256), 0, st, Q);

@@ -226,7 +226,8 @@ def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, 
     master (NH_SPLAT_DIRECT=0, at 1 / 4 / 8 rounds per workgroup), every workgroup staging (NH_SPLAT_LEAD=0), the jitter read
     from a per-record array instead of recomputed from the path stream (NH_SPLAT_JITTER=stored), a persistent grid of
     3 workgroups walking the items (NH_SPLAT_WGS=3), 256-thread workgroups with 6-row strips instead of the default
-    512 threads with 3-row strips (NH_SPLAT_T512=0, staged and all-direct) -- give the same
+    512 threads with 3-row strips (NH_SPLAT_T512=0, staged and all-direct), the all-direct splat in one launch with every
+    band pixel staged and merged (NH_SPLAT_PAIR=0) instead of the default pair splat -- give the same
     framebuffer bit for bit, and the oracle's: partial blocks and the master border of the last block column / row
     (100x70, 33x31), block subsets whose neighbours are absent (every tile quadrant case), several chunks (1 MiB path
     budget) and both render modes."""
@@ -238,10 +239,10 @@ def test_fused_splat_matches_staged_and_oracle(gpu, tmp_path, monkeypatch, res, 
     d0 = {"NH_SPLAT_DIRECT": "0"}
     variants = ({}, d0, {**d0, "NH_SPLAT_LEAD": "0"}, {**d0, "NH_SPLAT_ROUNDS": "4"}, {**d0, "NH_SPLAT_ROUNDS": "1"},
                 {"NH_SPLAT_FUSED": "1"}, {"NH_SPLAT_JITTER": "stored"}, {**d0, "NH_SPLAT_JITTER": "stored"},
-                {**d0, "NH_SPLAT_WGS": "3"}, {"NH_SPLAT_T512": "0"}, {**d0, "NH_SPLAT_T512": "0"})
+                {**d0, "NH_SPLAT_WGS": "3"}, {"NH_SPLAT_T512": "0"}, {**d0, "NH_SPLAT_T512": "0"}, {"NH_SPLAT_PAIR": "0"})
     for env in variants:
         for name in ("NH_SPLAT_DIRECT", "NH_SPLAT_LEAD", "NH_SPLAT_ROUNDS", "NH_SPLAT_FUSED", "NH_SPLAT_JITTER",
-                     "NH_SPLAT_WGS", "NH_SPLAT_T512"):
+                     "NH_SPLAT_WGS", "NH_SPLAT_T512", "NH_SPLAT_PAIR"):
             monkeypatch.delenv(name, raising=False)
         for name, val in env.items():
             monkeypatch.setenv(name, val)
