@@ -1,4 +1,4 @@
-"""Multi-rank tile sharding + framebuffer reduce on CPU (gloo, world size 2).
+"""Multi-rank tile sharding + framebuffer reduce on CPU (gloo, world sizes 2 and 4).
 
 Each rank renders its round-robin share of 32x32 blocks (nori_hip.tile_shard, as bench.py
 does per GPU) into a full-size RGBW framebuffer; a sum-reduce to rank 0 must equal the
@@ -36,17 +36,19 @@ def _worker(rank, world, xml, out_path, port):
     dist.destroy_process_group()
 
 
-def test_tile_shard_reduce_world2(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_tile_shard_reduce(tmp_path, world):
     sys.path.insert(0, os.path.join(REPO, "optix-renderer_amd"))
     import nori_hip as nh
     import nori_oracle as no
     import scenegen
     xml = scenegen.cbox_xml(str(tmp_path), "c1", width=100, height=70)
-    shards = [nh.tile_shard(100, 70, 2, r) for r in range(2)]
-    assert sorted(shards[0] + shards[1]) == list(range(4 * 3)) and not set(shards[0]) & set(shards[1])
+    shards = [nh.tile_shard(100, 70, world, r) for r in range(world)]
+    assert sorted(sum(shards, [])) == list(range(4 * 3)) and all(shards)
+    assert sum(len(x) for x in shards) == len(set(sum(shards, [])))
     out = str(tmp_path / "reduced.npy")
-    port = 29500 + os.getpid() % 1000
-    mp.spawn(_worker, args=(2, xml, out, port), nprocs=2, join=True)
+    port = 29500 + (os.getpid() + 7 * world) % 1000
+    mp.spawn(_worker, args=(world, xml, out, port), nprocs=world, join=True)
     reduced = np.load(out)
     full = no.OracleScene(nh.Scene(xml)).render(0, 4, seed=21, threads=4)
     err = np.sqrt(((reduced.astype(np.float64) - full) ** 2).sum() / (full.astype(np.float64) ** 2).sum())
@@ -86,8 +88,10 @@ def test_bench_gpus_n_launches_n_ranks():
 
 
 @pytest.mark.gpu
-def test_bench_two_hip_ranks_reduce_to_one_rank_render(tmp_path, gpu):
-    """bench.py --gpus 2: both ranks render their tile shard with the HIP path (gloo reduce, both on GPU 0);
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_hip_ranks_reduce_to_one_rank_render(tmp_path, gpu, world):
+    """bench.py --gpus 2 / 8: every rank renders its tile shard with the HIP path (gloo reduce, all on GPU 0: the
+    driver's 8-rank launch rehearsed on one card);
     the reduced framebuffer equals one HIP render of the whole image over the same sample range
     (src/utils/render.cpp:281-347 semantics: the samples of a block do not depend on who renders it), up to
     fp32 summation order where block footprints overlap."""
@@ -95,18 +99,18 @@ def test_bench_two_hip_ranks_reduce_to_one_rank_render(tmp_path, gpu):
     import nori_hip as nh
     import scenegen
     out = str(tmp_path / "reduced.npy")
-    line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--config", "c2", "--width", "160", "--height", "96",
-                   "--rounds", "2", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-denoise",
+    line = _bench(["--gpus", str(world), "--dist-backend", "gloo", "--config", "c2", "--width", "160", "--height",
+                   "96", "--rounds", "2", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-denoise",
                    "--traversal-1m-steps", "0", "--roofline-steps", "0", "--strong-spp", "0", "--no-extras",
                    "--dump-framebuffer", out])
-    assert line["n_gpus"] == 2 and line["value"] > 0
-    check_rank_breakdown(line["ranks"], line["ms_per_step"] * line["steps"] / 1e3)
+    assert line["n_gpus"] == world and line["value"] > 0
+    check_rank_breakdown(line["ranks"], line["ms_per_step"] * line["steps"] / 1e3, world)
     reduced = np.load(out).astype(np.float64)
     xml = scenegen.cbox_xml(str(tmp_path), "c2", width=160, height=96)
     s = nh.Scene(xml)
     ctx = nh.Context(0)
     ctx.upload(s, nh.Bvh(s))
-    R = 2 * 2  # --rounds x world: each rank's weak-scaling step
+    R = 2 * world  # --rounds x world: each rank's weak-scaling step
     ctx.render(0, 2 * R, seed=1234, traversal=nh.TRAVERSAL_ORDERED, clear=True, mode=nh.MODE_WAVEFRONT)
     full = ctx.framebuffer().astype(np.float64)
     ctx.close()
@@ -115,8 +119,9 @@ def test_bench_two_hip_ranks_reduce_to_one_rank_render(tmp_path, gpu):
 
 
 @pytest.mark.gpu
-def test_bench_two_hip_ranks_strong_scaling_equals_one_rank_render(tmp_path, gpu):
-    """bench.py --gpus 2 --scaling strong: a fixed image (the mirror + dielectric Cornell box, C4's scene at test
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_hip_ranks_strong_scaling_equals_one_rank_render(tmp_path, gpu, world):
+    """bench.py --gpus 2 / 4 --scaling strong (every rank a HIP context on GPU 0, gloo reduce): a fixed image (the mirror + dielectric Cornell box, C4's scene at test
     size) whose --rounds x --steps spp are split over the ranks by blocks; the reduced framebuffer equals one HIP
     render of the whole image over the same samples (render.cpp:281-347: the sample budget of a block does not
     depend on the rank that renders it), up to fp32 summation order where block footprints overlap. Also runs the
@@ -125,15 +130,15 @@ def test_bench_two_hip_ranks_strong_scaling_equals_one_rank_render(tmp_path, gpu
     import nori_hip as nh
     import scenegen
     out = str(tmp_path / "reduced.npy")
-    line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--scaling", "strong", "--config", "c1", "--width", "160",
-                   "--height", "96", "--rounds", "3", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-denoise",
+    line = _bench(["--gpus", str(world), "--dist-backend", "gloo", "--scaling", "strong", "--config", "c1", "--width",
+                   "160", "--height", "96", "--rounds", "3", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-denoise",
                    "--traversal-1m-steps", "0", "--roofline-steps", "0", "--strong-spp", "2", "--no-extras",
                    "--dump-framebuffer", out])
-    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["config"]["spp"] == 6
+    assert line["n_gpus"] == world and line["scaling"] == "strong" and line["config"]["spp"] == 6
     sc = line["strong_c4"]
-    assert sc["n_gpus"] == 2 and sc["spp"] == 2 and sc["msamples_s"] > 0
-    check_rank_breakdown(line["ranks"], line["ms_per_step"] * line["steps"] / 1e3)
-    check_rank_breakdown(sc["ranks"], sc["ms"] / 1e3)
+    assert sc["n_gpus"] == world and sc["spp"] == 2 and sc["msamples_s"] > 0
+    check_rank_breakdown(line["ranks"], line["ms_per_step"] * line["steps"] / 1e3, world)
+    check_rank_breakdown(sc["ranks"], sc["ms"] / 1e3, world)
     reduced = np.load(out).astype(np.float64)
     xml = scenegen.cbox_xml(str(tmp_path), "c1", width=160, height=96)
     s = nh.Scene(xml)
