@@ -149,3 +149,48 @@ def test_bench_hip_ranks_strong_scaling_equals_one_rank_render(tmp_path, gpu, wo
     ctx.close()
     err = np.sqrt(((reduced - full) ** 2).sum() / (full ** 2).sum())
     assert err < 1e-6, err
+
+
+_RCCL_ONE_RANK = r'''
+import os, sys, types
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["NH_REPO"])
+import bench
+import nori_hip as nh
+import scenegen
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ["NH_PORT"], RANK="0", WORLD_SIZE="1")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+xml = scenegen.cbox_xml(os.environ["NH_TMP"], "c2", width=96, height=64)
+s = nh.Scene(xml)
+ctx = nh.Context(0)
+ctx.upload(s, nh.Bvh(s))
+ctx.render(0, 4, seed=5, clear=True)
+before = ctx.framebuffer().copy()
+args = types.SimpleNamespace(dist_backend="nccl")
+assert bench.reduce_framebuffer(ctx, dist, args, 0, 0) is None  # RCCL: in place on the device framebuffer
+after = ctx.framebuffer()
+rk = bench.rank_breakdown(dist, args, 0, 0.25, 0.5, 3)
+mx = bench.max_over_ranks(1.5, dist, args, 0)
+dist.destroy_process_group()
+assert np.array_equal(before, after), "a one-rank sum-reduce must leave the framebuffer as it is"
+assert rk["total_s"] == [0.75] and rk["chunks"] == [3] and mx == 1.5, (rk, mx)
+print("rccl-one-rank ok", float(np.abs(after).sum()))
+'''
+
+
+@pytest.mark.gpu
+def test_bench_rccl_collectives_one_rank(tmp_path, gpu):
+    """bench.py's RCCL legs on the GPU with a one-rank NCCL (= RCCL) process group: the in-place dist.reduce of the
+    wrapped device framebuffer (reduce_framebuffer), the all_gather of the rank breakdown and the all_reduce MAX of
+    the step time -- the same calls an N-rank run makes, executed by RCCL on this box's single card."""
+    import subprocess
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", NH_REPO=REPO, NH_TMP=str(tmp_path),
+               NH_PORT=str(29700 + os.getpid() % 200),
+               PYTHONPATH=os.pathsep.join([REPO, os.path.join(REPO, "optix-renderer_amd")]))
+    p = subprocess.run([sys.executable, "-c", _RCCL_ONE_RANK], capture_output=True, text=True, timeout=240, env=env,
+                       cwd=REPO)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert "rccl-one-rank ok" in p.stdout
