@@ -142,6 +142,7 @@ struct nh_ctx {
     int n_bsdf_types = 0;              // distinct BSDF types in the scene
     bool specular = false;             // a mirror or dielectric BSDF: long discrete chains, long chunk tails
     bool textured = false;             // a BSDF with an albedo texture
+    bool normal_mapped = false;        // a shape with a normal map (the full bounce / tail bodies' NMAP instantiation)
     float *fb = nullptr;
     size_t fb_floats = 0;
     float *rec = nullptr;  // (r, g, b) per sample
@@ -691,7 +692,9 @@ int nh_upload_scene(nh_ctx *c, const nh_scene_desc *d) {
     // any BSDF with an albedo texture or shape with a normal map (wf_bounce_rr's lean instantiation has no lookup)
     c->textured = false;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) c->textured = c->textured || d->bsdfs[i].albedo_texture != 0;
-    for (uint32_t i = 0; i < d->n_shapes; ++i) c->textured = c->textured || d->shapes[i].normal_map != 0;
+    c->normal_mapped = false;
+    for (uint32_t i = 0; i < d->n_shapes; ++i) c->normal_mapped = c->normal_mapped || d->shapes[i].normal_map != 0;
+    c->textured = c->textured || c->normal_mapped;
     c->V.assign(d->V, d->V + 3 * nv);
     c->F.assign(d->F, d->F + 3 * (size_t)d->n_faces);
     c->width = d->camera.width;
@@ -1529,7 +1532,7 @@ static int pool_handoff(nh_ctx *c, WfPool &p, WfPool &T, int bound, hipEvent_t *
     HIP_TRY(c, hipEventRecord(ev[1], T.stream));
     HIP_TRY(c, hipEventRecord(ev[2], T.stream));
     nh::launch_wf_tail_rr(c->d_scene, c->tv, L, T.job.ordered, T.job.stats, bound, c->specular,
-                          !c->specular && !c->textured, T.stream);
+                          !c->specular && !c->textured, c->normal_mapped, T.stream);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(ev[3], T.stream));
     T.tail = true;
@@ -1595,7 +1598,7 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
         if (it > 0 && (int64_t)bound <= p.tail_at) {
             if (p.rr)
                 nh::launch_wf_tail_rr(c->d_scene, c->tv, L, ordered, stats, bound, c->specular, !c->specular && !c->textured,
-                                      p.stream);
+                                      c->normal_mapped, p.stream);
             else nh::launch_wf_tail(c->d_scene, c->tv, L, ordered, stats, false, bound, c->depth, p.stream);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev[3], p.stream));
@@ -1604,8 +1607,8 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
             p.state = WfPool::SPLAT;
             return NH_OK;
         }
-        if (p.rr) nh::launch_wf_bounce_rr(c->d_scene, c->tv, L, ordered, stats, p.sorted, !c->specular && !c->textured, bound,
-                                          p.stream);
+        if (p.rr) nh::launch_wf_bounce_rr(c->d_scene, c->tv, L, ordered, stats, p.sorted, !c->specular && !c->textured,
+                                          c->normal_mapped, bound, p.stream);
         else nh::launch_wf_bounce(c->d_scene, c->tv, L, ordered, stats, p.sorted, bound, p.stream);
         HIP_TRY(c, hipGetLastError());
         HIP_TRY(c, hipEventRecord(ev[3], p.stream));
@@ -2055,7 +2058,7 @@ int nh_render(nh_ctx *c, const nh_render_req *q) {
             HIP_TRY(c, hipEventCreate(&ev.d));
             HIP_TRY(c, hipEventRecord(ev.a, c->stream));
             nh::launch_path(c->d_scene, c->tv, L, q->traversal != NH_TRAVERSAL_REFERENCE, q->collect_stats != 0,
-                            c->depth, c->stream);
+                            c->depth, c->integrator == NH_INTEGRATOR_PATH_MIS && !c->normal_mapped, c->stream);
             HIP_TRY(c, hipGetLastError());
             HIP_TRY(c, hipEventRecord(ev.b, c->stream));
             if (q->collect_stats) nh::launch_count_invalid(c->rec, (size_t)L.n_paths, c->counters, c->stream);

@@ -109,8 +109,9 @@ void launch_trace(const nhd::DScene *S, const nhd::Traversal &tv, const RayBatch
 void launch_trace_wide(const nhd::DScene *S, const nhd::Traversal &tv, const RayBatch &rb, const HitBatch &hb, int n,
                        bool any, bool ordered, bool stats, int2 *spill, int spill_depth, unsigned long long *ctr,
                        hipStream_t st, int wide = 4);
+// pm: a path_mis scene without normal maps (the kernel instantiation with only li_path_mis and no normal maps)
 void launch_path(const nhd::DScene *S, const nhd::Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
-                 int depth, hipStream_t st);
+                 int depth, bool pm, hipStream_t st);
 void launch_splat(const SplatLaunch &P, hipStream_t st);
 // false: launch_splat adds the records straight into the master (no per-(round, block) staging buffer)
 bool splat_uses_staging(int border, int reach);
@@ -203,10 +204,12 @@ void launch_wf_bounce(const nhd::DScene *S, const nhd::Traversal &tv, const WfLa
                       bool sort, int bound, hipStream_t st);
 // RR-ahead variants of the fused bounce / tail (nh_wavefront.hip): the stored state is a path after its
 // vertex's Russian roulette
+// lean: the FULL = false body (no mirror / dielectric BSDF, no texture); nmap: the scene has shape normal maps (else the
+// full body is the NMAP = false instantiation)
 void launch_wf_bounce_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
-                         bool lean, int bound, hipStream_t st);
+                         bool lean, bool nmap, int bound, hipStream_t st);
 void launch_wf_tail_rr(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
-                       bool specular, bool lean, hipStream_t st);
+                       bool specular, bool lean, bool nmap, hipStream_t st);
 void launch_wf_tail(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,
                     int wide, int bound, int depth, hipStream_t st);
 // copies the live RR-ahead paths of L's input queue (at most bound) densely into dst, count into dst_counts[0]

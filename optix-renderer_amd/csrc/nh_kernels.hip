@@ -28,7 +28,7 @@ namespace {
 // Everything that does not depend on a traversal result is evaluated before it (pure
 // functions, same operands, same random-number draw order: traversals draw nothing), which
 // keeps the state that is live across traversals small.
-template <int DEPTH, bool ORDERED, bool STATS>
+template <int DEPTH, bool ORDERED, bool STATS, bool NMAP = true>
 __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, F3 d, float mint, float maxt,
                           uint32_t *stk, int stride, TravStats &st, uint32_t &queries) {
     F3 li = f3(0, 0, 0), t = f3(1, 1, 1);
@@ -43,7 +43,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
             break;
         }
         Its its;
-        hit_info(S, tv, h, o, d, its);
+        hit_info<NMAP>(S, tv, h, o, d, its);
         const DShape shape = S.shapes[its.shape];
         const DBsdf bsdf = S.bsdfs[shape.bsdf];
         const F3 alb = bsdf_albedo(S, bsdf, its.u, its.v);
@@ -118,7 +118,7 @@ __device__ F3 li_path_mis(const DScene &S, const Traversal &tv, Rng &rng, F3 o, 
             const int hem = S.shapes[hs_shape].emitter;
             if (hem >= 0) {
                 Its its_s;
-                hit_info(S, tv, h, no, nd, its_s);
+                hit_info<NMAP>(S, tv, h, no, nd, its_s);
                 const DEmitter em2 = S.emitters[hem];
                 const F3 wim = normalized(sub(its_s.p, no));
                 const float pdfmat_ems = emitter_pdf(S, em2, no, its_s.p, its_s.sh.n, wim) / n_lights;
@@ -423,7 +423,10 @@ __device__ F3 li_normals(const DScene &S, const Traversal &tv, F3 o, F3 d, float
     return f3(fabsf(n.x), fabsf(n.y), fabsf(n.z));
 }
 
-template <int BLOCK, int DEPTH, bool ORDERED, bool STATS, int MINW>
+// PM: a path_mis scene without normal maps -- only li_path_mis, normal maps compiled out. The kernel with every
+// integrator (and hit_info's normal-map calls) holds registers and code that cost the path_mis megakernel 6 %
+// (profiles/round6_ab_nmap.txt).
+template <int BLOCK, int DEPTH, bool ORDERED, bool STATS, int MINW, bool PM = false>
 __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__restrict__ Sp, Traversal tv, PathLaunch L) {
     __shared__ uint32_t stk[DEPTH * BLOCK];
     const DScene &S = *Sp;
@@ -445,7 +448,8 @@ __global__ __launch_bounds__(BLOCK, MINW) void nh_path_kernel(const DScene *__re
         float mint, maxt;
         camera_ray(S, spx, spy, o, d, mint, maxt, sample, pix);
         F3 li;
-        switch (S.integrator) {
+        if (PM) li = li_path_mis<DEPTH, ORDERED, STATS, false>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries);
+        else switch (S.integrator) {
             case 1: li = li_path_mats<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
             case 2: li = li_direct_ems<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
             case 3: li = li_direct_mats<DEPTH, ORDERED, STATS>(S, tv, rng, o, d, mint, maxt, stk + threadIdx.x, BLOCK, st, queries); break;
@@ -515,12 +519,15 @@ void launch_trace_wide(const DScene *S, const Traversal &tv, const RayBatch &rb,
 
 template <int BLOCK, int DEPTH, int MINW>
 static void launch_path_w(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
-                          hipStream_t st) {
+                          bool pm, hipStream_t st) {
     dim3 grid((L.n_paths + BLOCK - 1) / BLOCK);
 #define NH_PK(O, T) hipLaunchKernelGGL((nh_path_kernel<BLOCK, DEPTH, O, T, MINW>), grid, dim3(BLOCK), 0, st, S, tv, L)
-    if (ordered) { if (stats) NH_PK(true, true); else NH_PK(true, false); }
+#define NH_PKP(T) hipLaunchKernelGGL((nh_path_kernel<BLOCK, DEPTH, true, T, MINW, true>), grid, dim3(BLOCK), 0, st, S, tv, L)
+    if (ordered && pm) { if (stats) NH_PKP(true); else NH_PKP(false); }
+    else if (ordered) { if (stats) NH_PK(true, true); else NH_PK(true, false); }
     else { if (stats) NH_PK(false, true); else NH_PK(false, false); }
 #undef NH_PK
+#undef NH_PKP
 }
 
 // occupancy target of the megakernel (waves per SIMD the register allocator must allow)
@@ -534,26 +541,26 @@ static int path_min_waves() {
 }
 
 template <int BLOCK, int DEPTH>
-static void launch_path_d(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats,
+static void launch_path_d(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats, bool pm,
                           hipStream_t st) {
     // 4 waves/SIMD measured best (13.7 / 13.8 / 9.8 / 8.3 ms per 16M C2 samples at 1 / 2 / 3 / 4);
     // the 2-wave build stays selectable (NH_PATH_WAVES=2) for register-heavy experiments
     // deep stacks (DEPTH > 32) are LDS-limited below 4 waves anyway: build them for 2
     if constexpr (DEPTH > 32) {
-        launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, st);
+        launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, pm, st);
     } else {
-        if (path_min_waves() == 2) launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, st);
-        else launch_path_w<BLOCK, DEPTH, 4>(S, tv, L, ordered, stats, st);
+        if (path_min_waves() == 2) launch_path_w<BLOCK, DEPTH, 2>(S, tv, L, ordered, stats, pm, st);
+        else launch_path_w<BLOCK, DEPTH, 4>(S, tv, L, ordered, stats, pm, st);
     }
 }
 
 void launch_path(const DScene *S, const Traversal &tv, const PathLaunch &L, bool ordered, bool stats, int depth,
-                 hipStream_t st) {
+                 bool pm, hipStream_t st) {
     if (L.n_paths <= 0) return;
-    if (depth <= 16) launch_path_d<128, 16>(S, tv, L, ordered, stats, st);
-    else if (depth <= 32) launch_path_d<128, 32>(S, tv, L, ordered, stats, st);
-    else if (depth <= 64) launch_path_d<64, 64>(S, tv, L, ordered, stats, st);
-    else launch_path_d<64, 128>(S, tv, L, ordered, stats, st);
+    if (depth <= 16) launch_path_d<128, 16>(S, tv, L, ordered, stats, pm, st);
+    else if (depth <= 32) launch_path_d<128, 32>(S, tv, L, ordered, stats, pm, st);
+    else if (depth <= 64) launch_path_d<64, 64>(S, tv, L, ordered, stats, pm, st);
+    else launch_path_d<64, 128>(S, tv, L, ordered, stats, pm, st);
 }
 
 }  // namespace nh

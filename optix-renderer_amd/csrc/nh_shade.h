@@ -26,8 +26,14 @@ __device__ __noinline__ F3 tex_eval(const DTex *texs, const float4 *texels, int 
 
 // Mesh::setHitInformation (mesh.cpp:141-196) / Sphere::setHitInformation (sphere.cpp:96-124), with the shape's normal
 // map (DShape::tex_uv >> 1) unless NMAP = false (the lean RR-ahead bounce kernel: scenes without textures)
-template <bool NMAP = true>
+#ifdef NH_AB_NO_NMAP  // cost attribution builds only (scripts/build_variant.sh): normal maps compiled out, NOT exact
+#define NH_NMAP_ON false
+#else
+#define NH_NMAP_ON true
+#endif
+template <bool NMAP_ = true>
 __device__ __forceinline__ void hit_info(const DScene &S, const Traversal &tv, const Hit &h, F3 o, F3 d, Its &its) {
+    constexpr bool NMAP = NMAP_ && NH_NMAP_ON;
     const float4 a = tv.prims[3 * h.k], b = tv.prims[3 * h.k + 1];
     const int shape = __float_as_int(b.w);
     const DShape sh = S.shapes[shape];

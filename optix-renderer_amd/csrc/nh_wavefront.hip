@@ -1122,7 +1122,9 @@ struct TailClocks {
 // body of the current vertex, its light sample's any-hit query, the next ray's closest hit, and the next
 // vertex's head; false once the path has ended (its radiance written). G > 1: the path is carried by a G-lane
 // group (every lane the same state and arithmetic; leaf primitives tested cooperatively; one lane writes and counts).
-template <bool ORDERED, bool STATS, bool CLK = false, int G = 1, bool FULL = true>
+// NMAP: hit_info's normal maps (FULL kernels of scenes without normal maps compile them out: the inlined normal-map
+// branches and their tex_eval calls cost C1 / C4 2.5 % when present, profiles/round6_ab_nmap.txt)
+template <bool ORDERED, bool STATS, bool CLK = false, int G = 1, bool FULL = true, bool NMAP = FULL>
 __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, const WfLaunch &L, PathV &v, Its &its,
                                         Hit &h, uint32_t *stk, int stride, TravStats &st_e, TravStats &st_s,
                                         unsigned long long &q_e, unsigned long long &q_s, TailClocks *clk = nullptr) {
@@ -1169,7 +1171,7 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
         t0 = t1;
     }
     v = path_of(L, o);
-    const bool alive = shade_head<FULL>(S, tv, v, h, found, o.pdfmat, its);
+    const bool alive = shade_head<NMAP>(S, tv, v, h, found, o.pdfmat, its);
     if constexpr (CLK) {
         if (lead) cs[3] += clock64() - t0;
         if (lead) ++(G > 1 ? clk->coop_bounces : clk->bounces);
@@ -1188,7 +1190,7 @@ __device__ __forceinline__ bool rr_step(const DScene &S, const Traversal &tv, co
 
 // one queue entry of a RR-ahead bounce: load its path (or, at bounce 0, its camera ray and first hit) and run
 // rr_step; true when the path lives on (v, h: its state to store)
-template <bool ORDERED, bool STATS, bool FULL>
+template <bool ORDERED, bool STATS, bool FULL, bool NMAP = FULL>
 __device__ __forceinline__ bool bounce_path(const DScene &S, const Traversal &tv, const WfLaunch &L, const QView &qv,
                                             int q, uint32_t *my_stk, PathV &v, Hit &h, TravStats &st_e,
                                             TravStats &st_s, unsigned long long &q_e, unsigned long long &q_s,
@@ -1198,14 +1200,14 @@ __device__ __forceinline__ bool bounce_path(const DScene &S, const Traversal &tv
     bool alive = true;
     unsigned long long t_ph = 0;
     if constexpr (STATS) t_ph = clock64();
-    if (L.first) alive = first_vertex<ORDERED, STATS, FULL>(S, tv, L, s, v, h, its, my_stk, NH_BOUNCE_TB, st_e, q_e);
-    else load_post_head<FULL>(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
+    if (L.first) alive = first_vertex<ORDERED, STATS, NMAP>(S, tv, L, s, v, h, its, my_stk, NH_BOUNCE_TB, st_e, q_e);
+    else load_post_head<NMAP>(S, tv, L, L.st.buf[L.in_q], s, v, h, its);
     if constexpr (STATS) c_load += clock64() - t_ph;
-    return alive && rr_step<ORDERED, STATS, STATS, 1, FULL>(S, tv, L, v, its, h, my_stk, NH_BOUNCE_TB, st_e, st_s, q_e,
+    return alive && rr_step<ORDERED, STATS, STATS, 1, FULL, NMAP>(S, tv, L, v, its, h, my_stk, NH_BOUNCE_TB, st_e, st_s, q_e,
                                                             q_s, &clk);
 }
 
-template <bool ORDERED, bool STATS, bool SORT, bool FULL = true>
+template <bool ORDERED, bool STATS, bool SORT, bool FULL = true, bool NMAP = FULL>
 __global__ __launch_bounds__(NH_BOUNCE_TB, NH_BOUNCE_WAVES) void wf_bounce_rr(const DScene *__restrict__ Sp, Traversal tv_g,
                                                                      WfLaunch L) {
     __shared__ uint32_t stk[16 * NH_BOUNCE_TB];
@@ -1231,7 +1233,7 @@ __global__ __launch_bounds__(NH_BOUNCE_TB, NH_BOUNCE_WAVES) void wf_bounce_rr(co
     TailClocks clk;
     unsigned long long c_load = 0, c_store = 0, t_ph = 0;
     if (q < qv.n) {
-        cont = bounce_path<ORDERED, STATS, FULL>(S, tv, L, qv, q, my_stk, v, h, st_e, st_s, q_e, q_s, clk, c_load);
+        cont = bounce_path<ORDERED, STATS, FULL, NMAP>(S, tv, L, qv, q, my_stk, v, h, st_e, st_s, q_e, q_s, clk, c_load);
         if (cont) cls = prim_material(tv.prims[3 * h.k + 2]);  // a live path's ray has hit something
         if constexpr (STATS) t_ph = clock64();
     }
@@ -1282,7 +1284,7 @@ __global__ __launch_bounds__(NH_BOUNCE_TB, NH_BOUNCE_WAVES) void wf_bounce_rr(co
 // the other. Only which lanes run which operation changes; every path's operations and draws are the same.
 constexpr int kTailCoopWords = 48;  // 32-bit words of one handed-over path (PathV, Hit, Its, bounce count)
 // FULL = false: the lean body of wf_bounce_rr<.., FULL = false> (scenes with no mirror / dielectric BSDF and no texture)
-template <bool ORDERED, bool STATS, int TB, int W, bool FULL = true>
+template <bool ORDERED, bool STATS, int TB, int W, bool FULL = true, bool NMAP = FULL>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf_tail_rr(
     const DScene *__restrict__ Sp, Traversal tv_g, WfLaunch L, int coop) {
     __shared__ uint32_t stk[16 * TB];
@@ -1302,13 +1304,13 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
     Hit h;
     Its its;
     unsigned long long nb = 0;  // bounces of this lane's path
-    if (alive) load_post_head<FULL>(S, tv, L, B, queue_slot(qv.pre, L.seg_cap, q), v, h, its);
+    if (alive) load_post_head<NMAP>(S, tv, L, B, queue_slot(qv.pre, L.seg_cap, q), v, h, its);
     const bool can_coop = TB == 64 && coop == 16;
     for (;;) {
         const unsigned long long m = __ballot(alive);
         if (m == 0ull || (can_coop && __popcll(m) <= 4)) break;
         if (alive) {
-            alive = rr_step<ORDERED, STATS, STATS, 1, FULL>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s,
+            alive = rr_step<ORDERED, STATS, STATS, 1, FULL, NMAP>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e, st_s,
                                                             q_e, q_s, &clk);
             ++nb;
         }
@@ -1339,7 +1341,7 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(W))) void wf
             }
             while (__ballot(carry)) {
                 if (carry) {
-                    carry = rr_step<ORDERED, STATS, STATS, 16, FULL>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e,
+                    carry = rr_step<ORDERED, STATS, STATS, 16, FULL, NMAP>(S, tv, L, v, its, h, stk + threadIdx.x, TB, st_e,
                                                                     st_s, q_e, q_s, &clk);
                     ++nb;
                 }
@@ -1626,15 +1628,19 @@ void launch_wf_bounce(const DScene *S, const Traversal &tv, const WfLaunch &L, b
 
 #if NH_WF_HAS_PART(2)
 void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, bool sort,
-                         bool lean, int bound, hipStream_t st) {
+                         bool lean, bool nmap, int bound, hipStream_t st) {
     int blocks = std::max(1, (bound + NH_BOUNCE_TB - 1) / NH_BOUNCE_TB);
     blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
     const size_t lds = 16 * (size_t)rr_lds_f4(L);
 #define NH_FB(O, T, SO) hipLaunchKernelGGL((wf_bounce_rr<O, T, SO>), dim3(blocks), dim3(NH_BOUNCE_TB), lds, st, S, tv, L)
 #define NH_FBN(T, SO) hipLaunchKernelGGL((wf_bounce_rr<true, T, SO, false>), dim3(blocks), dim3(NH_BOUNCE_TB), lds, st, S, tv, L)
+#define NH_FBF(T, SO) hipLaunchKernelGGL((wf_bounce_rr<true, T, SO, true, false>), dim3(blocks), dim3(NH_BOUNCE_TB), lds, st, S, tv, L)
     if (ordered && lean) {  // no discrete BSDF, no texture: wf_bounce_rr<.., FULL = false>
         if (stats) { if (sort) NH_FBN(true, true); else NH_FBN(true, false); }
         else { if (sort) NH_FBN(false, true); else NH_FBN(false, false); }
+    } else if (ordered && !nmap) {  // the full body without normal maps: wf_bounce_rr<.., FULL = true, NMAP = false>
+        if (stats) { if (sort) NH_FBF(true, true); else NH_FBF(true, false); }
+        else { if (sort) NH_FBF(false, true); else NH_FBF(false, false); }
     } else if (ordered) {
         if (stats) { if (sort) NH_FB(true, true, true); else NH_FB(true, true, false); }
         else { if (sort) NH_FB(true, false, true); else NH_FB(true, false, false); }
@@ -1644,10 +1650,11 @@ void launch_wf_bounce_rr(const DScene *S, const Traversal &tv, const WfLaunch &L
     }
 #undef NH_FB
 #undef NH_FBN
+#undef NH_FBF
 }
 
 void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, bool ordered, bool stats, int bound,
-                       bool specular, bool lean, hipStream_t st) {
+                       bool specular, bool lean, bool nmap, hipStream_t st) {
     const char *e = std::getenv("NH_TAIL_WG");  // threads per tail workgroup: 64 (default) or 256
     const int tb = e && std::atoi(e) == 256 ? 256 : 64;
     // register budget, NH_TAIL_RR_WAVES=1|2|4: by default 1 wave/SIMD for scenes with mirror / dielectric BSDFs (their
@@ -1666,6 +1673,8 @@ void launch_wf_tail_rr(const DScene *S, const Traversal &tv, const WfLaunch &L, 
 #define NH_TR(O, T)                                                                                         \
     do {                                                                                                    \
         if (tb == 256) hipLaunchKernelGGL((wf_tail_rr<O, T, 256, 1>), grid, dim3(256), lds, st, S, tv, L, coop); \
+        else if (waves == 1 && !nmap && O)                                                                  \
+            hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 1, true, false>), grid, dim3(64), lds, st, S, tv, L, coop); \
         else if (waves == 1) hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 1>), grid, dim3(64), lds, st, S, tv, L, coop); \
         else if (lean && waves == 2)                                                                        \
             hipLaunchKernelGGL((wf_tail_rr<O, T, 64, 2, false>), grid, dim3(64), lds, st, S, tv, L, coop);  \
