@@ -1643,7 +1643,7 @@ static int pool_enqueue(nh_ctx *c, WfPool &p) {
         p.state = WfPool::SPLAT;
         return NH_OK;
     }
-    nh::launch_wf_shade(c->d_scene, c->tv, L, p.shade_sorted, bound, p.stream);
+    nh::launch_wf_shade(c->d_scene, c->tv, L, p.shade_sorted, c->normal_mapped, bound, p.stream);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipEventRecord(ev[3], p.stream));
     if (int rc_ = count_service(c, p, slot[in ^ 1], slot[in], it)) return rc_;

@@ -197,7 +197,7 @@ void launch_wf_trace2(const nhd::DScene *S, const nhd::Traversal &tv, const WfLa
 // bounce 0 of a thin-lens scene on the persistent kernels: every camera ray (camera_ray with its lens sample) into
 // buf[in_q].ray_o / ray_d, (origin, mint) / (direction, maxt), for the persistent refill to read (WfLaunch::cam_rays)
 void launch_wf_camera_rays(const nhd::DScene *S, const WfLaunch &L, int bound, hipStream_t st);
-void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool sort, int bound,
+void launch_wf_shade(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool sort, bool nmap, int bound,
                      hipStream_t st);
 // fused shade + any-hit + closest-hit bounce for LDS-staged BVHs; sort = material-sorted output queue
 void launch_wf_bounce(const nhd::DScene *S, const nhd::Traversal &tv, const WfLaunch &L, bool ordered, bool stats,

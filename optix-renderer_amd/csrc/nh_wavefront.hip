@@ -782,7 +782,7 @@ __device__ __forceinline__ void write_radiance(const WfLaunch &L, const PathV &v
 // One shade step of the path whose state src holds (slot s of the input queue), hv = the hit of its
 // ray: head + body. Returns whether the path continues (its next state in o); sets nee when it sampled a
 // light (shadow ray in so/sd). A terminated path writes its radiance to its sample record.
-template <class Src>
+template <class Src, bool NMAP = true>
 __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv, const WfLaunch &L, const Src &src,
                                            int s, const float4 hv, PState &o, bool &nee, float4 &so, float4 &sd) {
     float4 ro, rd, li4, th4;
@@ -826,7 +826,7 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
         }
     }
     Its its;
-    if (!shade_head(S, tv, v, h, found, ro.w, its)) {
+    if (!shade_head<NMAP>(S, tv, v, h, found, ro.w, its)) {
         write_radiance(L, v);
         return false;
     }
@@ -846,7 +846,8 @@ __device__ __forceinline__ bool shade_path(const DScene &S, const Traversal &tv,
 #ifndef NH_SHADE_WAVES
 #define NH_SHADE_WAVES 4
 #endif
-template <bool SORT>
+// NMAP: hit_info's normal maps (false for scenes without them, as the full RR-ahead bodies)
+template <bool SORT, bool NMAP = true>
 __global__ __launch_bounds__(256, NH_SHADE_WAVES) void wf_shade(const DScene *__restrict__ Sp, Traversal tv, WfLaunch L) {
     __shared__ unsigned s_n[2], s_base[2];
     __shared__ unsigned s_cls[SORT ? 6 : 1];
@@ -890,7 +891,7 @@ __global__ __launch_bounds__(256, NH_SHADE_WAVES) void wf_shade(const DScene *__
     float4 so, sd;
     if (q < qv.n) {
         const int s = queue_slot(qv.pre, L.seg_cap, q);
-        cont = shade_path(S, tv, L, MemState{B, s}, s, B.hit[s], o, nee, so, sd);
+        cont = shade_path<MemState, NMAP>(S, tv, L, MemState{B, s}, s, B.hit[s], o, nee, so, sd);
     }
     const int le = wave_append(&s_n[0], cont);
     const int ls = wave_append(&s_n[1], cont && nee);
@@ -1705,12 +1706,15 @@ void launch_wf_pack_rr(const WfLaunch &L, const WfBuf &dst, unsigned *dst_counts
     hipLaunchKernelGGL(wf_pack_rr, dim3(std::max(1, (bound + 255) / 256)), dim3(256), 0, st, L, dst, dst_counts);
 }
 
-void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, bool sort, int bound, hipStream_t st) {
+void launch_wf_shade(const DScene *S, const Traversal &tv, const WfLaunch &L, bool sort, bool nmap, int bound,
+                     hipStream_t st) {
     // one 256-entry chunk per workgroup up to the bound; a multiple of kQueueShards (see wf_shade)
     int blocks = std::max(1, (bound + 255) / 256);
     blocks = (blocks + kQueueShards - 1) / kQueueShards * kQueueShards;
-    if (sort) hipLaunchKernelGGL(wf_shade<true>, dim3(blocks), dim3(256), 0, st, S, tv, L);
-    else hipLaunchKernelGGL(wf_shade<false>, dim3(blocks), dim3(256), 0, st, S, tv, L);
+    if (sort && nmap) hipLaunchKernelGGL((wf_shade<true>), dim3(blocks), dim3(256), 0, st, S, tv, L);
+    else if (sort) hipLaunchKernelGGL((wf_shade<true, false>), dim3(blocks), dim3(256), 0, st, S, tv, L);
+    else if (nmap) hipLaunchKernelGGL((wf_shade<false>), dim3(blocks), dim3(256), 0, st, S, tv, L);
+    else hipLaunchKernelGGL((wf_shade<false, false>), dim3(blocks), dim3(256), 0, st, S, tv, L);
 }
 
 #endif
