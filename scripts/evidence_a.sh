@@ -14,7 +14,7 @@ T="TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"
 for cfg in c2 bumpy1m c5 c3; do
   scripts/pmc_groups.sh ${tag}_$cfg "FETCH_SIZE" "WRITE_SIZE" "$S" "$T" -- --config $cfg --strong-spp 0 --no-extras > /dev/null || exit 99
 done
-python3 scripts/pmc_traffic.py gpurun_out/pmc_${tag}_c2 c2_1024x1024_r16_ordered_wavefront/bounce "wf_bounce_rr<true, false, false, false>" || exit 97
+python3 scripts/pmc_traffic.py gpurun_out/pmc_${tag}_c2 c2_1024x1024_r16_ordered_wavefront/bounce "wf_bounce_rr<true, false, false, false, false>" || exit 97
 python3 scripts/pmc_traffic.py gpurun_out/pmc_${tag}_bumpy1m bumpy1m_1024x1024_r16_ordered_wavefront/trace "wf_trace_pt2<true, false, 4>" || exit 97
 python3 scripts/pmc_traffic.py gpurun_out/pmc_${tag}_c5 c5_4096x4096_r16_ordered_wavefront/extend "wf_trace_pt<64, true, false, false, 4>" || exit 97
 python3 scripts/pmc_traffic.py gpurun_out/pmc_${tag}_c5 c5_4096x4096_r16_ordered_wavefront/shadow "wf_trace_pt<64, true, true, false, 4>" || exit 97
